@@ -1,0 +1,149 @@
+/*
+ * nova_crc32c.h -- C-ABI of the MI355X-native batched CRC32C block-checksum
+ * engine (drop-in for NovaLSM's per-SSTable-block checksum path).
+ *
+ * Plain pointers and sizes only (no torch / HIP types in the signatures; a
+ * stream is passed as `void*` holding a hipStream_t, NULL = default stream).
+ * Every entry point below names the reference interface it replaces.
+ *
+ * Conventions
+ *   - Device-batch entry points take DEVICE pointers (hipMalloc'd, or any
+ *     address the GPU can load from) for data, descriptors and outputs, enqueue
+ *     work on `stream` and return without synchronising.  Return 0 on success,
+ *     a hipError_t value (> 0) or a NOVA_E_* code (< 0) on failure.  They never
+ *     fall back to the CPU: with no usable GPU they return an error.
+ *   - Results are bit-identical to looping leveldb::crc32c::Extend
+ *     (util/crc32c.cc:487-588) over the blocks, for any byte alignment of
+ *     starts and lengths.
+ *   - All entry points are reentrant; tables are built once per device
+ *     (thread-safe), and launches keep no mutable global state, so many host
+ *     threads may call concurrently on their own streams
+ *     (the reference's contract, SURVEY.md 8(b) "Threading").
+ */
+#ifndef NOVA_CRC32C_H_
+#define NOVA_CRC32C_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- flags ------------------------------------------------------------- */
+/* Extend each block's CRC by one trailing type byte, NOVA_CRC32C_TYPE(t):
+ * table/table_builder.cc:202-203 `crc = Extend(Value(block, n), &type, 1)`. */
+#define NOVA_CRC32C_APPEND_TYPE 0x1u
+/* Store Mask(crc) (util/crc32c.h:28-31) instead of the raw CRC. */
+#define NOVA_CRC32C_MASK_OUTPUT 0x2u
+/* Trailer writer only: TableBuilder ordering -- trailer[4] = '!' AFTER the
+ * masked CRC was encoded (table/table_builder.cc:204-206).  Without this flag
+ * the StoCWritableFileClient ordering is used ('!' first, then the encode
+ * overwrites it: ltc/stoc_file_client_impl.cpp:717-719). */
+#define NOVA_TRAILER_TB_QUIRK 0x4u
+/* Output the linear ("raw") CRC: zero initial register and no final
+ * complement, i.e. Extend(c, D) == ~(M_|D|(~c) ^ raw(D)).  Used to combine
+ * partial CRCs (nova_crc32c_combine).  Ignores init_or_null. */
+#define NOVA_CRC32C_RAW 0x8u
+#define NOVA_CRC32C_TYPE(t) (((uint32_t)(uint8_t)(t)) << 8)
+
+/* ---- error codes (negative; positive values are hipError_t) ------------ */
+#define NOVA_E_INVAL (-1)    /* bad argument */
+#define NOVA_E_NODEV (-2)    /* no usable gfx950 device / HIP runtime */
+#define NOVA_E_NOMEM (-3)    /* device or pinned allocation failed */
+
+/* ---- scalar API: util/crc32c.h:17-40 ------------------------------------
+ * Single-block calls stay on the host: one 4 KiB block costs ~1.4 us on a
+ * CPU core versus ~5+ us to launch a kernel.  The GPU is
+ * reached through the batch entry points below. */
+/* replaces leveldb::crc32c::Extend, util/crc32c.h:17 / util/crc32c.cc:487 */
+uint32_t nova_crc32c_extend(uint32_t init_crc, const char* data, size_t n);
+/* replaces leveldb::crc32c::Value, util/crc32c.h:20-22 */
+uint32_t nova_crc32c_value(const char* data, size_t n);
+/* replaces leveldb::crc32c::Mask, util/crc32c.h:28-31 */
+uint32_t nova_crc32c_mask(uint32_t crc);
+/* replaces leveldb::crc32c::Unmask, util/crc32c.h:34-37 */
+uint32_t nova_crc32c_unmask(uint32_t masked_crc);
+/* crc32_combine: CRC of A||B from crc(A), crc(B), |B| (host, O(log |B|)).
+ * The GF(2) shift the reference's stride tables encode (util/crc32c.cc:107-453). */
+uint32_t nova_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* ---- plug-in hook: port::AcceleratedCRC32C, port/port_stdcxx.h:179-189 ---
+ * Same contract: returns Extend(crc, buf, size) or 0 meaning "cannot
+ * accelerate" (no device).  `buf` is HOST memory; the buffer is copied to the
+ * GPU, checksummed by the HIP kernels and the result copied back, so it is
+ * worth it only for large buffers.  Passes the reference's self-test
+ * ("TestCRCBuffer" -> 0xdcbc59fa, util/crc32c.cc:477-485). */
+uint32_t nova_port_accelerated_crc32c(uint32_t crc, const char* buf, size_t size);
+
+/* ---- device batches ------------------------------------------------------
+ * Variable-length: block i is base[offsets[i] .. offsets[i]+lengths[i]).
+ * init_or_null[i] is block i's Extend() init (NULL: all 0, i.e. Value()).
+ * Replaces a caller loop of crc32c::Value/Extend over the blocks of one
+ * SSTable: table/table_builder.cc:202, ltc/stoc_file_client_impl.cpp:713-716,
+ * table/table.cc:436. */
+int nova_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                      const uint32_t* init_or_null, uint32_t* out_crc, size_t n_blocks,
+                      uint32_t flags, void* stream);
+
+/* Fixed-stride: block i is base[i*stride .. i*stride+len). */
+int nova_crc32c_batch_strided(const void* base, uint64_t stride, uint32_t len,
+                              size_t n_blocks, const uint32_t* init_or_null,
+                              uint32_t* out_crc, uint32_t flags, void* stream);
+
+/* ---- SSTable composites -----------------------
+ * Trailer writer: for each block (offsets[i], sizes[i]) of an SSTable image in
+ * device memory, write the 5-byte trailer at buf+offsets[i]+sizes[i]:
+ * [type][LE32 Mask(Extend(Value(block), type))], type = (flags >> 8) & 0xff,
+ * with NOVA_TRAILER_TB_QUIRK reproducing TableBuilder's trailer[4]='!'.
+ * Replaces TableBuilder::WriteRawBlock's checksum part
+ * (table/table_builder.cc:192-212) and StoCWritableFileClient::WriteRawBlock
+ * (ltc/stoc_file_client_impl.cpp:704-723). */
+int nova_sstable_write_trailers(void* buf, const uint64_t* offsets, const uint32_t* sizes,
+                                size_t n_blocks, uint32_t flags, void* stream);
+
+/* Read-verify: block i occupies sizes[i]+5 bytes at buf+offsets[i]
+ * (block, type byte, LE32 masked CRC).  ok_out[i] = 1 iff
+ * Unmask(DecodeFixed32(data+n+1)) == Value(data, n+1); *n_bad_out (device
+ * u32, must be zeroed by the caller, may be NULL) is incremented per mismatch.
+ * Replaces Table::ReadBlock's verify_checksums branch (table/table.cc:434-440,
+ * "block checksum mismatch"). */
+int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
+                               size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
+                               void* stream);
+
+/* ---- host-resident streamed path (BASELINE config 5) --------------------
+ * Blocks live in HOST memory (pinned or pageable; the analogue of NovaLSM's
+ * RDMA-registered backing_mem_, ltc/stoc_file_client_impl.cpp:43-45).  The
+ * batch is cut into chunks of chunk_blocks blocks that flow H2D -> CRC -> D2H
+ * over n_streams HIP streams; host_out receives n_blocks CRCs.  Synchronous.
+ * If host_base is not pinned it is registered (hipHostRegister) for the
+ * duration of the call. */
+int nova_crc32c_stream_host(const void* host_base, uint64_t stride, uint32_t len,
+                            size_t n_blocks, uint32_t* host_out, uint32_t flags,
+                            size_t chunk_blocks, int n_streams);
+
+/* ---- utilities ----------------------------------------------------------- */
+/* Fill nbytes of device memory with the splitmix64 counter stream
+ * (novalsm_amd/synth.py): synthetic blocks without host initialisation. */
+int nova_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t first_word,
+                         void* stream);
+/* Build + upload the tables for the current device (optional: done lazily). */
+int nova_device_init(void);
+/* Lanes per block ("G") and segment bytes the dispatcher would pick, and the
+ * kernel name, for reporting/profiling. */
+int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_unit,
+                     uint32_t* seg_bytes);
+const char* nova_crc32c_kernel_name(int lanes_per_unit);
+/* Overrides for tuning/tests: lanes per unit (0 = auto) and segment size
+ * (0 = auto).  Process-wide. */
+void nova_crc32c_set_tuning(int lanes_per_unit, uint32_t seg_bytes);
+const char* nova_error_string(int err);
+/* ABI version: bump on any signature change. */
+int nova_crc32c_abi_version(void);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* NOVA_CRC32C_H_ */

@@ -1,0 +1,731 @@
+// MI355X (gfx950) batched CRC-32C: kernels, per-device tables, C-ABI batch
+// entry points.  Drop-in for the per-SSTable-block checksum of NovaLSM
+// (util/crc32c.cc:487-588 called from table/table_builder.cc:202-204,
+// ltc/stoc_file_client_impl.cpp:713-719 and table/table.cc:434-440).
+//
+// ---------------------------------------------------------------------------
+// Algorithm (all arithmetic is GF(2) on the 32-bit reflected register)
+//
+// A "unit" is a byte range [u0,u1) of one block (a whole block, or one
+// segment of a long block).  G lanes ("a lane group", G in {1,2,4,8,16})
+// process a unit; each lane owns 4 word streams, so the unit is 4G interleaved
+// streams with a stride of S = 16G bytes -- the reference's 4-stream/16-byte
+// stride loop (util/crc32c.cc:543-577) widened from one CPU thread to G lanes.
+// Every wave-instruction of a group loads 16G contiguous bytes (dwordx4 per
+// lane).  One stream step is  c = w ^ T0[c&255] ^ T1[c>>8&255] ^ T2[..] ^ T3[..]
+// with T = "advance S bytes" split into four byte tables (the reference's
+// kStrideExtensionTable is the S=16 case).
+//
+//   * Alignment: loads are always 16-B aligned.  The unit's region is
+//     end-aligned at Eu = roundup16(u1); bytes before u0 read as zero (leading
+//     zeros do not change a zero-initialised register), bytes after u1 are
+//     zero (t = Eu-u1 trailing zeros, undone at the end by M_t^-1).
+//   * Init: Extend(init, D) runs the register from ~init; that equals running
+//     from 0 over D with ~init xor-ed into D's first four bytes.
+//   * Fold: the 4G stream states are the words of a virtual 16G-byte message;
+//     a tree (in-lane M4, M8, then cross-lane M16, M32, ... via shuffles)
+//     reduces it to one pending word V; raw(unit) = (M_t^-1 o M4)(V).
+//   * Long blocks are cut into segments so all lane groups of a wave carry
+//     equal work; a segment j units from the end contributes M_{seg*j}(raw),
+//     and contributions are xor-accumulated (order-free, so bit-exact).
+//
+// LDS (one 1024-thread workgroup per CU): the four main tables are stored as
+// 32 bank replicas -- entry idx of copy c at byte (idx<<8)|(c<<2) (+128 for
+// the odd table, +64 KiB for tables 2,3) -- so a ds_read_b32 wave-instruction
+// is conflict-free whatever the data, and one v_perm_b32 builds each address
+// from the register byte and the lane's replica offset.  128 KiB main tables
+// + 4 KiB per tree level + 512 B per wave scratch <= 160 KiB.
+// ---------------------------------------------------------------------------
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/nova_crc32c.h"
+#include "gf2_crc32c.hpp"
+
+namespace {
+
+constexpr int kWaves = 16;                 // waves per workgroup
+constexpr int kThreads = kWaves * 64;
+constexpr uint32_t kMainBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 B
+constexpr int kTreeLevels = 6;             // M4, M8, M16, M32, M64, M128
+constexpr uint32_t kTreeBytes = 4096;      // per level
+constexpr uint32_t kWaveScratch = 512;     // per wave: 64 prefix + 64 accumulators
+constexpr int kNumG = 5;                   // G = 1, 2, 4, 8, 16
+
+enum Mode { kStore = 0, kTrailer = 1, kVerify = 2 };
+
+struct CrcParams {
+  const uint8_t* base;
+  const uint64_t* offsets;   // null: strided
+  const uint32_t* lengths;
+  uint64_t stride;
+  uint32_t len;
+  uint32_t flags;
+  const uint32_t* init;      // may be null
+  uint32_t* out;             // kStore
+  uint8_t* ok_out;           // kVerify
+  uint32_t* n_bad;           // kVerify, may be null
+  uint64_t n_blocks;
+  uint32_t seg;              // segment bytes (multiple of 16); 0 = one unit per block
+  uint32_t chunk;            // blocks per wave chunk (<= 64)
+  uint64_t n_chunks;
+  const uint32_t* tab_main;  // replicated LDS image, 32768 u32
+  const uint32_t* tab_tree;  // kTreeLevels x 1024 u32
+  const uint32_t* tab_ft;    // 16 x 1024 u32
+  const uint32_t* tab_sh16;  // 32 x 1024 u32
+};
+
+// ---- device helpers --------------------------------------------------------
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32 (gfx950)
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+
+// 16-byte load through the global (not flat) address space.
+__device__ __forceinline__ uint4 gload16(uint64_t addr) {
+  const u32x4 v = *reinterpret_cast<gu32x4*>(addr);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Read a dword at an absolute LDS byte address.  The kernel holds no static
+// __shared__ objects, so the dynamic LDS region starts at address 0 and the
+// v_perm-built table address is used as is (no base add per lookup).
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t* /*lds*/, uint32_t byte_addr) {
+  return *reinterpret_cast<__attribute__((address_space(3))) const uint32_t*>(byte_addr);
+}
+
+// 4-lookup operator application from a [4][256] table in global memory.
+__device__ __forceinline__ uint32_t gapply(const uint32_t* __restrict__ t, uint32_t x) {
+  return t[x & 255] ^ t[256 + ((x >> 8) & 255)] ^ t[512 + ((x >> 16) & 255)] ^ t[768 + (x >> 24)];
+}
+
+// Same from a tree level held in LDS (non-replicated, used once per unit).
+__device__ __forceinline__ uint32_t tapply(const uint8_t* lds, int level, uint32_t x) {
+  const uint32_t* t = reinterpret_cast<const uint32_t*>(lds + kMainBytes + level * kTreeBytes);
+  return t[x & 255] ^ t[256 + ((x >> 8) & 255)] ^ t[512 + ((x >> 16) & 255)] ^ t[768 + (x >> 24)];
+}
+
+// Byte-selector for v_perm_b32(x, lo, sel): out byte0 = lo.byte0 (replica
+// offset, table parity bit 7), out byte1 = x.byte k (table row), out byte2 =
+// lo.byte2 (64 KiB half), out byte3 = 0.
+template <int K>
+struct Sel {
+  static constexpr uint32_t v = 0x0c020000u | ((4u + K) << 8);
+};
+
+// One stream step: c = w ^ M_S(c) via the replicated LDS tables.
+__device__ __forceinline__ uint32_t step(const uint8_t* lds, uint32_t c, uint32_t w, uint32_t lo0,
+                                         uint32_t lo1, uint32_t lo2, uint32_t lo3) {
+  const uint32_t a0 = __builtin_amdgcn_perm(c, lo0, Sel<0>::v);
+  const uint32_t a1 = __builtin_amdgcn_perm(c, lo1, Sel<1>::v);
+  const uint32_t a2 = __builtin_amdgcn_perm(c, lo2, Sel<2>::v);
+  const uint32_t a3 = __builtin_amdgcn_perm(c, lo3, Sel<3>::v);
+  const uint32_t t0 = lds_u32(lds, a0), t1 = lds_u32(lds, a1);
+  const uint32_t t2 = lds_u32(lds, a2), t3 = lds_u32(lds, a3);
+  return xor3(xor3(t0, t1, t2), t3, w);
+}
+
+// Four swaths (16 B per lane each) into the lane's four stream registers.
+__device__ __forceinline__ void fold4(const uint8_t* lds, uint32_t& c0, uint32_t& c1, uint32_t& c2,
+                                      uint32_t& c3, const uint4& d0, const uint4& d1,
+                                      const uint4& d2, const uint4& d3, uint32_t lo0, uint32_t lo1,
+                                      uint32_t lo2, uint32_t lo3) {
+  c0 = step(lds, c0, d0.x, lo0, lo1, lo2, lo3);
+  c1 = step(lds, c1, d0.y, lo0, lo1, lo2, lo3);
+  c2 = step(lds, c2, d0.z, lo0, lo1, lo2, lo3);
+  c3 = step(lds, c3, d0.w, lo0, lo1, lo2, lo3);
+  c0 = step(lds, c0, d1.x, lo0, lo1, lo2, lo3);
+  c1 = step(lds, c1, d1.y, lo0, lo1, lo2, lo3);
+  c2 = step(lds, c2, d1.z, lo0, lo1, lo2, lo3);
+  c3 = step(lds, c3, d1.w, lo0, lo1, lo2, lo3);
+  c0 = step(lds, c0, d2.x, lo0, lo1, lo2, lo3);
+  c1 = step(lds, c1, d2.y, lo0, lo1, lo2, lo3);
+  c2 = step(lds, c2, d2.z, lo0, lo1, lo2, lo3);
+  c3 = step(lds, c3, d2.w, lo0, lo1, lo2, lo3);
+  c0 = step(lds, c0, d3.x, lo0, lo1, lo2, lo3);
+  c1 = step(lds, c1, d3.y, lo0, lo1, lo2, lo3);
+  c2 = step(lds, c2, d3.z, lo0, lo1, lo2, lo3);
+  c3 = step(lds, c3, d3.w, lo0, lo1, lo2, lo3);
+}
+
+// Keep the bytes of word [wa, wa+4) that lie in [u0,u1); xor in the bytes of
+// ninit that sit at [u0, u0+4).
+__device__ __forceinline__ uint32_t fix_word(uint32_t w, uint64_t wa, uint64_t u0, uint64_t u1,
+                                             uint32_t ninit) {
+  int64_t lo = (int64_t)(u0 - wa);
+  int64_t hi = (int64_t)(u1 - wa);
+  lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+  hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
+  uint32_t keep = 0;
+  if (hi > lo)
+    keep = (uint32_t)(((1ull << (8 * hi)) - 1) ^ ((1ull << (8 * lo)) - 1));
+  const int64_t d = (int64_t)(wa - u0);
+  uint32_t iv = 0;
+  if (d >= 0 && d < 4) iv = ninit >> (8 * d);
+  else if (d < 0 && d > -4) iv = ninit << (8 * -d);
+  return (w & keep) ^ iv;
+}
+
+__device__ __noinline__ uint4 load_edge(uint64_t pa, uint64_t u0, uint64_t u1, uint32_t ninit) {
+  uint4 d = make_uint4(0, 0, 0, 0);
+  if (pa + 16 > u0) {  // some byte of the piece is at or after u0 (region ends at roundup16(u1))
+    d = gload16(pa);
+    d.x = fix_word(d.x, pa + 0, u0, u1, ninit);
+    d.y = fix_word(d.y, pa + 4, u0, u1, ninit);
+    d.z = fix_word(d.z, pa + 8, u0, u1, ninit);
+    d.w = fix_word(d.w, pa + 12, u0, u1, ninit);
+  }
+  return d;
+}
+
+// Bitwise byte step for the (rare) tiny-block and type-byte paths.
+__device__ __forceinline__ uint32_t byte_step(uint32_t l, uint32_t b) {
+  l ^= b;
+#pragma unroll
+  for (int i = 0; i < 8; i++) l = (l >> 1) ^ (0x82F63B78u & (0u - (l & 1u)));
+  return l;
+}
+
+__device__ __forceinline__ uint32_t mask_crc(uint32_t c) {
+  return ((c >> 15) | (c << 17)) + 0xa282ead8u;  // util/crc32c.h:28-31
+}
+__device__ __forceinline__ uint32_t unmask_crc(uint32_t m) {
+  const uint32_t r = m - 0xa282ead8u;  // util/crc32c.h:34-37
+  return (r >> 17) | (r << 15);
+}
+
+// Process unit [u0,u1) with G lanes; returns the pending word V of the
+// virtual message (identical in all G lanes of the group).
+template <int G>
+__device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0, uint64_t u1,
+                                                 uint32_t ninit, int q, uint32_t lo0,
+                                                 uint32_t lo1, uint32_t lo2, uint32_t lo3) {
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  if (u1 > u0) {
+    const uint64_t Eu = (u1 + 15) & ~15ull;
+    const uint64_t A0 = u0 & ~15ull;
+    const uint64_t K = (Eu - A0 + 16 * G - 1) / (16 * G);
+    uint64_t pa = Eu - K * 16 * G + 16 * q;
+    const uint64_t lo_edge = u0 + 4;   // pieces starting before this touch the head
+    const uint64_t hi_edge = u1 - 16;  // pieces starting after this touch the tail
+    uint64_t j = 0;
+    // Head swaths (edge handling) until the piece is clear of the head.
+    for (; j < K && (pa < lo_edge || pa > hi_edge); ++j, pa += 16 * G) {
+      const uint4 d = load_edge(pa, u0, u1, ninit);
+      c0 = step(lds, c0, d.x, lo0, lo1, lo2, lo3);
+      c1 = step(lds, c1, d.y, lo0, lo1, lo2, lo3);
+      c2 = step(lds, c2, d.z, lo0, lo1, lo2, lo3);
+      c3 = step(lds, c3, d.w, lo0, lo1, lo2, lo3);
+    }
+    // Body: no masking; groups of 4 swaths.  The loads of group g+1 are issued
+    // before group g is folded; the last prefetch re-reads the current group
+    // (an L2 hit) so the loop body stays one basic block and the compiler
+    // keeps the prefetch ahead of the fold with exact vmcnt counts.
+    const uint64_t body_end = hi_edge + 16 * G;  // first swath start that is not clean
+    uint64_t ngroups = 0;
+    if (j + 4 <= K && pa + 3 * 16 * G <= hi_edge) {
+      const uint64_t by_k = (K - j) / 4;
+      const uint64_t by_edge = (body_end - pa) / (4 * 16 * G);
+      ngroups = by_k < by_edge ? by_k : by_edge;
+    }
+    if (ngroups) {
+      // Two register sets, a and b, alternate without copies (a copy of a
+      // load destination would force a vmcnt(0) drain).
+      const uint64_t step_g = 4 * 16 * G;
+      uint4 a0 = gload16(pa), a1 = gload16(pa + 16 * G);
+      uint4 a2 = gload16(pa + 32 * G), a3 = gload16(pa + 48 * G);
+      for (uint64_t g = 0; g + 2 <= ngroups; g += 2) {
+        const uint64_t pb = pa + step_g;
+        const uint4 b0 = gload16(pb), b1 = gload16(pb + 16 * G);
+        const uint4 b2 = gload16(pb + 32 * G), b3 = gload16(pb + 48 * G);
+        fold4(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
+        const uint64_t pn = (g + 2 < ngroups) ? pb + step_g : pb;
+        a0 = gload16(pn);
+        a1 = gload16(pn + 16 * G);
+        a2 = gload16(pn + 32 * G);
+        a3 = gload16(pn + 48 * G);
+        fold4(lds, c0, c1, c2, c3, b0, b1, b2, b3, lo0, lo1, lo2, lo3);
+        pa += 2 * step_g;
+      }
+      if (ngroups & 1) {
+        fold4(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
+        pa += step_g;
+      }
+      j += 4 * ngroups;
+    }
+    // Remaining swaths (plain or tail edge).
+    for (; j < K; ++j, pa += 16 * G) {
+      uint4 d;
+      if (pa < lo_edge || pa > hi_edge) d = load_edge(pa, u0, u1, ninit);
+      else d = gload16(pa);
+      c0 = step(lds, c0, d.x, lo0, lo1, lo2, lo3);
+      c1 = step(lds, c1, d.y, lo0, lo1, lo2, lo3);
+      c2 = step(lds, c2, d.z, lo0, lo1, lo2, lo3);
+      c3 = step(lds, c3, d.w, lo0, lo1, lo2, lo3);
+    }
+  }
+  // Fold the 4G pending stream words (converged code: shuffles below).
+  uint32_t v = tapply(lds, 1, tapply(lds, 0, c0) ^ c1) ^ (tapply(lds, 0, c2) ^ c3);
+#pragma unroll
+  for (int k = 0; (1 << k) < G; ++k) {
+    const uint32_t o = __shfl_xor(v, 1 << k);
+    const bool right = (q >> k) & 1;
+    const uint32_t left_v = right ? o : v;
+    const uint32_t right_v = right ? v : o;
+    v = tapply(lds, 2 + k, left_v) ^ right_v;
+  }
+  return v;
+}
+
+template <int G, int MODE>
+__global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
+  {
+    const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
+    uint4* d = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += kThreads) d[i] = s[i];
+    const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
+    uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
+    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += kThreads) d2[i] = s2[i];
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane & (G - 1);   // lane within its group
+  const int grp = lane / G;       // group within the wave
+  constexpr int kGroups = 64 / G;
+  uint32_t* wpre = reinterpret_cast<uint32_t*>(lds + kMainBytes + kLevels * kTreeBytes +
+                                               wave * kWaveScratch);
+  uint32_t* wacc = wpre + 64;
+  const uint32_t rep = (uint32_t)(lane & 31) << 2;
+  const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
+  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
+  const uint32_t extra = (MODE == kVerify) ? 1u : 0u;  // verify covers block + type byte
+
+  for (uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave; chunk < p.n_chunks;
+       chunk += (uint64_t)gridDim.x * kWaves) {
+    // -- prologue: lane i owns block b = chunk*chunk_size + i
+    const uint64_t b = chunk * p.chunk + lane;
+    const bool valid = lane < (int)p.chunk && b < p.n_blocks;
+    uint64_t a = 0;
+    uint32_t n = 0, init = 0;
+    if (valid) {
+      a = (uint64_t)p.base + (p.offsets ? p.offsets[b] : b * p.stride);
+      n = (p.lengths ? p.lengths[b] : p.len) + extra;
+      init = p.init ? p.init[b] : 0u;
+    }
+    const uint32_t ninit = raw ? 0u : ~init;
+    uint32_t nq = 0;
+    uint32_t small_crc = 0;
+    if (valid) {
+      if (n >= 4) {
+        nq = p.seg ? (n / p.seg > 0 ? n / p.seg : 1u) : 1u;
+      } else {  // tiny block: bytewise on this lane
+        uint32_t l = ninit;
+        for (uint32_t i = 0; i < n; i++) l = byte_step(l, ((const uint8_t*)a)[i]);
+        small_crc = raw ? l : ~l;
+      }
+    }
+    // inclusive prefix of unit counts over the wave
+    uint32_t incl = nq;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const uint32_t o = __shfl_up(incl, s);
+      if (lane >= s) incl += o;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    wpre[lane] = incl;
+    wacc[lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // -- rounds: each lane group takes one unit
+    for (uint32_t r0 = 0; r0 < total; r0 += kGroups) {
+      const uint32_t u = r0 + grp;
+      const bool active = u < total;
+      int i = 0;
+#pragma unroll
+      for (int s = 32; s > 0; s >>= 1)
+        if (wpre[i + s - 1] <= u) i += s;
+      if (!active) i = 0;
+      const uint32_t a_lo = __shfl((uint32_t)a, i);
+      const uint32_t a_hi = __shfl((uint32_t)(a >> 32), i);
+      const uint32_t bn = __shfl(n, i);
+      const uint32_t bq = __shfl(nq, i);
+      const uint32_t binit = __shfl(ninit, i);
+      const uint32_t bincl = wpre[i];
+      const uint64_t ba = ((uint64_t)a_hi << 32) | a_lo;
+      const uint32_t j = bincl - 1 - u;  // 0 = last unit of the block
+      uint64_t u0 = 0, u1 = 0;
+      uint32_t uinit = 0;
+      if (active) {
+        const uint64_t E = ba + bn;
+        u1 = E - (uint64_t)p.seg * j;
+        const bool first = (j == bq - 1);
+        u0 = first ? ba : u1 - p.seg;
+        uinit = first ? binit : 0u;
+      }
+      const uint32_t v = unit_pending<G>(lds, u0, u1, uinit, q, lo0, lo1, lo2, lo3);
+      if (active && q == 0) {
+        const uint32_t t = (uint32_t)((16 - (u1 & 15)) & 15);
+        uint32_t c = gapply(p.tab_ft + t * 1024, v);
+        uint64_t m = (uint64_t)(p.seg >> 4) * j;  // shift in 16-byte units
+        while (m) {
+          const int bit = __builtin_ctzll(m);
+          c = gapply(p.tab_sh16 + bit * 1024, c);
+          m &= m - 1;
+        }
+        atomicXor(&wacc[i], c);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // -- epilogue: lane i finalises block b
+    if (valid) {
+      uint32_t crc = (n >= 4) ? (raw ? wacc[lane] : ~wacc[lane]) : small_crc;
+      if (MODE == kVerify) {
+        const uint8_t* d = (const uint8_t*)a;
+        const uint32_t stored = (uint32_t)d[n] | ((uint32_t)d[n + 1] << 8) |
+                                ((uint32_t)d[n + 2] << 16) | ((uint32_t)d[n + 3] << 24);
+        const bool ok = unmask_crc(stored) == crc;  // table/table.cc:435-437
+        p.ok_out[b] = ok ? 1 : 0;
+        if (!ok && p.n_bad) atomicAdd(p.n_bad, 1u);
+      } else {
+        if (p.flags & NOVA_CRC32C_APPEND_TYPE) {  // table/table_builder.cc:203
+          crc = ~byte_step(~crc, (p.flags >> 8) & 0xffu);
+        }
+        if (MODE == kTrailer) {
+          const uint32_t m = mask_crc(crc);
+          uint8_t* d = (uint8_t*)a + n;
+          d[0] = (uint8_t)(p.flags >> 8);
+          d[1] = (uint8_t)m;
+          d[2] = (uint8_t)(m >> 8);
+          d[3] = (uint8_t)(m >> 16);
+          d[4] = (p.flags & NOVA_TRAILER_TB_QUIRK) ? (uint8_t)'!' : (uint8_t)(m >> 24);
+        } else {
+          if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
+          p.out[b] = crc;
+        }
+      }
+    }
+  }
+}
+
+// Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
+__global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
+                                       uint64_t first_word) {
+  const uint64_t nw = nbytes / 8;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = tid; k < nw; k += stride) {
+    uint64_t z = seed + (first_word + k + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    reinterpret_cast<uint64_t*>(dst)[k] = z;
+  }
+  if (tid == 0 && (nbytes & 7)) {
+    uint64_t z = seed + (first_word + nw + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    for (uint64_t i = 0; i < (nbytes & 7); i++) dst[nw * 8 + i] = (uint8_t)(z >> (8 * i));
+  }
+}
+
+// ---- host: per-device tables ----------------------------------------------
+
+struct DevTables {
+  uint32_t* main[kNumG] = {};
+  uint32_t* tree = nullptr;
+  uint32_t* ft = nullptr;
+  uint32_t* sh16 = nullptr;
+  int cus = 0;
+  int err = 0;
+};
+
+constexpr int kMaxDevices = 64;
+DevTables g_dev[kMaxDevices];
+std::once_flag g_once[kMaxDevices];
+
+std::atomic<int> g_tune_g{0};
+std::atomic<uint32_t> g_tune_seg{0};
+
+void build_main_image(const nova::gf2::Lin& m, std::vector<uint32_t>& img) {
+  uint32_t t[4][256];
+  nova::gf2::byte_tables(m, t);
+  img.assign(kMainBytes / 4, 0);
+  for (int k = 0; k < 4; k++)
+    for (int idx = 0; idx < 256; idx++)
+      for (int c = 0; c < 32; c++) {
+        const uint32_t byte = (uint32_t)((k >> 1) << 16) | (uint32_t)(idx << 8) |
+                              (uint32_t)((k & 1) << 7) | (uint32_t)(c << 2);
+        img[byte / 4] = t[k][idx];
+      }
+}
+
+void append_op(const nova::gf2::Lin& m, std::vector<uint32_t>& v) {
+  uint32_t t[4][256];
+  nova::gf2::byte_tables(m, t);
+  for (int k = 0; k < 4; k++) v.insert(v.end(), t[k], t[k] + 256);
+}
+
+template <typename T>
+int upload(T** dst, const std::vector<uint32_t>& src) {
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, src.size() * 4);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemcpy(p, src.data(), src.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return (int)e;
+  *dst = reinterpret_cast<T*>(p);
+  return 0;
+}
+
+template <int G, int MODE>
+int set_lds_attr() {
+  const int lds = (int)(kMainBytes + (2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16)) * kTreeBytes +
+                        kWaves * kWaveScratch);
+  return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_units_kernel<G, MODE>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+template <int MODE>
+int set_lds_attrs_mode() {
+  int e = 0;
+  if ((e = set_lds_attr<1, MODE>())) return e;
+  if ((e = set_lds_attr<2, MODE>())) return e;
+  if ((e = set_lds_attr<4, MODE>())) return e;
+  if ((e = set_lds_attr<8, MODE>())) return e;
+  return set_lds_attr<16, MODE>();
+}
+
+void init_device(int dev, DevTables* t) {
+  hipDeviceProp_t prop;
+  hipError_t e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) { t->err = (int)e; return; }
+  t->cus = prop.multiProcessorCount;
+  using namespace nova::gf2;
+  const Lin m1 = zero_byte();
+  std::vector<uint32_t> img;
+  for (int gi = 0; gi < kNumG; gi++) {
+    const int G = 1 << gi;
+    build_main_image(power(m1, 16 * G), img);
+    if ((t->err = upload(&t->main[gi], img))) return;
+  }
+  std::vector<uint32_t> tree;
+  for (int l = 0; l < kTreeLevels; l++) append_op(power(m1, 4u << l), tree);
+  if ((t->err = upload(&t->tree, tree))) return;
+  std::vector<uint32_t> ft;
+  const Lin m1inv = inverse(m1);
+  const Lin m4 = power(m1, 4);
+  for (int tt = 0; tt < 16; tt++) append_op(compose(power(m1inv, tt), m4), ft);
+  if ((t->err = upload(&t->ft, ft))) return;
+  std::vector<uint32_t> sh;
+  Lin s = power(m1, 16);
+  for (int b = 0; b < 32; b++) {
+    append_op(s, sh);
+    s = compose(s, s);
+  }
+  if ((t->err = upload(&t->sh16, sh))) return;
+  if ((t->err = set_lds_attrs_mode<kStore>())) return;
+  if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
+  if ((t->err = set_lds_attrs_mode<kVerify>())) return;
+}
+
+DevTables* tables(int* err) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) { *err = NOVA_E_NODEV; return nullptr; }
+  if (dev < 0 || dev >= kMaxDevices) { *err = NOVA_E_INVAL; return nullptr; }
+  std::call_once(g_once[dev], [&] { init_device(dev, &g_dev[dev]); });
+  if (g_dev[dev].err) { *err = g_dev[dev].err; return nullptr; }
+  *err = 0;
+  return &g_dev[dev];
+}
+
+int gindex(int G) { return G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4; }
+
+// Dispatcher policy (lanes per unit G, segment bytes).  Small G keeps the
+// per-unit fold cheap relative to the stream work; longer blocks are split so
+// every lane group of a wave carries about `seg` bytes.
+void plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int* G, uint32_t* seg) {
+  int g = 4;
+  uint32_t s = uniform ? 0u : 4096u;
+  (void)n_blocks;
+  (void)bytes_per_block;
+  const int tg = g_tune_g.load();
+  const uint32_t ts = g_tune_seg.load();
+  if (tg == 1 || tg == 2 || tg == 4 || tg == 8 || tg == 16) g = tg;
+  if (ts) s = ts & ~15u;
+  *G = g;
+  *seg = s;
+}
+
+template <int MODE>
+int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
+  p.tab_main = t->main[gindex(G)];
+  p.tab_tree = t->tree;
+  p.tab_ft = t->ft;
+  p.tab_sh16 = t->sh16;
+  p.chunk = 64;
+  p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
+  uint64_t wgs = (p.n_chunks + kWaves - 1) / kWaves;
+  if (wgs > (uint64_t)t->cus) wgs = t->cus;
+  if (wgs == 0) return 0;
+  const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
+  const size_t lds = kMainBytes + levels * kTreeBytes + kWaves * kWaveScratch;
+  switch (G) {
+    case 1: hipLaunchKernelGGL((crc32c_units_kernel<1, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
+    case 2: hipLaunchKernelGGL((crc32c_units_kernel<2, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
+    case 4: hipLaunchKernelGGL((crc32c_units_kernel<4, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
+    case 8: hipLaunchKernelGGL((crc32c_units_kernel<8, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
+    default: hipLaunchKernelGGL((crc32c_units_kernel<16, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
+  }
+  return (int)hipGetLastError();
+}
+
+int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStream_t stream) {
+  int err = 0;
+  DevTables* t = tables(&err);
+  if (!t) return err;
+  if (p.n_blocks == 0) return 0;
+  int G;
+  uint32_t seg;
+  plan(p.n_blocks, bytes_per_block, uniform, &G, &seg);
+  p.seg = seg;
+  switch (mode) {
+    case kStore: return launch_mode<kStore>(G, p, t, stream);
+    case kTrailer: return launch_mode<kTrailer>(G, p, t, stream);
+    default: return launch_mode<kVerify>(G, p, t, stream);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int nova_crc32c_abi_version(void) { return 1; }
+
+int nova_device_init(void) {
+  int err = 0;
+  return tables(&err) ? 0 : err;
+}
+
+int nova_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                      const uint32_t* init_or_null, uint32_t* out_crc, size_t n_blocks,
+                      uint32_t flags, void* stream) {
+  if (n_blocks && (!base || !offsets || !lengths || !out_crc)) return NOVA_E_INVAL;
+  CrcParams p{};
+  p.base = (const uint8_t*)base;
+  p.offsets = offsets;
+  p.lengths = lengths;
+  p.flags = flags;
+  p.init = init_or_null;
+  p.out = out_crc;
+  p.n_blocks = n_blocks;
+  return run(kStore, p, false, 0, (hipStream_t)stream);
+}
+
+int nova_crc32c_batch_strided(const void* base, uint64_t stride, uint32_t len, size_t n_blocks,
+                              const uint32_t* init_or_null, uint32_t* out_crc, uint32_t flags,
+                              void* stream) {
+  if (n_blocks && (!base || !out_crc)) return NOVA_E_INVAL;
+  CrcParams p{};
+  p.base = (const uint8_t*)base;
+  p.stride = stride;
+  p.len = len;
+  p.flags = flags;
+  p.init = init_or_null;
+  p.out = out_crc;
+  p.n_blocks = n_blocks;
+  return run(kStore, p, true, len, (hipStream_t)stream);
+}
+
+int nova_sstable_write_trailers(void* buf, const uint64_t* offsets, const uint32_t* sizes,
+                                size_t n_blocks, uint32_t flags, void* stream) {
+  if (n_blocks && (!buf || !offsets || !sizes)) return NOVA_E_INVAL;
+  CrcParams p{};
+  p.base = (const uint8_t*)buf;
+  p.offsets = offsets;
+  p.lengths = sizes;
+  p.flags = (flags & (0xff00u | NOVA_TRAILER_TB_QUIRK)) | NOVA_CRC32C_APPEND_TYPE;
+  p.n_blocks = n_blocks;
+  return run(kTrailer, p, false, 0, (hipStream_t)stream);
+}
+
+int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
+                               size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
+                               void* stream) {
+  if (n_blocks && (!buf || !offsets || !sizes || !ok_out)) return NOVA_E_INVAL;
+  CrcParams p{};
+  p.base = (const uint8_t*)buf;
+  p.offsets = offsets;
+  p.lengths = sizes;
+  p.ok_out = ok_out;
+  p.n_bad = n_bad_out;
+  p.n_blocks = n_blocks;
+  return run(kVerify, p, false, 0, (hipStream_t)stream);
+}
+
+int nova_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t first_word,
+                         void* stream) {
+  if (!dev && nbytes) return NOVA_E_INVAL;
+  if (!nbytes) return 0;
+  uint64_t blocks = (nbytes / 8 + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(fill_splitmix64_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     (uint8_t*)dev, (uint64_t)nbytes, seed, first_word);
+  return (int)hipGetLastError();
+}
+
+int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_unit,
+                     uint32_t* seg_bytes) {
+  int g;
+  uint32_t s;
+  plan(n_blocks, bytes_per_block, true, &g, &s);
+  if (lanes_per_unit) *lanes_per_unit = g;
+  if (seg_bytes) *seg_bytes = s;
+  return 0;
+}
+
+const char* nova_crc32c_kernel_name(int lanes_per_unit) {
+  switch (lanes_per_unit) {
+    case 1: return "crc32c_units_kernel<1, 0>";
+    case 2: return "crc32c_units_kernel<2, 0>";
+    case 4: return "crc32c_units_kernel<4, 0>";
+    case 8: return "crc32c_units_kernel<8, 0>";
+    case 16: return "crc32c_units_kernel<16, 0>";
+    default: return "crc32c_units_kernel";
+  }
+}
+
+void nova_crc32c_set_tuning(int lanes_per_unit, uint32_t seg_bytes) {
+  g_tune_g.store(lanes_per_unit);
+  g_tune_seg.store(seg_bytes);
+}
+
+const char* nova_error_string(int err) {
+  switch (err) {
+    case 0: return "success";
+    case NOVA_E_INVAL: return "invalid argument";
+    case NOVA_E_NODEV: return "no usable HIP device";
+    case NOVA_E_NOMEM: return "allocation failed";
+    default: return hipGetErrorString((hipError_t)err);
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+"""Pin the CPU oracle (the checker) against the reference's own answers.
+
+Known answers: util/crc32c_test.cc:14-61 and the self-test constant
+util/crc32c.cc:479-481.  Golden vectors: tests/golden/crc32c_golden.json,
+produced by the reference util/crc32c.cc compiled unmodified
+(oracle/gen_golden.py).  CPU only.
+"""
+import numpy as np
+import pytest
+
+from novalsm_amd.synth import splitmix64_bytes
+
+
+def test_standard_results(oracle):
+    # util/crc32c_test.cc:14-46 (RFC 3720 B.4)
+    assert oracle.value(bytes(32)) == 0x8A9136AA
+    assert oracle.value(b"\xff" * 32) == 0x62A8AB43
+    assert oracle.value(bytes(range(32))) == 0x46DD794E
+    assert oracle.value(bytes(range(31, -1, -1))) == 0x113FDB5C
+    iscsi = bytes([0x01, 0xC0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x14, 0, 0, 0, 0, 0,
+                   0x04, 0, 0, 0, 0, 0x14, 0, 0, 0, 0x18, 0x28, 0, 0, 0, 0, 0, 0, 0, 0x02, 0,
+                   0, 0, 0, 0, 0, 0])
+    assert oracle.value(iscsi) == 0xD9963A56
+
+
+def test_values_extend_mask(oracle):
+    # util/crc32c_test.cc:48-61
+    assert oracle.value(b"a") != oracle.value(b"foo")
+    assert oracle.value(b"hello world") == oracle.extend(oracle.value(b"hello "), b"world")
+    crc = oracle.value(b"foo")
+    assert crc != oracle.mask(crc)
+    assert crc != oracle.mask(oracle.mask(crc))
+    assert crc == oracle.unmask(oracle.mask(crc))
+    assert crc == oracle.unmask(oracle.unmask(oracle.mask(oracle.mask(crc))))
+
+
+def test_self_test_constant(oracle):
+    # util/crc32c.cc:477-485 CanAccelerateCRC32C
+    assert oracle.value(b"TestCRCBuffer") == 0xDCBC59FA
+
+
+def test_known_answers_fixture(oracle, golden):
+    for k in golden["known_answers"]:
+        assert oracle.value(bytes.fromhex(k["hex"])) == k["crc"], k["name"]
+
+
+def test_extra_goldens(oracle, golden):
+    ex = golden["extra"]
+    assert oracle.value(b"123456789") == ex["check_123456789"] == 0xE3069283
+    assert oracle.value(b"hello world") == ex["hello_world"]
+    x = b"x" * 4096
+    assert oracle.value(x) == ex["x4096_value"]
+    assert oracle.extend(ex["x4096_value"], b"\x00") == ex["x4096_type0"]
+    assert oracle.mask(ex["x4096_type0"]) == ex["x4096_mask"]
+
+
+def test_byte_table_matches_reference(oracle, golden):
+    # kByteExtensionTable (util/crc32c.cc:20-105) as observed through the reference
+    bt, st = oracle.tables()
+    assert [int(v) for v in bt] == golden["byte_table"]
+    assert int(bt[1]) == 0xF26B8303
+
+
+def test_stride_tables_are_16_byte_shift(oracle):
+    # kStrideExtensionTable{3,2,1,0}[b] == byte b at position {0,1,2,3}, advanced
+    # through 16 zero bytes; re-derive from the byte table.
+    bt, st = oracle.tables()
+
+    def zero_byte(l):
+        return int(bt[l & 0xFF]) ^ (l >> 8)
+
+    for k in range(4):
+        for b in (0, 1, 2, 0x80, 0xFF, 0x5A):
+            l = b << (8 * k)
+            for _ in range(16):
+                l = zero_byte(l)
+            assert int(st[k][b]) == l
+
+
+def test_mask_fixture(oracle, golden):
+    for m in golden["mask"]:
+        assert oracle.mask(m["crc"]) == m["mask"]
+        assert oracle.unmask(m["crc"]) == m["unmask"]
+
+
+def test_cases_fixture(oracle, golden):
+    for c in golden["cases"]:
+        data = splitmix64_bytes(c["seed"], c["length"], c["offset"]).tobytes()
+        assert oracle.extend(c["init"], data) == c["crc"], c
+
+
+def test_packed_sstable_fixture(oracle, golden):
+    pk = golden["packed"]
+    buf = splitmix64_bytes(pk["seed"], pk["total"])
+    got = oracle.batch(buf, pk["offsets"], pk["sizes"])
+    assert [int(x) for x in got] == pk["crc"]
+    for o, s, tb, st in zip(pk["offsets"], pk["sizes"], pk["tb_trailer_hex"],
+                            pk["stoc_trailer_hex"]):
+        blk = buf[o:o + s].tobytes()
+        assert oracle.trailer(blk, 0, True).hex() == tb
+        assert oracle.trailer(blk, 0, False).hex() == st
+        # a StoC trailer verifies; a TableBuilder trailer does not unless the
+        # true MSB happens to be '!' (the latent quirk).
+        assert oracle.verify(blk + bytes.fromhex(st))
+
+
+def test_config1_fixture(oracle, golden):
+    c1 = golden["config1"]
+    buf = splitmix64_bytes(c1["seed"], c1["n"] * c1["len"])
+    got = oracle.batch_strided(buf, c1["len"], c1["len"], c1["n"])
+    assert [int(x) for x in got] == c1["crc"]
+    mt = oracle.batch_strided_mt(buf, c1["len"], c1["len"], c1["n"], threads=4)
+    assert np.array_equal(mt, got)
+
+
+def test_splitmix64_c_matches_numpy(oracle):
+    for seed, n, w in [(1, 4096, 0), (2, 1001, 0), (3, 77, 5)]:
+        a = oracle.splitmix64(n, seed, w)
+        b = splitmix64_bytes(seed, n, 8 * w)
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 65])
+def test_alignment_independence(oracle, n):
+    # util/crc32c.cc: result independent of the start alignment (probe)
+    base = splitmix64_bytes(5, n + 16)
+    want = oracle.value(base[:n].tobytes())
+    for off in range(1, 8):
+        shifted = np.zeros(n + 16, dtype=np.uint8)
+        shifted[off:off + n] = base[:n]
+        assert oracle.value(shifted[off:off + n].tobytes()) == want
