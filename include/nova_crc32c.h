@@ -139,6 +139,16 @@ const char* nova_crc32c_kernel_name(int lanes_per_unit);
  * (0 = auto).  Process-wide. */
 void nova_crc32c_set_tuning(int lanes_per_unit, uint32_t seg_bytes);
 const char* nova_error_string(int err);
+
+/* ---- diagnostics (profiling only; not part of the drop-in surface) ------
+ * variant: 0 production, 1 ablation (no table lookups -- WRONG CRCs, timing
+ * only), 2 non-temporal data loads.  Process-wide. */
+void nova_diag_set_variant(int variant);
+/* Plain coalesced streaming read of `bytes` (multiple of 16) with `wgs`
+ * 256-thread workgroups; out_dev receives wgs*256 words.  The chip's read
+ * ceiling for the roofline discussion. */
+int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
+                          void* stream);
 /* ABI version: bump on any signature change. */
 int nova_crc32c_abi_version(void);
 

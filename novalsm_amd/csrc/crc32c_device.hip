@@ -66,7 +66,8 @@ struct CrcParams {
   uint64_t stride;
   uint32_t len;
   uint32_t flags;
-  const uint32_t* init;      // may be null
+  const uint32_t* init;      // may be null (units kernel); stream kernel: never null
+  uint32_t init_stride;      // 1, or 0 with init -> a zero word (stream kernel)
   uint32_t* out;             // kStore
   uint8_t* ok_out;           // kVerify
   uint32_t* n_bad;           // kVerify, may be null
@@ -89,9 +90,18 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
+// Kernel variants (diagnostics / tuning; 0 = production).
+constexpr int kVarNoLookup = 1;  // ablation: stream step without table lookups
+constexpr int kVarNT = 2;        // non-temporal (nt) data loads
+
 // 16-byte load through the global (not flat) address space.
+template <int VAR = 0>
 __device__ __forceinline__ uint4 gload16(uint64_t addr) {
-  const u32x4 v = *reinterpret_cast<gu32x4*>(addr);
+  u32x4 v;
+  if constexpr ((VAR & kVarNT) != 0)
+    v = __builtin_nontemporal_load(reinterpret_cast<gu32x4*>(addr));
+  else
+    v = *reinterpret_cast<gu32x4*>(addr);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -122,8 +132,10 @@ struct Sel {
 };
 
 // One stream step: c = w ^ M_S(c) via the replicated LDS tables.
+template <int VAR = 0>
 __device__ __forceinline__ uint32_t step(const uint8_t* lds, uint32_t c, uint32_t w, uint32_t lo0,
                                          uint32_t lo1, uint32_t lo2, uint32_t lo3) {
+  if constexpr ((VAR & kVarNoLookup) != 0) return ((c << 1) | (c >> 31)) ^ w;  // keeps c live
   const uint32_t a0 = __builtin_amdgcn_perm(c, lo0, Sel<0>::v);
   const uint32_t a1 = __builtin_amdgcn_perm(c, lo1, Sel<1>::v);
   const uint32_t a2 = __builtin_amdgcn_perm(c, lo2, Sel<2>::v);
@@ -134,26 +146,27 @@ __device__ __forceinline__ uint32_t step(const uint8_t* lds, uint32_t c, uint32_
 }
 
 // Four swaths (16 B per lane each) into the lane's four stream registers.
+template <int VAR = 0>
 __device__ __forceinline__ void fold4(const uint8_t* lds, uint32_t& c0, uint32_t& c1, uint32_t& c2,
                                       uint32_t& c3, const uint4& d0, const uint4& d1,
                                       const uint4& d2, const uint4& d3, uint32_t lo0, uint32_t lo1,
                                       uint32_t lo2, uint32_t lo3) {
-  c0 = step(lds, c0, d0.x, lo0, lo1, lo2, lo3);
-  c1 = step(lds, c1, d0.y, lo0, lo1, lo2, lo3);
-  c2 = step(lds, c2, d0.z, lo0, lo1, lo2, lo3);
-  c3 = step(lds, c3, d0.w, lo0, lo1, lo2, lo3);
-  c0 = step(lds, c0, d1.x, lo0, lo1, lo2, lo3);
-  c1 = step(lds, c1, d1.y, lo0, lo1, lo2, lo3);
-  c2 = step(lds, c2, d1.z, lo0, lo1, lo2, lo3);
-  c3 = step(lds, c3, d1.w, lo0, lo1, lo2, lo3);
-  c0 = step(lds, c0, d2.x, lo0, lo1, lo2, lo3);
-  c1 = step(lds, c1, d2.y, lo0, lo1, lo2, lo3);
-  c2 = step(lds, c2, d2.z, lo0, lo1, lo2, lo3);
-  c3 = step(lds, c3, d2.w, lo0, lo1, lo2, lo3);
-  c0 = step(lds, c0, d3.x, lo0, lo1, lo2, lo3);
-  c1 = step(lds, c1, d3.y, lo0, lo1, lo2, lo3);
-  c2 = step(lds, c2, d3.z, lo0, lo1, lo2, lo3);
-  c3 = step(lds, c3, d3.w, lo0, lo1, lo2, lo3);
+  c0 = step<VAR>(lds, c0, d0.x, lo0, lo1, lo2, lo3);
+  c1 = step<VAR>(lds, c1, d0.y, lo0, lo1, lo2, lo3);
+  c2 = step<VAR>(lds, c2, d0.z, lo0, lo1, lo2, lo3);
+  c3 = step<VAR>(lds, c3, d0.w, lo0, lo1, lo2, lo3);
+  c0 = step<VAR>(lds, c0, d1.x, lo0, lo1, lo2, lo3);
+  c1 = step<VAR>(lds, c1, d1.y, lo0, lo1, lo2, lo3);
+  c2 = step<VAR>(lds, c2, d1.z, lo0, lo1, lo2, lo3);
+  c3 = step<VAR>(lds, c3, d1.w, lo0, lo1, lo2, lo3);
+  c0 = step<VAR>(lds, c0, d2.x, lo0, lo1, lo2, lo3);
+  c1 = step<VAR>(lds, c1, d2.y, lo0, lo1, lo2, lo3);
+  c2 = step<VAR>(lds, c2, d2.z, lo0, lo1, lo2, lo3);
+  c3 = step<VAR>(lds, c3, d2.w, lo0, lo1, lo2, lo3);
+  c0 = step<VAR>(lds, c0, d3.x, lo0, lo1, lo2, lo3);
+  c1 = step<VAR>(lds, c1, d3.y, lo0, lo1, lo2, lo3);
+  c2 = step<VAR>(lds, c2, d3.z, lo0, lo1, lo2, lo3);
+  c3 = step<VAR>(lds, c3, d3.w, lo0, lo1, lo2, lo3);
 }
 
 // Keep the bytes of word [wa, wa+4) that lie in [u0,u1); xor in the bytes of
@@ -174,10 +187,11 @@ __device__ __forceinline__ uint32_t fix_word(uint32_t w, uint64_t wa, uint64_t u
   return (w & keep) ^ iv;
 }
 
+template <int VAR = 0>
 __device__ __noinline__ uint4 load_edge(uint64_t pa, uint64_t u0, uint64_t u1, uint32_t ninit) {
   uint4 d = make_uint4(0, 0, 0, 0);
   if (pa + 16 > u0) {  // some byte of the piece is at or after u0 (region ends at roundup16(u1))
-    d = gload16(pa);
+    d = gload16<VAR>(pa);
     d.x = fix_word(d.x, pa + 0, u0, u1, ninit);
     d.y = fix_word(d.y, pa + 4, u0, u1, ninit);
     d.z = fix_word(d.z, pa + 8, u0, u1, ninit);
@@ -202,9 +216,28 @@ __device__ __forceinline__ uint32_t unmask_crc(uint32_t m) {
   return (r >> 17) | (r << 15);
 }
 
+// Fold the 4G pending stream words of a lane group (4 per lane, lane q holds
+// the words at byte offsets 16q+0,4,8,12 of each 16G-byte swath) into the
+// pending word V of the group's last word: in-lane M4, M8, then cross-lane
+// M16, M32, ... with xor-shuffles.  Must be called from converged code.
+template <int G>
+__device__ __forceinline__ uint32_t group_fold(const uint8_t* lds, uint32_t c0, uint32_t c1,
+                                               uint32_t c2, uint32_t c3, int q) {
+  uint32_t v = tapply(lds, 1, tapply(lds, 0, c0) ^ c1) ^ (tapply(lds, 0, c2) ^ c3);
+#pragma unroll
+  for (int k = 0; (1 << k) < G; ++k) {
+    const uint32_t o = __shfl_xor(v, 1 << k);
+    const bool right = (q >> k) & 1;
+    const uint32_t left_v = right ? o : v;
+    const uint32_t right_v = right ? v : o;
+    v = tapply(lds, 2 + k, left_v) ^ right_v;
+  }
+  return v;
+}
+
 // Process unit [u0,u1) with G lanes; returns the pending word V of the
 // virtual message (identical in all G lanes of the group).
-template <int G>
+template <int G, int VAR = 0>
 __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0, uint64_t u1,
                                                  uint32_t ninit, int q, uint32_t lo0,
                                                  uint32_t lo1, uint32_t lo2, uint32_t lo3) {
@@ -219,11 +252,11 @@ __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0
     uint64_t j = 0;
     // Head swaths (edge handling) until the piece is clear of the head.
     for (; j < K && (pa < lo_edge || pa > hi_edge); ++j, pa += 16 * G) {
-      const uint4 d = load_edge(pa, u0, u1, ninit);
-      c0 = step(lds, c0, d.x, lo0, lo1, lo2, lo3);
-      c1 = step(lds, c1, d.y, lo0, lo1, lo2, lo3);
-      c2 = step(lds, c2, d.z, lo0, lo1, lo2, lo3);
-      c3 = step(lds, c3, d.w, lo0, lo1, lo2, lo3);
+      const uint4 d = load_edge<VAR>(pa, u0, u1, ninit);
+      c0 = step<VAR>(lds, c0, d.x, lo0, lo1, lo2, lo3);
+      c1 = step<VAR>(lds, c1, d.y, lo0, lo1, lo2, lo3);
+      c2 = step<VAR>(lds, c2, d.z, lo0, lo1, lo2, lo3);
+      c3 = step<VAR>(lds, c3, d.w, lo0, lo1, lo2, lo3);
     }
     // Body: no masking; groups of 4 swaths.  The loads of group g+1 are issued
     // before group g is folded; the last prefetch re-reads the current group
@@ -240,23 +273,23 @@ __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0
       // Two register sets, a and b, alternate without copies (a copy of a
       // load destination would force a vmcnt(0) drain).
       const uint64_t step_g = 4 * 16 * G;
-      uint4 a0 = gload16(pa), a1 = gload16(pa + 16 * G);
-      uint4 a2 = gload16(pa + 32 * G), a3 = gload16(pa + 48 * G);
+      uint4 a0 = gload16<VAR>(pa), a1 = gload16<VAR>(pa + 16 * G);
+      uint4 a2 = gload16<VAR>(pa + 32 * G), a3 = gload16<VAR>(pa + 48 * G);
       for (uint64_t g = 0; g + 2 <= ngroups; g += 2) {
         const uint64_t pb = pa + step_g;
-        const uint4 b0 = gload16(pb), b1 = gload16(pb + 16 * G);
-        const uint4 b2 = gload16(pb + 32 * G), b3 = gload16(pb + 48 * G);
-        fold4(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
+        const uint4 b0 = gload16<VAR>(pb), b1 = gload16<VAR>(pb + 16 * G);
+        const uint4 b2 = gload16<VAR>(pb + 32 * G), b3 = gload16<VAR>(pb + 48 * G);
+        fold4<VAR>(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
         const uint64_t pn = (g + 2 < ngroups) ? pb + step_g : pb;
-        a0 = gload16(pn);
-        a1 = gload16(pn + 16 * G);
-        a2 = gload16(pn + 32 * G);
-        a3 = gload16(pn + 48 * G);
-        fold4(lds, c0, c1, c2, c3, b0, b1, b2, b3, lo0, lo1, lo2, lo3);
+        a0 = gload16<VAR>(pn);
+        a1 = gload16<VAR>(pn + 16 * G);
+        a2 = gload16<VAR>(pn + 32 * G);
+        a3 = gload16<VAR>(pn + 48 * G);
+        fold4<VAR>(lds, c0, c1, c2, c3, b0, b1, b2, b3, lo0, lo1, lo2, lo3);
         pa += 2 * step_g;
       }
       if (ngroups & 1) {
-        fold4(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
+        fold4<VAR>(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
         pa += step_g;
       }
       j += 4 * ngroups;
@@ -264,28 +297,18 @@ __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0
     // Remaining swaths (plain or tail edge).
     for (; j < K; ++j, pa += 16 * G) {
       uint4 d;
-      if (pa < lo_edge || pa > hi_edge) d = load_edge(pa, u0, u1, ninit);
-      else d = gload16(pa);
-      c0 = step(lds, c0, d.x, lo0, lo1, lo2, lo3);
-      c1 = step(lds, c1, d.y, lo0, lo1, lo2, lo3);
-      c2 = step(lds, c2, d.z, lo0, lo1, lo2, lo3);
-      c3 = step(lds, c3, d.w, lo0, lo1, lo2, lo3);
+      if (pa < lo_edge || pa > hi_edge) d = load_edge<VAR>(pa, u0, u1, ninit);
+      else d = gload16<VAR>(pa);
+      c0 = step<VAR>(lds, c0, d.x, lo0, lo1, lo2, lo3);
+      c1 = step<VAR>(lds, c1, d.y, lo0, lo1, lo2, lo3);
+      c2 = step<VAR>(lds, c2, d.z, lo0, lo1, lo2, lo3);
+      c3 = step<VAR>(lds, c3, d.w, lo0, lo1, lo2, lo3);
     }
   }
-  // Fold the 4G pending stream words (converged code: shuffles below).
-  uint32_t v = tapply(lds, 1, tapply(lds, 0, c0) ^ c1) ^ (tapply(lds, 0, c2) ^ c3);
-#pragma unroll
-  for (int k = 0; (1 << k) < G; ++k) {
-    const uint32_t o = __shfl_xor(v, 1 << k);
-    const bool right = (q >> k) & 1;
-    const uint32_t left_v = right ? o : v;
-    const uint32_t right_v = right ? v : o;
-    v = tapply(lds, 2 + k, left_v) ^ right_v;
-  }
-  return v;
+  return group_fold<G>(lds, c0, c1, c2, c3, q);
 }
 
-template <int G, int MODE>
+template <int G, int MODE, int VAR = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
@@ -376,7 +399,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
         u0 = first ? ba : u1 - p.seg;
         uinit = first ? binit : 0u;
       }
-      const uint32_t v = unit_pending<G>(lds, u0, u1, uinit, q, lo0, lo1, lo2, lo3);
+      const uint32_t v = unit_pending<G, VAR>(lds, u0, u1, uinit, q, lo0, lo1, lo2, lo3);
       if (active && q == 0) {
         const uint32_t t = (uint32_t)((16 - (u1 & 15)) & 15);
         uint32_t c = gapply(p.tab_ft + t * 1024, v);
@@ -424,6 +447,104 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
   }
 }
 
+// Aligned uniform batches (base, stride 16-B aligned, len a multiple of 64G):
+// every lane group walks its blocks b = gid, gid+T, gid+2T, ... as ONE flat
+// stream of 4-swath steps, so the two-register-set prefetch never stops at a
+// block boundary; the per-block fold + store runs between steps while the
+// next block's loads are in flight.  No masking, no unit bookkeeping.
+template <int G, int VAR = 0>
+__global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
+  {
+    const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
+    uint4* d = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += kThreads) d[i] = s[i];
+    const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
+    uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
+    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += kThreads) d2[i] = s2[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane & (G - 1);
+  constexpr int kGroups = 64 / G;
+  const uint64_t T = (uint64_t)gridDim.x * kWaves * kGroups;  // lane groups in the grid
+  const uint64_t gid = ((uint64_t)blockIdx.x * kWaves + wave) * kGroups + lane / G;
+  const uint64_t n = p.n_blocks;
+  const uint32_t KG = p.len / (64 * G);  // 4-swath steps per block (>= 1)
+  const uint64_t rounds = (n + T - 1) / T;
+  const uint64_t S = rounds * KG;        // uniform over the grid
+  const uint32_t rep = (uint32_t)(lane & 31) << 2;
+  const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
+  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
+  const uint64_t base = (uint64_t)p.base + 16 * q;
+  const uint64_t stride = p.stride;
+
+  // next-load cursor (block nb, step nk); loads of blocks past the end are
+  // clamped to the last block (valid memory, results discarded)
+  uint64_t nb = gid;
+  uint32_t nk = 0;
+  uint64_t na = base + (nb < n ? nb : n - 1) * stride;
+  auto advance = [&]() {
+    if (++nk == KG) {
+      nk = 0;
+      nb += T;
+      na = base + (nb < n ? nb : n - 1) * stride;
+    } else {
+      na += 64 * G;
+    }
+  };
+  // fold cursor
+  uint64_t cb = gid;
+  uint32_t ck = 0;
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  // init words are loaded one block ahead and complemented only where they
+  // are used, so the load never forces a vmcnt drain of the data stream; a
+  // NULL init arrives as a zero word with stride 0 (Value() semantics).
+  auto init_of = [&](uint64_t b) -> uint32_t {
+    return p.init[(b < n ? b : n - 1) * p.init_stride];
+  };
+  uint32_t init_cur = init_of(cb);
+  uint32_t init_next = init_of(cb + T);
+  auto finish_step = [&]() {
+    if (++ck == KG) {  // wave-uniform: every group ends a block on the same step
+      const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
+      const uint32_t r = tapply(lds, 0, v);  // M4: pending -> register at block end
+      uint32_t crc = raw ? r : ~r;
+      if (p.flags & NOVA_CRC32C_APPEND_TYPE) crc = ~byte_step(~crc, (p.flags >> 8) & 0xffu);
+      if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
+      if (q == 0 && cb < n) p.out[cb] = crc;
+      c0 = c1 = c2 = c3 = 0;
+      ck = 0;
+      cb += T;
+      init_cur = init_next;
+      init_next = init_of(cb + T);
+    }
+  };
+
+  uint4 a0 = gload16<VAR>(na), a1 = gload16<VAR>(na + 16 * G);
+  uint4 a2 = gload16<VAR>(na + 32 * G), a3 = gload16<VAR>(na + 48 * G);
+  advance();
+  for (uint64_t st = 0; st < S; st += 2) {
+    uint4 b0 = gload16<VAR>(na), b1 = gload16<VAR>(na + 16 * G);
+    uint4 b2 = gload16<VAR>(na + 32 * G), b3 = gload16<VAR>(na + 48 * G);
+    advance();
+    if (ck == 0 && q == 0 && !raw) a0.x ^= ~init_cur;  // Extend init folded into word 0
+    fold4<VAR>(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
+    finish_step();
+    if (st + 1 >= S) break;
+    a0 = gload16<VAR>(na);
+    a1 = gload16<VAR>(na + 16 * G);
+    a2 = gload16<VAR>(na + 32 * G);
+    a3 = gload16<VAR>(na + 48 * G);
+    advance();
+    if (ck == 0 && q == 0 && !raw) b0.x ^= ~init_cur;
+    fold4<VAR>(lds, c0, c1, c2, c3, b0, b1, b2, b3, lo0, lo1, lo2, lo3);
+    finish_step();
+  }
+}
+
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
 __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                        uint64_t first_word) {
@@ -446,6 +567,28 @@ __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t s
   }
 }
 
+// Diagnostic: plain coalesced streaming read (grid-stride, 4 x 16 B per lane
+// in flight), the chip's read ceiling for comparison with the CRC kernels.
+__global__ void __launch_bounds__(256) read_stream_kernel(const uint8_t* base, uint64_t n16,
+                                                          uint32_t* out) {
+  const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t nth = (uint64_t)gridDim.x * 256;
+  uint32_t acc = 0;
+  uint64_t i = tid;
+  const uint64_t b = (uint64_t)base;
+  for (; i + 3 * nth < n16; i += 4 * nth) {
+    const uint4 a0 = gload16(b + 16 * i), a1 = gload16(b + 16 * (i + nth));
+    const uint4 a2 = gload16(b + 16 * (i + 2 * nth)), a3 = gload16(b + 16 * (i + 3 * nth));
+    acc ^= a0.x ^ a0.y ^ a0.z ^ a0.w ^ a1.x ^ a1.y ^ a1.z ^ a1.w;
+    acc ^= a2.x ^ a2.y ^ a2.z ^ a2.w ^ a3.x ^ a3.y ^ a3.z ^ a3.w;
+  }
+  for (; i < n16; i += nth) {
+    const uint4 a = gload16(b + 16 * i);
+    acc ^= a.x ^ a.y ^ a.z ^ a.w;
+  }
+  out[tid] = acc;
+}
+
 // ---- host: per-device tables ----------------------------------------------
 
 struct DevTables {
@@ -453,6 +596,7 @@ struct DevTables {
   uint32_t* tree = nullptr;
   uint32_t* ft = nullptr;
   uint32_t* sh16 = nullptr;
+  uint32_t* zero_word = nullptr;  // 16 zero bytes: the NULL-init stand-in
   int cus = 0;
   int err = 0;
 };
@@ -462,6 +606,7 @@ DevTables g_dev[kMaxDevices];
 std::once_flag g_once[kMaxDevices];
 
 std::atomic<int> g_tune_g{0};
+std::atomic<int> g_tune_var{0};
 std::atomic<uint32_t> g_tune_seg{0};
 
 void build_main_image(const nova::gf2::Lin& m, std::vector<uint32_t>& img) {
@@ -494,22 +639,39 @@ int upload(T** dst, const std::vector<uint32_t>& src) {
   return 0;
 }
 
-template <int G, int MODE>
+template <int G, int MODE, int VAR = 0>
 int set_lds_attr() {
   const int lds = (int)(kMainBytes + (2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16)) * kTreeBytes +
                         kWaves * kWaveScratch);
-  return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_units_kernel<G, MODE>),
+  return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_units_kernel<G, MODE, VAR>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
-template <int MODE>
+template <int G, int VAR = 0>
+int set_lds_attr_stream() {
+  const int lds = (int)(kMainBytes + (2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16)) * kTreeBytes);
+  return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_stream_kernel<G, VAR>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+template <int VAR = 0>
+int set_lds_attrs_stream() {
+  int e = 0;
+  if ((e = set_lds_attr_stream<1, VAR>())) return e;
+  if ((e = set_lds_attr_stream<2, VAR>())) return e;
+  if ((e = set_lds_attr_stream<4, VAR>())) return e;
+  if ((e = set_lds_attr_stream<8, VAR>())) return e;
+  return set_lds_attr_stream<16, VAR>();
+}
+
+template <int MODE, int VAR = 0>
 int set_lds_attrs_mode() {
   int e = 0;
-  if ((e = set_lds_attr<1, MODE>())) return e;
-  if ((e = set_lds_attr<2, MODE>())) return e;
-  if ((e = set_lds_attr<4, MODE>())) return e;
-  if ((e = set_lds_attr<8, MODE>())) return e;
-  return set_lds_attr<16, MODE>();
+  if ((e = set_lds_attr<1, MODE, VAR>())) return e;
+  if ((e = set_lds_attr<2, MODE, VAR>())) return e;
+  if ((e = set_lds_attr<4, MODE, VAR>())) return e;
+  if ((e = set_lds_attr<8, MODE, VAR>())) return e;
+  return set_lds_attr<16, MODE, VAR>();
 }
 
 void init_device(int dev, DevTables* t) {
@@ -540,9 +702,14 @@ void init_device(int dev, DevTables* t) {
     s = compose(s, s);
   }
   if ((t->err = upload(&t->sh16, sh))) return;
+  if ((t->err = upload(&t->zero_word, std::vector<uint32_t>(4, 0u)))) return;
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;
+  if ((t->err = set_lds_attrs_mode<kStore, kVarNoLookup>())) return;
+  if ((t->err = set_lds_attrs_mode<kStore, kVarNT>())) return;
+  if ((t->err = set_lds_attrs_stream<0>())) return;
+  if ((t->err = set_lds_attrs_stream<kVarNoLookup>())) return;
 }
 
 DevTables* tables(int* err) {
@@ -574,6 +741,18 @@ void plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int* G, uin
   *seg = s;
 }
 
+template <int MODE, int VAR>
+int launch_g(int G, dim3 grid, size_t lds, hipStream_t stream, const CrcParams& p) {
+  switch (G) {
+    case 1: hipLaunchKernelGGL((crc32c_units_kernel<1, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    case 2: hipLaunchKernelGGL((crc32c_units_kernel<2, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    case 4: hipLaunchKernelGGL((crc32c_units_kernel<4, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    case 8: hipLaunchKernelGGL((crc32c_units_kernel<8, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    default: hipLaunchKernelGGL((crc32c_units_kernel<16, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+  }
+  return (int)hipGetLastError();
+}
+
 template <int MODE>
 int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   p.tab_main = t->main[gindex(G)];
@@ -587,14 +766,48 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   if (wgs == 0) return 0;
   const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   const size_t lds = kMainBytes + levels * kTreeBytes + kWaves * kWaveScratch;
+  const int var = g_tune_var.load();
+  if (MODE == kStore && var == kVarNoLookup) return launch_g<kStore, kVarNoLookup>(G, dim3(wgs), lds, stream, p);
+  if (MODE == kStore && var == kVarNT) return launch_g<kStore, kVarNT>(G, dim3(wgs), lds, stream, p);
+  return launch_g<MODE, 0>(G, dim3(wgs), lds, stream, p);
+}
+
+template <int VAR>
+int launch_stream_g(int G, dim3 grid, size_t lds, hipStream_t stream, const CrcParams& p) {
   switch (G) {
-    case 1: hipLaunchKernelGGL((crc32c_units_kernel<1, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
-    case 2: hipLaunchKernelGGL((crc32c_units_kernel<2, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
-    case 4: hipLaunchKernelGGL((crc32c_units_kernel<4, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
-    case 8: hipLaunchKernelGGL((crc32c_units_kernel<8, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
-    default: hipLaunchKernelGGL((crc32c_units_kernel<16, MODE>), dim3(wgs), dim3(kThreads), lds, stream, p); break;
+    case 1: hipLaunchKernelGGL((crc32c_stream_kernel<1, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    case 2: hipLaunchKernelGGL((crc32c_stream_kernel<2, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    case 4: hipLaunchKernelGGL((crc32c_stream_kernel<4, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    case 8: hipLaunchKernelGGL((crc32c_stream_kernel<8, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    default: hipLaunchKernelGGL((crc32c_stream_kernel<16, VAR>), grid, dim3(kThreads), lds, stream, p); break;
   }
   return (int)hipGetLastError();
+}
+
+// Lanes per block for the streaming kernel, or 0 if the batch is not eligible
+// (unaligned base/stride, or len not a multiple of 64*G for any G).
+int stream_lanes(const CrcParams& p) {
+  if (((uint64_t)p.base & 15) || (p.stride & 15) || p.len == 0 || p.stride < p.len) return 0;
+  int want = p.len >= 16384 ? 16 : 8;
+  const int tg = g_tune_g.load();
+  if (tg == 1 || tg == 2 || tg == 4 || tg == 8 || tg == 16) want = tg;
+  for (int g = want; g >= 1; g >>= 1)
+    if (p.len % (64u * g) == 0) return g;
+  return 0;
+}
+
+int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
+  p.init_stride = p.init ? 1u : 0u;
+  if (!p.init) p.init = t->zero_word;
+  p.tab_main = t->main[gindex(G)];
+  p.tab_tree = t->tree;
+  const uint64_t groups_per_wg = (uint64_t)kWaves * (64 / G);
+  uint64_t wgs = (p.n_blocks + groups_per_wg - 1) / groups_per_wg;
+  if (wgs > (uint64_t)t->cus) wgs = t->cus;
+  const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
+  const size_t lds = kMainBytes + levels * kTreeBytes;
+  if (g_tune_var.load() == kVarNoLookup) return launch_stream_g<kVarNoLookup>(G, dim3(wgs), lds, stream, p);
+  return launch_stream_g<0>(G, dim3(wgs), lds, stream, p);
 }
 
 int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStream_t stream) {
@@ -602,6 +815,10 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   DevTables* t = tables(&err);
   if (!t) return err;
   if (p.n_blocks == 0) return 0;
+  if (mode == kStore && uniform && !g_tune_seg.load() && g_tune_var.load() != kVarNT) {
+    const int sg = stream_lanes(p);
+    if (sg) return launch_stream(sg, p, t, stream);
+  }
   int G;
   uint32_t seg;
   plan(p.n_blocks, bytes_per_block, uniform, &G, &seg);
@@ -716,6 +933,16 @@ const char* nova_crc32c_kernel_name(int lanes_per_unit) {
 void nova_crc32c_set_tuning(int lanes_per_unit, uint32_t seg_bytes) {
   g_tune_g.store(lanes_per_unit);
   g_tune_seg.store(seg_bytes);
+}
+
+void nova_diag_set_variant(int variant) { g_tune_var.store(variant); }
+
+int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
+                          void* stream) {
+  if (!base || !out_dev || wgs <= 0) return NOVA_E_INVAL;
+  hipLaunchKernelGGL(read_stream_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)base, (uint64_t)(bytes / 16), out_dev);
+  return (int)hipGetLastError();
 }
 
 const char* nova_error_string(int err) {
