@@ -255,9 +255,10 @@ def main() -> int:
 
     value = world * bytes_step * args.steps / dt / 2**30
     achieved = bytes_step / avg_launch_s / 1e9
-    lanes, seg = C.plan(n, bytes_step // n)
-    if args.lanes:
-        lanes = args.lanes
+    if wl["kind"] == "strided":
+        dispatch = C.describe(n, L, L, variable=False)
+    else:
+        dispatch = C.describe(n, 0, 0, variable=True)
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_config{args.config}.json")
     if os.path.exists(pmc_path):
@@ -284,7 +285,7 @@ def main() -> int:
             "data": "synthetic (splitmix64 generated on device)",
             "config": {"workload": wl["workload"], "n_blocks": n, "bytes_per_gpu": bytes_step,
                        "parallelism": f"shard{world}" if world > 1 else "single",
-                       "lanes_per_unit": lanes, "kernel": C.kernel_name(lanes)},
+                       "dispatch": dispatch},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,

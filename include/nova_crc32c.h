@@ -130,10 +130,14 @@ int nova_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t first
                          void* stream);
 /* Build + upload the tables for the current device (optional: done lazily). */
 int nova_device_init(void);
-/* Lanes per block ("G") and segment bytes the dispatcher would pick, and the
- * kernel name, for reporting/profiling. */
+/* Lanes per block ("G") and segment bytes the dispatcher would pick for an
+ * aligned fixed-stride batch; returns 1 for the streaming kernel, 0 for the
+ * units kernel.  nova_crc32c_describe writes a JSON object naming the kernel
+ * and its launch parameters (for reports and profiles). */
 int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_unit,
                      uint32_t* seg_bytes);
+int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int variable, char* buf,
+                         size_t buflen);
 const char* nova_crc32c_kernel_name(int lanes_per_unit);
 /* Overrides for tuning/tests: lanes per unit (0 = auto) and segment size
  * (0 = auto).  Process-wide. */
@@ -144,6 +148,14 @@ const char* nova_error_string(int err);
  * variant: 0 production, 1 ablation (no table lookups -- WRONG CRCs, timing
  * only), 2 non-temporal data loads.  Process-wide. */
 void nova_diag_set_variant(int variant);
+/* variant 4: the streaming kernel writes {begin, end, XCC id} per wave
+ * (s_memrealtime ticks, 100 MHz) to dev_stamps[3*wave ...]. */
+void nova_diag_set_stamps(uint64_t* dev_stamps);
+/* Streaming kernel: how many other workgroups' claim counters a wave probes
+ * for work once its own are exhausted (default 8 = one per XCD; -1 default). */
+void nova_diag_set_static_pct(int steal_probes);
+/* Streaming kernel: consecutive blocks per lane group per round (default 1). */
+void nova_diag_set_blocks_per_group(int bpg);
 /* Plain coalesced streaming read of `bytes` (multiple of 16) with `wgs`
  * 256-thread workgroups; out_dev receives wgs*256 words.  The chip's read
  * ceiling for the roofline discussion. */

@@ -69,6 +69,7 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
         "nova_device_init": (i32, []),
         "nova_crc32c_plan": (i32, [sz, u64, ctypes.POINTER(i32), ctypes.POINTER(u32)]),
         "nova_crc32c_kernel_name": (ctypes.c_char_p, [i32]),
+        "nova_crc32c_describe": (i32, [sz, u64, u64, i32, ctypes.c_char_p, sz]),
         "nova_crc32c_set_tuning": (None, [i32, u32]),
         "nova_error_string": (ctypes.c_char_p, [i32]),
         "nova_crc32c_abi_version": (i32, []),
@@ -232,6 +233,13 @@ def plan(n_blocks: int, bytes_per_block: int):
     s = ctypes.c_uint32(0)
     load().nova_crc32c_plan(n_blocks, bytes_per_block, ctypes.byref(g), ctypes.byref(s))
     return g.value, s.value
+
+
+def describe(n_blocks: int, length: int, stride: int, variable: bool = False) -> dict:
+    import json
+    buf = ctypes.create_string_buffer(512)
+    load().nova_crc32c_describe(n_blocks, length, stride, 1 if variable else 0, buf, 512)
+    return json.loads(buf.value.decode())
 
 
 def kernel_name(lanes_per_unit: int) -> str:

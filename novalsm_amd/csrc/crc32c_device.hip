@@ -79,6 +79,10 @@ struct CrcParams {
   const uint32_t* tab_tree;  // kTreeLevels x 1024 u32
   const uint32_t* tab_ft;    // 16 x 1024 u32
   const uint32_t* tab_sh16;  // 32 x 1024 u32
+  uint64_t* stamps;          // diagnostics: per-wave {tables loaded, done} (or null)
+  uint32_t* sched;           // stream kernel: per-workgroup claim counters, 64 B apart
+  uint32_t steal_limit;      // stream kernel: max other workgroups probed when out of work
+  uint32_t bpg;              // stream kernel: consecutive blocks per lane group per round
 };
 
 // ---- device helpers --------------------------------------------------------
@@ -93,6 +97,8 @@ typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 // Kernel variants (diagnostics / tuning; 0 = production).
 constexpr int kVarNoLookup = 1;  // ablation: stream step without table lookups
 constexpr int kVarNT = 2;        // non-temporal (nt) data loads
+constexpr int kVarStamps = 4;    // record per-wave s_memrealtime stamps (diagnostics)
+constexpr int kVarStaticClaims = 8;  // stream kernel: claims without atomics (diagnostics)
 
 // 16-byte load through the global (not flat) address space.
 template <int VAR = 0>
@@ -447,11 +453,21 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
   }
 }
 
-// Aligned uniform batches (base, stride 16-B aligned, len a multiple of 64G):
-// every lane group walks its blocks b = gid, gid+T, gid+2T, ... as ONE flat
-// stream of 4-swath steps, so the two-register-set prefetch never stops at a
-// block boundary; the per-block fold + store runs between steps while the
-// next block's loads are in flight.  No masking, no unit bookkeeping.
+// Aligned uniform batches (base, stride 16-B aligned, len a multiple of 64G).
+//
+// A "round" is kGroups = 64/G consecutive blocks, one per lane group of a
+// wave.  Each wave owns a stream of rounds and walks it as ONE flat sequence
+// of 4-swath steps, so the two-register-set prefetch never stops at a block
+// boundary; the per-block fold + store runs between steps while the next
+// block's loads are in flight.
+//
+// Scheduling is guided-dynamic: wave w first takes a static share of
+// `static_rounds` rounds, then tickets of shrinking size from one device-scope
+// counter (relaxed fetch_add by lane 0, requested one ticket ahead so its
+// latency hides under a whole ticket of streaming).  Per-wave timestamps showed
+// static partitioning leaves ~20% of wave time idle at the tail (XCDs and CUs
+// stream at different speeds); the tickets absorb that skew.  The counter is
+// zeroed by a memset on the launch stream before every launch.
 template <int G, int VAR = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -468,80 +484,199 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int q = lane & (G - 1);
+  const int grp = lane / G;
   constexpr int kGroups = 64 / G;
-  const uint64_t T = (uint64_t)gridDim.x * kWaves * kGroups;  // lane groups in the grid
-  const uint64_t gid = ((uint64_t)blockIdx.x * kWaves + wave) * kGroups + lane / G;
+  const uint64_t wid = (uint64_t)blockIdx.x * kWaves + wave;
   const uint64_t n = p.n_blocks;
-  const uint32_t KG = p.len / (64 * G);  // 4-swath steps per block (>= 1)
-  const uint64_t rounds = (n + T - 1) / T;
-  const uint64_t S = rounds * KG;        // uniform over the grid
+  const uint64_t R = (n + (uint64_t)kGroups * p.bpg - 1) / ((uint64_t)kGroups * p.bpg);  // rounds
+  const uint32_t KG = p.len / (64 * G);            // 4-swath steps per block (even, >= 2)
   const uint32_t rep = (uint32_t)(lane & 31) << 2;
   const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
   const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
   const uint64_t base = (uint64_t)p.base + 16 * q;
   const uint64_t stride = p.stride;
+  constexpr uint64_t kStep = 64 * G;  // bytes of one 4-swath step per lane group
+  uint64_t t_begin = 0;
+  if constexpr ((VAR & kVarStamps) != 0) t_begin = __builtin_amdgcn_s_memrealtime();
 
-  // next-load cursor (block nb, step nk); loads of blocks past the end are
-  // clamped to the last block (valid memory, results discarded)
-  uint64_t nb = gid;
-  uint32_t nk = 0;
-  uint64_t na = base + (nb < n ? nb : n - 1) * stride;
+  // A round is kGroups*BPG consecutive blocks; lane group grp owns BPG
+  // consecutive blocks of it (longer contiguous runs per group).  Blocks past
+  // the end clamp to the last block: valid memory, results discarded.
+  const uint32_t BPG = p.bpg;
+  auto blk_of = [&](uint64_t r, uint32_t j) -> uint64_t {
+    return (r * kGroups + grp) * BPG + j;
+  };
+  auto blk_addr = [&](uint64_t r, uint32_t j) -> uint64_t {
+    uint64_t b = blk_of(r, j);
+    if (b >= n) b = n - 1;
+    return base + b * stride;
+  };
+  auto init_of = [&](uint64_t r, uint32_t j) -> uint32_t {
+    uint64_t b = blk_of(r, j);
+    if (b >= n) b = n - 1;
+    return p.init[b * p.init_stride];
+  };
+
+  // ---- work distribution ----------------------------------------------------
+  // Workgroup w owns the interleaved rounds w, w+nwg, w+2*nwg, ... (so the
+  // whole grid sweeps memory together: contiguous per-workgroup ranges 16 MiB
+  // apart measured ~30% slower, all streams hitting the same HBM channels).
+  // Its waves claim those rounds one at a time from a per-workgroup counter in
+  // global memory (relaxed device-scope atomic add by lane 0), one round AHEAD
+  // of use, so the waves of a CU finish together instead of in age-priority
+  // order; when its rounds run out a wave steals from other workgroups'
+  // counters.  ~1 claim per round per wave keeps every counter far below its
+  // atomic rate.  Wave k's first round is implicit (claim index k); counted
+  // claims start after those.  The atomic is issued from inline asm with
+  // EXEC = lane 0 so the compiler does not drain vmcnt(0) at a divergent join;
+  // its result is read one round later after an explicit vmcnt(7): a round is
+  // >= 2 steps, so >= 8 loads were issued after the claim and it is complete
+  // once all but the 7 newest ops are; a smaller count would also wait on the
+  // block's output store and the fresh prefetch (measured: ~14% slower).  The
+  // asm "writes" the result register so the readfirstlane cannot be hoisted.
+  const uint32_t nwg = gridDim.x;
+  uint32_t victim = blockIdx.x;  // counter currently claimed from
+  uint32_t tried = 0;            // victims found exhausted
+  uint32_t req_old = 0;
+  uint32_t static_idx = 0;
+  auto claim = [&](uint32_t v) {
+    if constexpr ((VAR & kVarStaticClaims) != 0) {
+      req_old = wave + kWaves * (++static_idx) - kWaves;  // wave k takes k, k+16, ...
+      return;
+    }
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %[save], exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "global_atomic_add %[old], %[zoff], %[one], %[ctr] sc0\n\t"
+        "s_mov_b64 exec, %[save]"
+        : [old] "=&v"(req_old), [save] "=&s"(save)
+        : [zoff] "v"(v * 16u), [one] "v"(1u), [ctr] "s"(p.sched)
+        : "memory");
+  };
+  // round for claim index idx of workgroup v, or ~0 if v's rounds are exhausted
+  auto round_of = [&](uint32_t v, uint32_t idx) -> uint64_t {
+    const uint64_t r = ((uint64_t)idx + kWaves) * nwg + v;  // first kWaves claims are implicit
+    return r < R ? r : ~0ull;
+  };
+  // Collect the pending claim; on an exhausted range move to the next victim
+  // and claim synchronously (only happens at the tail).  Returns ~0 when all
+  // ranges are exhausted.
+  auto collect = [&](bool wait_all) -> uint64_t {
+    if (wait_all) asm volatile("s_waitcnt vmcnt(0)" : "+v"(req_old) : : "memory");
+    else asm volatile("s_waitcnt vmcnt(7)" : "+v"(req_old) : : "memory");
+    uint64_t r = round_of(victim, __builtin_amdgcn_readfirstlane(req_old));
+    while (r == ~0ull && ++tried < p.steal_limit) {
+      victim = (victim + 1) % nwg;
+      claim(victim);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(req_old) : : "memory");
+      r = round_of(victim, __builtin_amdgcn_readfirstlane(req_old));
+    }
+    return r;
+  };
+
+  // load cursor: round lr, block lj of the group's BPG blocks, step lk; the
+  // wave streams its rounds as one flat sequence of steps (wave-uniform)
+  uint64_t lr = (uint64_t)wave * nwg + blockIdx.x;
+  bool live = lr < R;
+  if (!live) {  // tiny batch: no implicit round; claim synchronously
+    claim(victim);
+    lr = collect(true);
+    live = lr != ~0ull;
+  }
+  if (live) claim(victim);  // next round in flight
+  uint32_t lk = 0, lj = 0;
+  uint64_t na = live ? blk_addr(lr, 0) : base;
   auto advance = [&]() {
-    if (++nk == KG) {
-      nk = 0;
-      nb += T;
-      na = base + (nb < n ? nb : n - 1) * stride;
+    if (!live) return;  // exhausted: keep re-reading the current step (discarded)
+    if (++lk == KG) {
+      lk = 0;
+      if (++lj == BPG) {
+        lj = 0;
+        const uint64_t nr = collect(false);
+        if (nr != ~0ull) {
+          lr = nr;
+          claim(victim);
+          na = blk_addr(lr, 0);
+        } else {
+          live = false;  // keep re-reading the last round (results discarded)
+        }
+      } else {
+        na = blk_addr(lr, lj);
+      }
     } else {
-      na += 64 * G;
+      na += kStep;
     }
   };
-  // fold cursor
-  uint64_t cb = gid;
-  uint32_t ck = 0;
+  // fold cursor: round fr, block fj (lags the load cursor by one step)
+  uint64_t fr = lr;
+  uint32_t fk = 0, fj = 0;
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-  // init words are loaded one block ahead and complemented only where they
-  // are used, so the load never forces a vmcnt drain of the data stream; a
-  // NULL init arrives as a zero word with stride 0 (Value() semantics).
-  auto init_of = [&](uint64_t b) -> uint32_t {
-    return p.init[(b < n ? b : n - 1) * p.init_stride];
-  };
-  uint32_t init_cur = init_of(cb);
-  uint32_t init_next = init_of(cb + T);
+  uint32_t init_cur = p.init_stride ? init_of(fr, 0) : 0u;
+  uint32_t init_next = 0;
+  uint64_t fr_next = fr;
+  bool fold_live = live;
   auto finish_step = [&]() {
-    if (++ck == KG) {  // wave-uniform: every group ends a block on the same step
+    if (++fk == KG) {  // wave-uniform: every group ends a block on the same step
       const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
-      const uint32_t r = tapply(lds, 0, v);  // M4: pending -> register at block end
-      uint32_t crc = raw ? r : ~r;
+      const uint32_t reg = tapply(lds, 0, v);  // M4: pending -> register at block end
+      uint32_t crc = raw ? reg : ~reg;
       if (p.flags & NOVA_CRC32C_APPEND_TYPE) crc = ~byte_step(~crc, (p.flags >> 8) & 0xffu);
       if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
-      if (q == 0 && cb < n) p.out[cb] = crc;
+      const uint64_t blk = blk_of(fr, fj);
+      if (q == 0 && blk < n) p.out[blk] = crc;
       c0 = c1 = c2 = c3 = 0;
-      ck = 0;
-      cb += T;
+      fk = 0;
       init_cur = init_next;
-      init_next = init_of(cb + T);
+      if (++fj == BPG) {
+        fj = 0;
+        fold_live = fr != fr_next;  // the load cursor moved on to another round
+        fr = fr_next;
+      }
     }
   };
+  const bool has_init = p.init_stride != 0;  // uniform; NULL init needs no loads
+  auto note_block = [&]() {  // called right after loading step 0 of block (lr, lj)
+    if (lj == 0) fr_next = lr;
+    if (has_init) init_next = init_of(lr, lj);
+  };
 
-  uint4 a0 = gload16<VAR>(na), a1 = gload16<VAR>(na + 16 * G);
-  uint4 a2 = gload16<VAR>(na + 32 * G), a3 = gload16<VAR>(na + 48 * G);
-  advance();
-  for (uint64_t st = 0; st < S; st += 2) {
-    uint4 b0 = gload16<VAR>(na), b1 = gload16<VAR>(na + 16 * G);
-    uint4 b2 = gload16<VAR>(na + 32 * G), b3 = gload16<VAR>(na + 48 * G);
+  if (live) {
+    uint4 a0 = gload16<VAR>(na), a1 = gload16<VAR>(na + 16 * G);
+    uint4 a2 = gload16<VAR>(na + 32 * G), a3 = gload16<VAR>(na + 48 * G);
     advance();
-    if (ck == 0 && q == 0 && !raw) a0.x ^= ~init_cur;  // Extend init folded into word 0
-    fold4<VAR>(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
-    finish_step();
-    if (st + 1 >= S) break;
-    a0 = gload16<VAR>(na);
-    a1 = gload16<VAR>(na + 16 * G);
-    a2 = gload16<VAR>(na + 32 * G);
-    a3 = gload16<VAR>(na + 48 * G);
-    advance();
-    if (ck == 0 && q == 0 && !raw) b0.x ^= ~init_cur;
-    fold4<VAR>(lds, c0, c1, c2, c3, b0, b1, b2, b3, lo0, lo1, lo2, lo3);
-    finish_step();
+    for (;;) {
+      if (lk == 0 && live) note_block();
+      uint4 b0 = gload16<VAR>(na), b1 = gload16<VAR>(na + 16 * G);
+      uint4 b2 = gload16<VAR>(na + 32 * G), b3 = gload16<VAR>(na + 48 * G);
+      const bool b_live = live;
+      advance();
+      if (fk == 0 && q == 0 && !raw) a0.x ^= ~init_cur;  // Extend init -> word 0
+      fold4<VAR>(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
+      finish_step();
+      if (!fold_live) break;
+      if (!b_live && fk == 0 && fj == 0) break;
+      if (lk == 0 && live) note_block();
+      a0 = gload16<VAR>(na);
+      a1 = gload16<VAR>(na + 16 * G);
+      a2 = gload16<VAR>(na + 32 * G);
+      a3 = gload16<VAR>(na + 48 * G);
+      const bool a_live = live;
+      advance();
+      if (fk == 0 && q == 0 && !raw) b0.x ^= ~init_cur;
+      fold4<VAR>(lds, c0, c1, c2, c3, b0, b1, b2, b3, lo0, lo1, lo2, lo3);
+      finish_step();
+      if (!fold_live) break;
+      if (!a_live && fk == 0 && fj == 0) break;
+    }
+  }
+  if constexpr ((VAR & kVarStamps) != 0) {
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && p.stamps) {
+      p.stamps[3 * wid] = t_begin;
+      p.stamps[3 * wid + 1] = t_end;
+      p.stamps[3 * wid + 2] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+    }
   }
 }
 
@@ -597,16 +732,23 @@ struct DevTables {
   uint32_t* ft = nullptr;
   uint32_t* sh16 = nullptr;
   uint32_t* zero_word = nullptr;  // 16 zero bytes: the NULL-init stand-in
+  uint32_t* sched = nullptr;      // kSchedSlots x 256 claim counters, 64 B apart
   int cus = 0;
   int err = 0;
 };
 
 constexpr int kMaxDevices = 64;
+constexpr int kSchedSlots = 64;  // concurrent stream-kernel launches per device (round-robin)
+constexpr int kSchedWords = 256 * 16;  // per launch: up to 256 workgroups x 64 B
+std::atomic<uint64_t> g_sched_ticket{0};
+std::atomic<int> g_tune_static_pct{-1};  // reused: steal probe limit (-1 = default)
 DevTables g_dev[kMaxDevices];
 std::once_flag g_once[kMaxDevices];
 
 std::atomic<int> g_tune_g{0};
 std::atomic<int> g_tune_var{0};
+std::atomic<int> g_tune_bpg{0};
+std::atomic<uint64_t*> g_diag_stamps{nullptr};
 std::atomic<uint32_t> g_tune_seg{0};
 
 void build_main_image(const nova::gf2::Lin& m, std::vector<uint32_t>& img) {
@@ -703,6 +845,7 @@ void init_device(int dev, DevTables* t) {
   }
   if ((t->err = upload(&t->sh16, sh))) return;
   if ((t->err = upload(&t->zero_word, std::vector<uint32_t>(4, 0u)))) return;
+  if ((t->err = upload(&t->sched, std::vector<uint32_t>(kSchedSlots * kSchedWords, 0u)))) return;
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;
@@ -710,6 +853,8 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_mode<kStore, kVarNT>())) return;
   if ((t->err = set_lds_attrs_stream<0>())) return;
   if ((t->err = set_lds_attrs_stream<kVarNoLookup>())) return;
+  if ((t->err = set_lds_attrs_stream<kVarStamps>())) return;
+  if ((t->err = set_lds_attrs_stream<kVarStamps | kVarStaticClaims>())) return;
 }
 
 DevTables* tables(int* err) {
@@ -728,9 +873,11 @@ int gindex(int G) { return G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4
 // Dispatcher policy (lanes per unit G, segment bytes).  Small G keeps the
 // per-unit fold cheap relative to the stream work; longer blocks are split so
 // every lane group of a wave carries about `seg` bytes.
+// Measured on MI355X for BASELINE config 3 (mixed 4/16/64 KiB, unaligned):
+// G = 16 lanes per 16 KiB segment was best among G 4..16 x seg 4..32 KiB.
 void plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int* G, uint32_t* seg) {
-  int g = 4;
-  uint32_t s = uniform ? 0u : 4096u;
+  int g = uniform ? 8 : 16;
+  uint32_t s = uniform ? 0u : 16384u;
   (void)n_blocks;
   (void)bytes_per_block;
   const int tg = g_tune_g.load();
@@ -785,15 +932,27 @@ int launch_stream_g(int G, dim3 grid, size_t lds, hipStream_t stream, const CrcP
 }
 
 // Lanes per block for the streaming kernel, or 0 if the batch is not eligible
-// (unaligned base/stride, or len not a multiple of 64*G for any G).
+// (unaligned base/stride, or len not a multiple of 128*G for any G).
+// Measured on MI355X (tools/sweep.py): G = 16 for blocks >= 16 KiB, else 8.
 int stream_lanes(const CrcParams& p) {
   if (((uint64_t)p.base & 15) || (p.stride & 15) || p.len == 0 || p.stride < p.len) return 0;
   int want = p.len >= 16384 ? 16 : 8;
   const int tg = g_tune_g.load();
   if (tg == 1 || tg == 2 || tg == 4 || tg == 8 || tg == 16) want = tg;
   for (int g = want; g >= 1; g >>= 1)
-    if (p.len % (64u * g) == 0) return g;
+    if (p.len % (128u * g) == 0) return g;  // KG = len / 64G even
   return 0;
+}
+
+// Blocks per lane group per round: a wave-round of ~64 KiB measured best on
+// MI355X at every block size tried (4 KiB: G=8 x 2 blocks, 76% of 8 TB/s vs
+// 71% with 1; 16 KiB: G=16 x 1 block, 82%).
+uint32_t stream_bpg(int G, uint32_t len) {
+  const int tb = g_tune_bpg.load();
+  if (tb > 0) return (uint32_t)tb;
+  const uint64_t per_round = (uint64_t)(64 / G) * len;
+  uint64_t b = 65536 / (per_round ? per_round : 1);
+  return b < 1 ? 1u : (b > 64 ? 64u : (uint32_t)b);
 }
 
 int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
@@ -801,12 +960,34 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   if (!p.init) p.init = t->zero_word;
   p.tab_main = t->main[gindex(G)];
   p.tab_tree = t->tree;
-  const uint64_t groups_per_wg = (uint64_t)kWaves * (64 / G);
-  uint64_t wgs = (p.n_blocks + groups_per_wg - 1) / groups_per_wg;
+  p.bpg = stream_bpg(G, p.len);
+  const uint64_t groups = 64 / G;
+  const uint64_t rounds = (p.n_blocks + groups * p.bpg - 1) / (groups * p.bpg);
+  uint64_t wgs = (rounds + kWaves - 1) / kWaves;
   if (wgs > (uint64_t)t->cus) wgs = t->cus;
+  const uint64_t waves = wgs * kWaves;
+  if (wgs > 256) wgs = 256;
+  {
+    const int sl = g_tune_static_pct.load();
+    p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;  // 8 probes = one victim per XCD
+    p.bpg = stream_bpg(G, p.len);
+  }
+  // per-launch claim counters, zeroed on the launch stream (no host sync)
+  const uint64_t slot = g_sched_ticket.fetch_add(1) % kSchedSlots;
+  p.sched = t->sched + slot * kSchedWords;
+  hipError_t e = hipMemsetAsync(p.sched, 0, wgs * 64, stream);
+  if (e != hipSuccess) return (int)e;
   const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   const size_t lds = kMainBytes + levels * kTreeBytes;
   if (g_tune_var.load() == kVarNoLookup) return launch_stream_g<kVarNoLookup>(G, dim3(wgs), lds, stream, p);
+  if (g_tune_var.load() == kVarStamps) {
+    p.stamps = g_diag_stamps.load();
+    return launch_stream_g<kVarStamps>(G, dim3(wgs), lds, stream, p);
+  }
+  if (g_tune_var.load() == (kVarStamps | kVarStaticClaims)) {
+    p.stamps = g_diag_stamps.load();
+    return launch_stream_g<kVarStamps | kVarStaticClaims>(G, dim3(wgs), lds, stream, p);
+  }
   return launch_stream_g<0>(G, dim3(wgs), lds, stream, p);
 }
 
@@ -911,12 +1092,51 @@ int nova_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t first
 
 int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_unit,
                      uint32_t* seg_bytes) {
+  // Plan for an aligned fixed-stride batch of bytes_per_block blocks.
+  CrcParams p{};
+  p.base = reinterpret_cast<const uint8_t*>(uintptr_t(256));
+  p.len = (uint32_t)bytes_per_block;
+  p.stride = bytes_per_block;
+  p.n_blocks = n_blocks;
+  const int sg = (g_tune_seg.load() || g_tune_var.load() == kVarNT) ? 0 : stream_lanes(p);
+  if (sg) {
+    if (lanes_per_unit) *lanes_per_unit = sg;
+    if (seg_bytes) *seg_bytes = 0;
+    return 1;  // streaming kernel
+  }
   int g;
   uint32_t s;
   plan(n_blocks, bytes_per_block, true, &g, &s);
   if (lanes_per_unit) *lanes_per_unit = g;
   if (seg_bytes) *seg_bytes = s;
-  return 0;
+  return 0;  // units kernel
+}
+
+int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int variable, char* buf,
+                         size_t buflen) {
+  CrcParams p{};
+  p.base = reinterpret_cast<const uint8_t*>(uintptr_t(256));
+  p.len = (uint32_t)len;
+  p.stride = stride;
+  p.n_blocks = n_blocks;
+  int sg = 0;
+  if (!variable && !g_tune_seg.load() && g_tune_var.load() != kVarNT) sg = stream_lanes(p);
+  int n;
+  if (sg) {
+    n = snprintf(buf, buflen,
+                 "{\"kernel\": \"crc32c_stream_kernel<%d, 0>\", \"lanes_per_block\": %d, "
+                 "\"blocks_per_group\": %u, \"steal_probes\": %d}",
+                 sg, sg, stream_bpg(sg, (uint32_t)len),
+                 g_tune_static_pct.load() < 0 ? 8 : g_tune_static_pct.load());
+  } else {
+    int g;
+    uint32_t s;
+    plan(n_blocks, len, !variable, &g, &s);
+    n = snprintf(buf, buflen,
+                 "{\"kernel\": \"crc32c_units_kernel<%d, 0>\", \"lanes_per_unit\": %d, "
+                 "\"segment_bytes\": %u}", g, g, s);
+  }
+  return n;
 }
 
 const char* nova_crc32c_kernel_name(int lanes_per_unit) {
@@ -936,6 +1156,12 @@ void nova_crc32c_set_tuning(int lanes_per_unit, uint32_t seg_bytes) {
 }
 
 void nova_diag_set_variant(int variant) { g_tune_var.store(variant); }
+
+void nova_diag_set_stamps(uint64_t* dev_stamps) { g_diag_stamps.store(dev_stamps); }
+
+void nova_diag_set_static_pct(int pct) { g_tune_static_pct.store(pct); }
+
+void nova_diag_set_blocks_per_group(int bpg) { g_tune_bpg.store(bpg); }
 
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {

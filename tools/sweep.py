@@ -25,7 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--configs", default="2,4,3")
+    ap.add_argument("--configs", default="2,4")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
     args = ap.parse_args()
     import torch
@@ -37,6 +37,8 @@ def main():
     L.nova_diag_read_stream.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_void_p]
     L.nova_diag_read_stream.restype = ctypes.c_int
+    L.nova_diag_set_static_pct.argtypes = [ctypes.c_int]
+    L.nova_diag_set_blocks_per_group.argtypes = [ctypes.c_int]
     assert L.nova_device_init() == 0
     results = []
 
@@ -63,15 +65,17 @@ def main():
             nbytes = total
             ref = C.batch_strided(buf, Lb, Lb, n).clone()
 
-            def mk(g, seg, var):
+            def mk(g, seg, var, bpg=1):
                 def f():
                     C.set_tuning(g, seg)
                     L.nova_diag_set_variant(var)
+                    L.nova_diag_set_blocks_per_group(bpg)
                     C.batch_strided(buf, Lb, Lb, n, out=out)
                 return f
             # seg 0 -> streaming kernel; seg == block length -> units kernel
-            variants = [(g, 0, v) for g in (2, 4, 8, 16) for v in (0, 1)]
-            variants += [(g, Lb, 0) for g in (4, 8, 16)]
+            variants = [(g, 0, 0, b) for g in (4, 8, 16) for b in (1, 2, 4, 8)]
+            variants += [(g, 0, 1, b) for g in (8, 16) for b in (1, 4)]
+            variants += [(8, Lb, 0, 1)]
         else:
             offs_np, lens_np, total = bench.config3_layout(n, 3)
             buf = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
@@ -82,16 +86,15 @@ def main():
             nbytes = int(lens_np.astype(np.uint64).sum())
             ref = C.batch(buf, offs, lens).clone()
 
-            def mk(g, seg, var):
+            def mk(g, seg, var, steal=0):
                 def f():
                     C.set_tuning(g, seg)
                     L.nova_diag_set_variant(var)
                     C.batch(buf, offs, lens, out=out)
                 return f
-            variants = [(g, s, v) for g in (4, 8, 16) for s in (4096, 8192, 16384, 32768)
-                        for v in (0,)] + [(8, 8192, 1), (16, 16384, 1)]
+            variants = [(g, s, 0, 0) for g in (8, 16) for s in (8192, 16384)]
         rs_out = torch.empty(1 << 22, dtype=torch.int32, device="cuda")
-        stream_variants = [2048, 4096, 8192]
+        stream_variants = [8192]
         times: dict = {}
         for r in range(args.rounds):
             for key in variants:
@@ -108,6 +111,8 @@ def main():
                 assert torch.equal(out, ref), ("mismatch", cfg, key)
         C.set_tuning(0, 0)
         L.nova_diag_set_variant(0)
+        L.nova_diag_set_static_pct(-1)
+        L.nova_diag_set_blocks_per_group(0)
         for key, ts in times.items():
             t = statistics.median(ts)
             b = nbytes if key[0] == "units" else (buf.numel() // 16) * 16
