@@ -48,7 +48,7 @@ def main():
     }
     if algo:
         res["read_over_algorithmic"] = res["hbm_read_bytes_per_launch"] / algo
-    out = os.path.join(ROOT, "profiles", f"pmc_config{cfg}.json")
+    out = os.path.join(ROOT, os.environ.get("PMC_OUT_DIR", "profiles"), f"pmc_config{cfg}.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
