@@ -281,3 +281,121 @@ def test_baseline_config3_sampled(torch_gpu, oracle):
         o, l = int(offs[i]), int(lens[i])
         want.append(oracle.value(buf[o:o + l].cpu().numpy().tobytes()))
     assert np.array_equal(out[idx], np.array(want, np.uint32))
+
+
+@pytest.mark.parametrize("length", [256, 1024, 2048, 4096, 8192, 16384, 65536])
+@pytest.mark.parametrize("n", [1, 7, 100, 4099])
+def test_stream_kernel_shapes(torch_gpu, oracle, length, n):
+    """Aligned uniform batches go through crc32c_stream_kernel: ragged tail rounds,
+    batches smaller than one round, init arrays and flags."""
+    torch = torch_gpu
+    d = C.describe(n, length, length)
+    assert d["kernel"].startswith("crc32c_stream_kernel"), d
+    host = splitmix64_bytes(length + n, n * length)
+    buf = dev(torch, host)
+    rng = np.random.default_rng(n)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    for flags, ini in [(0, None), (0, init), (C.APPEND_TYPE | C.TYPE(0) | C.MASK_OUTPUT, init),
+                       (C.RAW, None)]:
+        out = C.batch_strided(buf, length, length, n, flags=flags,
+                              init=None if ini is None else dev(torch, ini.view(np.int32)))
+        if flags & C.RAW:
+            want = oracle.batch_strided(host, length, length, n,
+                                        init=np.full(n, 0xFFFFFFFF, np.uint32)) ^ np.uint32(
+                0xFFFFFFFF)
+        else:
+            want = oracle.batch_strided(host, length, length, n, init=ini, flags=flags)
+        assert np.array_equal(u32(out), want), (flags, length, n)
+
+
+@pytest.mark.parametrize("lanes,bpg,steal", [(1, 1, 0), (2, 3, 1), (4, 2, 8), (8, 1, 8),
+                                             (8, 4, 0), (16, 2, 255), (16, 1, 8)])
+def test_stream_kernel_tuning_variants(torch_gpu, oracle, lanes, bpg, steal):
+    torch = torch_gpu
+    import ctypes
+    L = C.load()
+    L.nova_diag_set_static_pct.argtypes = [ctypes.c_int]
+    L.nova_diag_set_blocks_per_group.argtypes = [ctypes.c_int]
+    try:
+        C.set_tuning(lanes, 0)
+        L.nova_diag_set_blocks_per_group(bpg)
+        L.nova_diag_set_static_pct(steal)
+        n, length = 30011, 4096
+        buf = torch.empty(n * length, dtype=torch.uint8, device="cuda")
+        C.fill_splitmix64(buf, 77)
+        out = u32(C.batch_strided(buf, length, length, n))
+        want = oracle.batch_strided_mt(buf.cpu().numpy(), length, length, n, threads=8)
+        assert np.array_equal(out, want)
+    finally:
+        L.nova_diag_set_blocks_per_group(0)
+        L.nova_diag_set_static_pct(-1)
+
+
+def test_pinned_host_zero_copy(torch_gpu, oracle, golden):
+    """Kernels read (and the trailer writer writes) pinned host memory directly:
+    the RDMA-registered backing_mem_ integration of INTEGRATION.md 3a."""
+    torch = torch_gpu
+    n, length = 2000, 4096
+    host = torch.empty(n * length, dtype=torch.uint8).pin_memory()
+    host.copy_(torch.from_numpy(splitmix64_bytes(9, n * length)))
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    rc = C.load().nova_crc32c_batch_strided(host.data_ptr(), length, length, n, None,
+                                            out.data_ptr(), 0, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(u32(out), oracle.batch_strided(host.numpy(), length, length, n))
+    # trailers written in place into pinned host memory
+    pk = golden["packed"]
+    img = torch.from_numpy(splitmix64_bytes(pk["seed"], pk["total"])).pin_memory()
+    offs = dev(torch, np.array(pk["offsets"], np.uint64), torch.int64)
+    sizes = dev(torch, np.array(pk["sizes"], np.uint32), torch.int32)
+    rc = C.load().nova_sstable_write_trailers(img.data_ptr(), offs.data_ptr(), sizes.data_ptr(),
+                                              len(pk["sizes"]), C.TYPE(0) | C.TB_QUIRK, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    h = img.numpy()
+    for o, s, tb in zip(pk["offsets"], pk["sizes"], pk["tb_trailer_hex"]):
+        assert h[o + s:o + s + 5].tobytes().hex() == tb
+
+
+def test_concurrent_host_threads(torch_gpu, oracle):
+    """Reentrancy (SURVEY 8(b) Threading): several host threads, each on its own
+    HIP stream, checksum different batches at the same time."""
+    torch = torch_gpu
+    import threading
+    n, length = 20000, 4096
+    bufs = []
+    for t in range(6):
+        b = torch.empty(n * length, dtype=torch.uint8, device="cuda")
+        C.fill_splitmix64(b, 100 + t)
+        bufs.append(b)
+    torch.cuda.synchronize()
+    results = [None] * 6
+    errors = []
+
+    def work(t):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                outs = []
+                for _ in range(5):
+                    outs.append(C.batch_strided(bufs[t], length, length, n, stream=s))
+                    outs.append(C.batch(bufs[t], torch.arange(0, n * length, length,
+                                                              device="cuda", dtype=torch.int64),
+                                        torch.full((n,), length, device="cuda",
+                                                   dtype=torch.int32), stream=s))
+            s.synchronize()
+            results[t] = [u32(o) for o in outs]
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(6)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    for t in range(6):
+        want = oracle.batch_strided_mt(bufs[t].cpu().numpy(), length, length, n, threads=8)
+        for r in results[t]:
+            assert np.array_equal(r, want)
