@@ -112,6 +112,26 @@ int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const u
                                size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
                                void* stream);
 
+/* ---- MANIFEST / write-ahead log records ----------
+ * record_offsets[i] points at a log record header [LE32 masked crc][LE16
+ * length][type] (db/log_format.h:27-30) followed by `length` payload bytes.
+ * Write: header crc = Mask(Extend(type_crc[type], payload, length)) --
+ * db/log_writer.cc:99-114 (type_crc[t] = Value(&t, 1), :16-21), computed as
+ * Value(header+6, 1+length).  Verify: ok_out[i] = Unmask(stored) ==
+ * Value(header+6, 1+length) -- db/log_reader.cc:251-262 ("checksum mismatch"). */
+int nova_log_write_crcs(void* buf, const uint64_t* record_offsets, size_t n_records,
+                        void* stream);
+int nova_log_verify_records(const void* buf, const uint64_t* record_offsets, size_t n_records,
+                            uint8_t* ok_out, uint32_t* n_bad_out, void* stream);
+
+/* ---- XOR parity block ------------------------------
+ * out[i] = XOR over fragments f of base[frag_offsets[f] + i], i < parity_len
+ * (device pointers).  Replaces the byte-at-a-time host loop of
+ * StoCWritableFileClient::Format, ltc/stoc_file_client_impl.cpp:334-349,
+ * including its reading of parity_len bytes from every fragment start. */
+int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_frags,
+                    size_t parity_len, void* out, void* stream);
+
 /* ---- host-resident streamed path (BASELINE config 5) --------------------
  * Blocks live in HOST memory (pinned or pageable; the analogue of NovaLSM's
  * RDMA-registered backing_mem_, ltc/stoc_file_client_impl.cpp:43-45).  The

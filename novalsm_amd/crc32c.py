@@ -65,6 +65,9 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
         "nova_sstable_write_trailers": (i32, [vp, vp, vp, sz, u32, vp]),
         "nova_sstable_verify_blocks": (i32, [vp, vp, vp, sz, vp, vp, vp]),
         "nova_crc32c_stream_host": (i32, [vp, u64, u32, sz, vp, u32, sz, i32]),
+        "nova_log_write_crcs": (i32, [vp, vp, sz, vp]),
+        "nova_log_verify_records": (i32, [vp, vp, sz, vp, vp, vp]),
+        "nova_xor_parity": (i32, [vp, vp, sz, sz, vp, vp]),
         "nova_fill_splitmix64": (i32, [vp, sz, u64, u64, vp]),
         "nova_device_init": (i32, []),
         "nova_crc32c_plan": (i32, [sz, u64, ctypes.POINTER(i32), ctypes.POINTER(u32)]),
@@ -198,6 +201,40 @@ def verify_blocks(buf, offsets, sizes, stream=None):
                                            _ptr(bad), _stream_ptr(stream))
     _check(rc, "nova_sstable_verify_blocks")
     return ok, bad
+
+
+def log_write_crcs(buf, record_offsets, stream=None):
+    """db/log_writer.cc:99-114 for every record header at record_offsets (in place)."""
+    _require_gpu()
+    rc = load().nova_log_write_crcs(_ptr(buf), _ptr(record_offsets), int(record_offsets.numel()),
+                                    _stream_ptr(stream))
+    _check(rc, "nova_log_write_crcs")
+    return buf
+
+
+def log_verify_records(buf, record_offsets, stream=None):
+    """db/log_reader.cc:251-262 per record -> (ok uint8 tensor, n_bad int32 tensor[1])."""
+    import torch
+    _require_gpu()
+    n = int(record_offsets.numel())
+    ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
+    bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    rc = load().nova_log_verify_records(_ptr(buf), _ptr(record_offsets), n, _ptr(ok), _ptr(bad),
+                                        _stream_ptr(stream))
+    _check(rc, "nova_log_verify_records")
+    return ok, bad
+
+
+def xor_parity(buf, frag_offsets, parity_len: int, out=None, stream=None):
+    """ltc/stoc_file_client_impl.cpp:334-349 XOR parity block over fragments."""
+    import torch
+    _require_gpu()
+    if out is None:
+        out = torch.empty(parity_len, dtype=torch.uint8, device=buf.device)
+    rc = load().nova_xor_parity(_ptr(buf), _ptr(frag_offsets), int(frag_offsets.numel()),
+                                parity_len, _ptr(out), _stream_ptr(stream))
+    _check(rc, "nova_xor_parity")
+    return out
 
 
 def stream_host(host_u8, stride: int, length: int, n_blocks: int, flags: int = 0,

@@ -57,7 +57,10 @@ constexpr uint32_t kTreeBytes = 4096;      // per level
 constexpr uint32_t kWaveScratch = 512;     // per wave: 64 prefix + 64 accumulators
 constexpr int kNumG = 5;                   // G = 1, 2, 4, 8, 16
 
-enum Mode { kStore = 0, kTrailer = 1, kVerify = 2 };
+// kLogWrite / kLogVerify: offsets[i] points at a log record header
+// [LE32 masked crc][LE16 length][type] (db/log_format.h:27-30); the CRC covers
+// type byte + payload (db/log_writer.cc:112-114, db/log_reader.cc:251-262).
+enum Mode { kStore = 0, kTrailer = 1, kVerify = 2, kLogWrite = 3, kLogVerify = 4 };
 
 struct CrcParams {
   const uint8_t* base;
@@ -350,7 +353,13 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
     uint32_t n = 0, init = 0;
     if (valid) {
       a = (uint64_t)p.base + (p.offsets ? p.offsets[b] : b * p.stride);
-      n = (p.lengths ? p.lengths[b] : p.len) + extra;
+      if (MODE == kLogWrite || MODE == kLogVerify) {
+        const uint8_t* h = (const uint8_t*)a;  // record header
+        n = 1u + ((uint32_t)h[4] | ((uint32_t)h[5] << 8));
+        a += 6;  // CRC input starts at the type byte
+      } else {
+        n = (p.lengths ? p.lengths[b] : p.len) + extra;
+      }
       init = p.init ? p.init[b] : 0u;
     }
     const uint32_t ninit = raw ? 0u : ~init;
@@ -425,7 +434,22 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
     // -- epilogue: lane i finalises block b
     if (valid) {
       uint32_t crc = (n >= 4) ? (raw ? wacc[lane] : ~wacc[lane]) : small_crc;
-      if (MODE == kVerify) {
+      if (MODE == kLogWrite || MODE == kLogVerify) {
+        uint8_t* h = (uint8_t*)a - 6;
+        const uint32_t m = mask_crc(crc);  // db/log_writer.cc:113
+        if (MODE == kLogWrite) {
+          h[0] = (uint8_t)m;
+          h[1] = (uint8_t)(m >> 8);
+          h[2] = (uint8_t)(m >> 16);
+          h[3] = (uint8_t)(m >> 24);
+        } else {
+          const uint32_t stored = (uint32_t)h[0] | ((uint32_t)h[1] << 8) |
+                                  ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+          const bool ok = unmask_crc(stored) == crc;  // db/log_reader.cc:254-256
+          p.ok_out[b] = ok ? 1 : 0;
+          if (!ok && p.n_bad) atomicAdd(p.n_bad, 1u);
+        }
+      } else if (MODE == kVerify) {
         const uint8_t* d = (const uint8_t*)a;
         const uint32_t stored = (uint32_t)d[n] | ((uint32_t)d[n + 1] << 8) |
                                 ((uint32_t)d[n + 2] << 16) | ((uint32_t)d[n + 3] << 24);
@@ -680,6 +704,52 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   }
 }
 
+// XOR parity block over k data fragments (ltc/stoc_file_client_impl.cpp:334-349):
+// parity[i] = XOR_f mem[frag_off[f] + i] for i < parity_len.  Like the
+// reference, every fragment contributes parity_len bytes from its start (the
+// reference loop reads past a shorter fragment's end).  Each thread makes 16
+// output bytes; a fragment's misalignment s is wave-uniform, so unaligned
+// fragments cost one extra aligned load + v_alignbyte funnel shifts.
+__global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, const uint64_t* frag_off,
+                                                         uint32_t n_frags, uint64_t parity_len,
+                                                         uint8_t* out) {
+  const uint64_t nchunks = (parity_len + 15) / 16;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += stride) {
+    uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
+    for (uint32_t f = 0; f < n_frags; f++) {
+      const uint64_t addr = (uint64_t)base + frag_off[f] + 16 * c;
+      const uint32_t s = (uint32_t)(addr & 15);
+      const uint4 lo = gload16(addr - s);
+      if (s == 0) {
+        x0 ^= lo.x; x1 ^= lo.y; x2 ^= lo.z; x3 ^= lo.w;
+      } else {
+        const uint4 hi = gload16(addr - s + 16);
+        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const uint32_t ws = s >> 2, bs = s & 3;
+        uint32_t r[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          // select W[k+ws], W[k+ws+1] without dynamic register indexing
+          uint32_t a = w[k], b = w[k + 1];
+          if (ws == 1) { a = w[k + 1]; b = w[k + 2]; }
+          else if (ws == 2) { a = w[k + 2]; b = w[k + 3]; }
+          else if (ws == 3) { a = w[k + 3]; b = w[k + 4]; }
+          r[k] = __builtin_amdgcn_alignbyte(b, a, bs);
+        }
+        x0 ^= r[0]; x1 ^= r[1]; x2 ^= r[2]; x3 ^= r[3];
+      }
+    }
+    const uint64_t o = 16 * c;
+    if (o + 16 <= parity_len) {
+      *reinterpret_cast<uint4*>(out + o) = make_uint4(x0, x1, x2, x3);
+    } else {
+      const uint32_t v[4] = {x0, x1, x2, x3};
+      for (uint64_t i = o; i < parity_len; i++) out[i] = (uint8_t)(v[(i - o) >> 2] >> (8 * ((i - o) & 3)));
+    }
+  }
+}
+
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
 __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                        uint64_t first_word) {
@@ -849,6 +919,8 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;
+  if ((t->err = set_lds_attrs_mode<kLogWrite>())) return;
+  if ((t->err = set_lds_attrs_mode<kLogVerify>())) return;
   if ((t->err = set_lds_attrs_mode<kStore, kVarNoLookup>())) return;
   if ((t->err = set_lds_attrs_mode<kStore, kVarNT>())) return;
   if ((t->err = set_lds_attrs_stream<0>())) return;
@@ -1007,6 +1079,8 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   switch (mode) {
     case kStore: return launch_mode<kStore>(G, p, t, stream);
     case kTrailer: return launch_mode<kTrailer>(G, p, t, stream);
+    case kLogWrite: return launch_mode<kLogWrite>(G, p, t, stream);
+    case kLogVerify: return launch_mode<kLogVerify>(G, p, t, stream);
     default: return launch_mode<kVerify>(G, p, t, stream);
   }
 }
@@ -1076,6 +1150,45 @@ int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const u
   p.n_bad = n_bad_out;
   p.n_blocks = n_blocks;
   return run(kVerify, p, false, 0, (hipStream_t)stream);
+}
+
+int nova_log_write_crcs(void* buf, const uint64_t* record_offsets, size_t n_records,
+                        void* stream) {
+  if (n_records && (!buf || !record_offsets)) return NOVA_E_INVAL;
+  CrcParams p{};
+  p.base = (const uint8_t*)buf;
+  p.offsets = record_offsets;
+  p.n_blocks = n_records;
+  return run(kLogWrite, p, false, 0, (hipStream_t)stream);
+}
+
+int nova_log_verify_records(const void* buf, const uint64_t* record_offsets, size_t n_records,
+                            uint8_t* ok_out, uint32_t* n_bad_out, void* stream) {
+  if (n_records && (!buf || !record_offsets || !ok_out)) return NOVA_E_INVAL;
+  CrcParams p{};
+  p.base = (const uint8_t*)buf;
+  p.offsets = record_offsets;
+  p.ok_out = ok_out;
+  p.n_bad = n_bad_out;
+  p.n_blocks = n_records;
+  return run(kLogVerify, p, false, 0, (hipStream_t)stream);
+}
+
+int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_frags,
+                    size_t parity_len, void* out, void* stream) {
+  if (!parity_len) return 0;
+  if (!base || !frag_offsets || !out || n_frags == 0 || n_frags > 0xffffffffu) return NOVA_E_INVAL;
+  int err = 0;
+  DevTables* t = tables(&err);
+  if (!t) return err;
+  uint64_t chunks = (parity_len + 15) / 16;
+  uint64_t wgs = (chunks + 255) / 256;
+  const uint64_t cap = (uint64_t)t->cus * 8;
+  if (wgs > cap) wgs = cap;
+  hipLaunchKernelGGL(xor_parity_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)base, frag_offsets, (uint32_t)n_frags, (uint64_t)parity_len,
+                     (uint8_t*)out);
+  return (int)hipGetLastError();
 }
 
 int nova_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t first_word,

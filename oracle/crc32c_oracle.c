@@ -205,6 +205,37 @@ int oracle_verify(const uint8_t *data, size_t n) {
   return oracle_value(data, n + 1) == want;
 }
 
+/* db/log_writer.cc:99-114 EmitPhysicalRecord: header crc =
+ * Mask(Extend(type_crc_[t], payload, length)), type_crc_[t] = Value(&t, 1)
+ * (db/log_writer.cc:16-21).  Writes the 4 crc bytes of the header at rec. */
+void oracle_log_write(uint8_t *rec) {
+  uint32_t len = (uint32_t)rec[4] | ((uint32_t)rec[5] << 8);
+  uint8_t t = rec[6];
+  uint32_t crc = oracle_mask(oracle_extend(oracle_value(&t, 1), rec + 7, len));
+  rec[0] = (uint8_t)crc;
+  rec[1] = (uint8_t)(crc >> 8);
+  rec[2] = (uint8_t)(crc >> 16);
+  rec[3] = (uint8_t)(crc >> 24);
+}
+
+/* db/log_reader.cc:251-262: Unmask(DecodeFixed32(header)) == Value(header+6, 1+length). */
+int oracle_log_verify(const uint8_t *rec) {
+  uint32_t len = (uint32_t)rec[4] | ((uint32_t)rec[5] << 8);
+  return oracle_unmask(read_le32(rec)) == oracle_value(rec + 6, 1 + len);
+}
+
+/* ltc/stoc_file_client_impl.cpp:340-348: parity[i] = XOR over fragments of
+ * backing_mem_[fragment.offset() + i] for i < parity_block_size_ (every
+ * fragment contributes parity_len bytes from its start). */
+void oracle_xor_parity(const uint8_t *base, const uint64_t *frag_off, size_t n_frags,
+                       size_t parity_len, uint8_t *out) {
+  for (size_t i = 0; i < parity_len; i++) {
+    uint8_t b = 0;
+    for (size_t f = 0; f < n_frags; f++) b ^= base[frag_off[f] + i];
+    out[i] = b;
+  }
+}
+
 /* Multi-threaded strided batch for the CPU baseline ("port" kind): one
  * pthread per core on contiguous shards, as BASELINE.md's CPU plan says. */
 struct shard_arg {

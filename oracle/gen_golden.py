@@ -133,7 +133,29 @@ def main() -> None:
     out["packed"] = {"seed": seed, "total": total, "offsets": offs, "sizes": sizes,
                      "crc": crcs, "tb_trailer_hex": tb, "stoc_trailer_hex": stoc}
 
-    # 7. BASELINE config 1 sample: 1024 x 4 KiB blocks, splitmix64 seed 1
+    # 7. a write-ahead/MANIFEST log image: records [LE32 masked crc][LE16 len]
+    # [type][payload] whose crc is db/log_writer.cc:112-114:
+    # Mask(Extend(type_crc[t], payload, len)), type_crc[t] = Value(&t, 1) (:16-21).
+    r = np.random.default_rng(4)
+    recs, pos = [], 0
+    for i in range(300):
+        ln = int(r.integers(0, 3000)) if i % 11 else int(r.integers(0, 4))
+        t = int(r.integers(1, 5))
+        recs.append((pos, ln, t))
+        pos += 7 + ln
+    logbuf = bytearray(splitmix64_bytes(6, pos).tobytes())
+    log_crc = []
+    for o, ln, t in recs:
+        logbuf[o + 4] = ln & 0xff
+        logbuf[o + 5] = ln >> 8
+        logbuf[o + 6] = t
+        c = ref.ref_mask(ext(ext(0, bytes([t])), bytes(logbuf[o + 7:o + 7 + ln])))
+        log_crc.append(c)
+        logbuf[o:o + 4] = c.to_bytes(4, "little")
+    out["log"] = {"seed": 6, "total": pos, "records": [[o, ln, t] for o, ln, t in recs],
+                  "header_crc": log_crc}
+
+    # 8. BASELINE config 1 sample: 1024 x 4 KiB blocks, splitmix64 seed 1
     data = splitmix64_bytes(1, 1024 * 4096).tobytes()
     c1 = [ext(0, data[i * 4096:(i + 1) * 4096]) for i in range(1024)]
     out["config1"] = {"seed": 1, "n": 1024, "len": 4096, "crc": c1}

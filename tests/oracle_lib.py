@@ -49,6 +49,12 @@ class Oracle:
         lib.oracle_verify.argtypes = [ctypes.c_char_p, sz]
         lib.oracle_fill_splitmix64.restype = None
         lib.oracle_fill_splitmix64.argtypes = [vp, sz, u64, u64]
+        lib.oracle_log_write.restype = None
+        lib.oracle_log_write.argtypes = [vp]
+        lib.oracle_log_verify.restype = ctypes.c_int
+        lib.oracle_log_verify.argtypes = [vp]
+        lib.oracle_xor_parity.restype = None
+        lib.oracle_xor_parity.argtypes = [vp, vp, sz, sz, vp]
         lib.oracle_tables.restype = None
         lib.oracle_tables.argtypes = [vp, vp]
 
@@ -104,6 +110,21 @@ class Oracle:
     def splitmix64(self, nbytes: int, seed: int, first_word: int = 0) -> np.ndarray:
         out = np.empty(nbytes, dtype=np.uint8)
         self.lib.oracle_fill_splitmix64(out.ctypes.data, nbytes, seed, first_word)
+        return out
+
+    def log_write(self, buf: np.ndarray, rec_offsets) -> None:
+        for o in rec_offsets:
+            self.lib.oracle_log_write(buf.ctypes.data + int(o))
+
+    def log_verify(self, buf: np.ndarray, rec_offsets) -> np.ndarray:
+        return np.array([self.lib.oracle_log_verify(buf.ctypes.data + int(o))
+                         for o in rec_offsets], dtype=np.uint8)
+
+    def xor_parity(self, buf: np.ndarray, frag_offsets, parity_len: int) -> np.ndarray:
+        fo = np.ascontiguousarray(frag_offsets, dtype=np.uint64)
+        out = np.empty(parity_len, dtype=np.uint8)
+        self.lib.oracle_xor_parity(buf.ctypes.data, fo.ctypes.data, len(fo), parity_len,
+                                   out.ctypes.data)
         return out
 
     def tables(self):

@@ -399,3 +399,50 @@ def test_concurrent_host_threads(torch_gpu, oracle):
         want = oracle.batch_strided_mt(bufs[t].cpu().numpy(), length, length, n, threads=8)
         for r in results[t]:
             assert np.array_equal(r, want)
+
+
+def _log_image(golden):
+    lg = golden["log"]
+    buf = splitmix64_bytes(lg["seed"], lg["total"]).copy()
+    for (o, ln, t) in lg["records"]:
+        buf[o + 4] = ln & 0xFF
+        buf[o + 5] = ln >> 8
+        buf[o + 6] = t
+    return buf, np.array([r[0] for r in lg["records"]], np.uint64)
+
+
+def test_log_records_write_verify(torch_gpu, golden, oracle):
+    """MANIFEST/WAL record CRCs (db/log_writer.cc:99-114,
+    db/log_reader.cc:251-262) against the reference-generated log fixture."""
+    torch = torch_gpu
+    host, offs = _log_image(golden)
+    buf = dev(torch, host)
+    doffs = dev(torch, offs, torch.int64)
+    C.log_write_crcs(buf, doffs)
+    h = buf.cpu().numpy()
+    for o, c in zip(offs, golden["log"]["header_crc"]):
+        assert int.from_bytes(h[int(o):int(o) + 4].tobytes(), "little") == c
+    ok, bad = C.log_verify_records(buf, doffs)
+    assert ok.cpu().numpy().all() and int(bad.item()) == 0
+    victims = [3, 50, 299]
+    for v in victims:
+        o = int(offs[v]) + 6  # corrupt the type byte (covered by the crc)
+        buf[o] ^= 0x01
+    ok, bad = C.log_verify_records(buf, doffs)
+    assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == victims
+    assert int(bad.item()) == 3
+    assert np.array_equal(ok.cpu().numpy(), oracle.log_verify(buf.cpu().numpy(), offs))
+
+
+@pytest.mark.parametrize("align", [True, False])
+@pytest.mark.parametrize("plen", [1, 15, 16, 4096, 100003])
+def test_xor_parity(torch_gpu, oracle, align, plen):
+    """XOR parity block (ltc/stoc_file_client_impl.cpp:334-349)."""
+    torch = torch_gpu
+    rng = np.random.default_rng(plen)
+    k = 5
+    host = splitmix64_bytes(plen, k * (plen + 64) + 64)
+    offs = np.array([f * (plen + 64) + (0 if align else int(rng.integers(0, 16)))
+                     for f in range(k)], np.uint64)
+    out = C.xor_parity(dev(torch, host), dev(torch, offs, torch.int64), plen)
+    assert np.array_equal(out.cpu().numpy(), oracle.xor_parity(host, offs, plen))

@@ -129,3 +129,28 @@ def test_alignment_independence(oracle, n):
         shifted = np.zeros(n + 16, dtype=np.uint8)
         shifted[off:off + n] = base[:n]
         assert oracle.value(shifted[off:off + n].tobytes()) == want
+
+
+def test_log_fixture(oracle, golden):
+    # db/log_writer.cc:99-114 / db/log_reader.cc:251-262 through the oracle
+    lg = golden["log"]
+    buf = splitmix64_bytes(lg["seed"], lg["total"]).copy()
+    for (o, ln, t) in lg["records"]:
+        buf[o + 4] = ln & 0xFF
+        buf[o + 5] = ln >> 8
+        buf[o + 6] = t
+    offs = [r[0] for r in lg["records"]]
+    oracle.log_write(buf, offs)
+    for (o, _, _), c in zip(lg["records"], lg["header_crc"]):
+        assert int.from_bytes(buf[o:o + 4].tobytes(), "little") == c
+    assert oracle.log_verify(buf, offs).all()
+
+
+def test_xor_parity_oracle():
+    from tests.oracle_lib import load_oracle
+    orc = load_oracle()
+    buf = splitmix64_bytes(8, 10000)
+    offs = [0, 1003, 5001]
+    par = orc.xor_parity(buf, offs, 3000)
+    want = buf[0:3000] ^ buf[1003:4003] ^ buf[5001:8001]
+    assert np.array_equal(par, want)
