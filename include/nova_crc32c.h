@@ -176,6 +176,8 @@ void nova_diag_set_stamps(uint64_t* dev_stamps);
 void nova_diag_set_static_pct(int steal_probes);
 /* Streaming kernel: consecutive blocks per lane group per round (default 1). */
 void nova_diag_set_blocks_per_group(int bpg);
+/* Units kernel: blocks per claimed wave chunk (1..16, default 8; 0 = default). */
+void nova_diag_set_chunk_blocks(int blocks);
 /* Plain coalesced streaming read of `bytes` (multiple of 16) with `wgs`
  * 256-thread workgroups; out_dev receives wgs*256 words.  The chip's read
  * ceiling for the roofline discussion. */

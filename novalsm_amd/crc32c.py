@@ -76,6 +76,10 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
         "nova_crc32c_set_tuning": (None, [i32, u32]),
         "nova_error_string": (ctypes.c_char_p, [i32]),
         "nova_crc32c_abi_version": (i32, []),
+        "nova_diag_set_variant": (None, [i32]),
+        "nova_diag_set_static_pct": (None, [i32]),
+        "nova_diag_set_blocks_per_group": (None, [i32]),
+        "nova_diag_set_chunk_blocks": (None, [i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -54,7 +54,7 @@ constexpr int kThreads = kWaves * 64;
 constexpr uint32_t kMainBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 B
 constexpr int kTreeLevels = 6;             // M4, M8, M16, M32, M64, M128
 constexpr uint32_t kTreeBytes = 4096;      // per level
-constexpr uint32_t kWaveScratch = 512;     // per wave: 64 prefix + 64 accumulators
+constexpr uint32_t kWaveScratch = 512;     // per wave: 2x16 prefixes (+pad) + accumulators
 constexpr int kNumG = 5;                   // G = 1, 2, 4, 8, 16
 
 // kLogWrite / kLogVerify: offsets[i] points at a log record header
@@ -76,7 +76,7 @@ struct CrcParams {
   uint32_t* n_bad;           // kVerify, may be null
   uint64_t n_blocks;
   uint32_t seg;              // segment bytes (multiple of 16); 0 = one unit per block
-  uint32_t chunk;            // blocks per wave chunk (<= 64)
+  uint32_t chunk;            // blocks per wave chunk (<= 16)
   uint64_t n_chunks;
   const uint32_t* tab_main;  // replicated LDS image, 32768 u32
   const uint32_t* tab_tree;  // kTreeLevels x 1024 u32
@@ -344,9 +344,32 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
   const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
   const uint32_t extra = (MODE == kVerify) ? 1u : 0u;  // verify covers block + type byte
 
-  for (uint64_t chunk = (uint64_t)blockIdx.x * kWaves + wave; chunk < p.n_chunks;
-       chunk += (uint64_t)gridDim.x * kWaves) {
-    // -- prologue: lane i owns block b = chunk*chunk_size + i
+  // Chunks of p.chunk (<= 16) blocks.  Workgroup w owns the interleaved chunks
+  // w, w+nwg, ... and its waves claim them from a per-workgroup counter (one
+  // relaxed device-scope atomic per chunk); a wave whose workgroup ran out
+  // steals from up to p.steal_limit other workgroups.  Wave k's first chunk is
+  // implicit.  (Static chunk assignment left the tail unbalanced, as measured
+  // for the streaming kernel in DESIGN.md 3.3.)
+  const uint32_t nwg = gridDim.x;
+  uint32_t victim = blockIdx.x, tried = 0;
+  uint64_t chunk = (uint64_t)wave * nwg + blockIdx.x;
+  auto next_chunk = [&]() -> uint64_t {
+    for (;;) {
+      uint32_t idx = 0;
+      if (lane == 0)
+        idx = __hip_atomic_fetch_add(p.sched + victim * 16, 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+      idx = __builtin_amdgcn_readfirstlane(idx);
+      const uint64_t c = ((uint64_t)idx + kWaves) * nwg + victim;
+      if (c < p.n_chunks) return c;
+      if (++tried >= p.steal_limit + 1) return ~0ull;
+      victim = (victim + 1) % nwg;
+    }
+  };
+  if (chunk >= p.n_chunks) chunk = next_chunk();
+
+  for (; chunk != ~0ull; chunk = next_chunk()) {
+    // -- prologue: lane i < chunk owns block b = chunk*chunk_size + i
     const uint64_t b = chunk * p.chunk + lane;
     const bool valid = lane < (int)p.chunk && b < p.n_blocks;
     uint64_t a = 0;
@@ -363,27 +386,41 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
       init = p.init ? p.init[b] : 0u;
     }
     const uint32_t ninit = raw ? 0u : ~init;
-    uint32_t nq = 0;
+    // Units: blocks >= seg bytes are cut into floor(n/seg) segments ("big"
+    // units, seg..2seg-1 bytes); shorter blocks are one "small" unit.  Rounds
+    // take all big units first, then the small ones, so a round rarely mixes
+    // sizes (a round lasts as long as its longest unit).
+    uint32_t nq_big = 0, nq_small = 0;
     uint32_t small_crc = 0;
     if (valid) {
       if (n >= 4) {
-        nq = p.seg ? (n / p.seg > 0 ? n / p.seg : 1u) : 1u;
+        if (p.seg == 0) nq_big = 1;
+        else if (n >= p.seg) nq_big = n / p.seg;
+        else nq_small = 1;
       } else {  // tiny block: bytewise on this lane
         uint32_t l = ninit;
         for (uint32_t i = 0; i < n; i++) l = byte_step(l, ((const uint8_t*)a)[i]);
         small_crc = raw ? l : ~l;
       }
     }
-    // inclusive prefix of unit counts over the wave
-    uint32_t incl = nq;
+    const uint32_t nq = nq_big + nq_small;
+    // inclusive prefixes of big and small unit counts over the chunk's lanes
+    uint32_t ib = nq_big, is = nq_small;
 #pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-      const uint32_t o = __shfl_up(incl, s);
-      if (lane >= s) incl += o;
+    for (int s = 1; s < 16; s <<= 1) {
+      const uint32_t ob = __shfl_up(ib, s), os = __shfl_up(is, s);
+      if ((lane & 15) >= s) {
+        ib += ob;
+        is += os;
+      }
     }
-    const uint32_t total = __shfl(incl, 63);
-    wpre[lane] = incl;
-    wacc[lane] = 0;
+    const uint32_t total_big = __shfl(ib, 15);
+    const uint32_t total = total_big + __shfl(is, 15);
+    if (lane < 16) {
+      wpre[lane] = ib;
+      wpre[16 + lane] = is;
+      wacc[lane] = 0;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -392,19 +429,22 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
     for (uint32_t r0 = 0; r0 < total; r0 += kGroups) {
       const uint32_t u = r0 + grp;
       const bool active = u < total;
+      const bool big = u < total_big;
+      const uint32_t uu = big ? u : u - total_big;
+      const uint32_t* pre = big ? wpre : wpre + 16;
       int i = 0;
 #pragma unroll
-      for (int s = 32; s > 0; s >>= 1)
-        if (wpre[i + s - 1] <= u) i += s;
+      for (int s = 8; s > 0; s >>= 1)
+        if (pre[i + s - 1] <= uu) i += s;
       if (!active) i = 0;
       const uint32_t a_lo = __shfl((uint32_t)a, i);
       const uint32_t a_hi = __shfl((uint32_t)(a >> 32), i);
       const uint32_t bn = __shfl(n, i);
       const uint32_t bq = __shfl(nq, i);
       const uint32_t binit = __shfl(ninit, i);
-      const uint32_t bincl = wpre[i];
+      const uint32_t bincl = pre[i];
       const uint64_t ba = ((uint64_t)a_hi << 32) | a_lo;
-      const uint32_t j = bincl - 1 - u;  // 0 = last unit of the block
+      const uint32_t j = big ? bincl - 1 - uu : 0u;  // 0 = last unit of the block
       uint64_t u0 = 0, u1 = 0;
       uint32_t uinit = 0;
       if (active) {
@@ -417,7 +457,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
       const uint32_t v = unit_pending<G, VAR>(lds, u0, u1, uinit, q, lo0, lo1, lo2, lo3);
       if (active && q == 0) {
         const uint32_t t = (uint32_t)((16 - (u1 & 15)) & 15);
-        uint32_t c = gapply(p.tab_ft + t * 1024, v);
+        uint32_t c = t ? gapply(p.tab_ft + t * 1024, v) : tapply(lds, 0, v);  // M4 in LDS
         uint64_t m = (uint64_t)(p.seg >> 4) * j;  // shift in 16-byte units
         while (m) {
           const int bit = __builtin_ctzll(m);
@@ -818,6 +858,7 @@ std::once_flag g_once[kMaxDevices];
 std::atomic<int> g_tune_g{0};
 std::atomic<int> g_tune_var{0};
 std::atomic<int> g_tune_bpg{0};
+std::atomic<int> g_tune_chunk{0};
 std::atomic<uint64_t*> g_diag_stamps{nullptr};
 std::atomic<uint32_t> g_tune_seg{0};
 
@@ -978,11 +1019,23 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   p.tab_tree = t->tree;
   p.tab_ft = t->ft;
   p.tab_sh16 = t->sh16;
-  p.chunk = 64;
+  {
+    const int ch = g_tune_chunk.load();
+    p.chunk = (ch > 0 && ch <= 16) ? (uint32_t)ch : 8u;
+  }
   p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
   uint64_t wgs = (p.n_chunks + kWaves - 1) / kWaves;
   if (wgs > (uint64_t)t->cus) wgs = t->cus;
+  if (wgs > 256) wgs = 256;
   if (wgs == 0) return 0;
+  {
+    const int sl = g_tune_static_pct.load();
+    p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;
+  }
+  const uint64_t slot = g_sched_ticket.fetch_add(1) % kSchedSlots;
+  p.sched = t->sched + slot * kSchedWords;
+  hipError_t e = hipMemsetAsync(p.sched, 0, wgs * 64, stream);
+  if (e != hipSuccess) return (int)e;
   const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   const size_t lds = kMainBytes + levels * kTreeBytes + kWaves * kWaveScratch;
   const int var = g_tune_var.load();
@@ -1275,6 +1328,8 @@ void nova_diag_set_stamps(uint64_t* dev_stamps) { g_diag_stamps.store(dev_stamps
 void nova_diag_set_static_pct(int pct) { g_tune_static_pct.store(pct); }
 
 void nova_diag_set_blocks_per_group(int bpg) { g_tune_bpg.store(bpg); }
+
+void nova_diag_set_chunk_blocks(int blocks) { g_tune_chunk.store(blocks); }
 
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {

@@ -26,10 +26,14 @@ def torch_gpu():
 def _reset_tuning():
     yield
     C.set_tuning(0, 0)
+    L = C.load()
+    L.nova_diag_set_chunk_blocks(0)
+    L.nova_diag_set_static_pct(-1)
+    L.nova_diag_set_blocks_per_group(0)
 
 
 def dev(torch, arr, dtype=None):
-    t = torch.from_numpy(np.ascontiguousarray(arr))
+    t = torch.from_numpy(np.array(arr, order="C"))  # writable copy
     if dtype is not None:
         t = t.to(dtype)
     return t.cuda()
@@ -147,12 +151,19 @@ def test_strided_vs_oracle(torch_gpu, oracle, length):
         assert np.array_equal(u32(out), want), (flags, length)
 
 
-@pytest.mark.parametrize("lanes,seg", [(0, 0), (1, 0), (2, 0), (4, 0), (8, 0), (16, 0),
-                                       (4, 16), (4, 64), (4, 1024), (1, 4096), (16, 256),
-                                       (8, 65536)])
-def test_variable_batch_vs_oracle(torch_gpu, oracle, lanes, seg):
+@pytest.mark.parametrize("lanes,seg,chunk,steal", [
+    (0, 0, 0, -1), (1, 0, 0, -1), (2, 0, 0, -1), (4, 0, 0, -1), (8, 0, 0, -1), (16, 0, 0, -1),
+    (4, 16, 0, -1), (4, 64, 0, -1), (4, 1024, 0, -1), (1, 4096, 0, -1), (16, 256, 0, -1),
+    (8, 65536, 0, -1), (16, 16384, 1, 0), (16, 16384, 3, 1), (8, 8192, 16, 255),
+    (4, 4096, 5, 8)])
+def test_variable_batch_vs_oracle(torch_gpu, oracle, lanes, seg, chunk, steal):
+    """Variable-length batch through the units kernel, across unit sizes and
+    the claim scheduler's chunk size / steal bound."""
     torch = torch_gpu
     C.set_tuning(lanes, seg)
+    L = C.load()
+    L.nova_diag_set_chunk_blocks(chunk)
+    L.nova_diag_set_static_pct(steal)
     rng = np.random.default_rng(lanes * 1000 + seg)
     n = 1500
     cls = rng.choice([1, 3, 4, 17, 600, 4096, 16384, 65536], n, p=[.03, .03, .04, .1, .1, .4,

@@ -39,6 +39,7 @@ def main():
     L.nova_diag_read_stream.restype = ctypes.c_int
     L.nova_diag_set_static_pct.argtypes = [ctypes.c_int]
     L.nova_diag_set_blocks_per_group.argtypes = [ctypes.c_int]
+    L.nova_diag_set_chunk_blocks.argtypes = [ctypes.c_int]
     assert L.nova_device_init() == 0
     results = []
 
@@ -86,13 +87,15 @@ def main():
             nbytes = int(lens_np.astype(np.uint64).sum())
             ref = C.batch(buf, offs, lens).clone()
 
-            def mk(g, seg, var, steal=0):
+            def mk(g, seg, var, chunk=0):
                 def f():
                     C.set_tuning(g, seg)
                     L.nova_diag_set_variant(var)
+                    L.nova_diag_set_chunk_blocks(chunk)
                     C.batch(buf, offs, lens, out=out)
                 return f
-            variants = [(g, s, 0, 0) for g in (8, 16) for s in (8192, 16384)]
+            variants = [(g, s, 0, ch) for g in (8, 16) for s in (8192, 16384)
+                        for ch in (4, 8, 16)]
         rs_out = torch.empty(1 << 22, dtype=torch.int32, device="cuda")
         stream_variants = [8192]
         times: dict = {}
@@ -113,6 +116,7 @@ def main():
         L.nova_diag_set_variant(0)
         L.nova_diag_set_static_pct(-1)
         L.nova_diag_set_blocks_per_group(0)
+        L.nova_diag_set_chunk_blocks(0)
         for key, ts in times.items():
             t = statistics.median(ts)
             b = nbytes if key[0] == "units" else (buf.numel() // 16) * 16
