@@ -17,6 +17,9 @@ the device-resident value.
 Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes per
 launch (sum of block lengths) / average launch time measured
 with HIP events on the launch stream inside the timed region.
+Defaults W=50, K=200: back-to-back launches show a power-management transient
+(launches ~4-25 run up to 30% slower, then settle; tools/launches.py), so
+the timed steps start after it.
 `cpu_baseline` = the reference util/crc32c.cc (oracle/_ref, compiled from the
 reference sources) or the oracle restatement, timed on this host's cores.
 """
@@ -124,8 +127,8 @@ def cpu_baseline(threads: int, seconds: float = 4.0):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--lanes", type=int, default=0, help="lanes per unit override (tuning)")
     ap.add_argument("--seg", type=int, default=0, help="segment bytes override (tuning)")
@@ -289,7 +292,9 @@ def main() -> int:
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel_ms_avg": round(avg_launch_s * 1e3, 4)},
+                         "kernel_ms_avg": round(avg_launch_s * 1e3, 4),
+                         "kernel_ms_min": round(min(kernel_ms), 4),
+                         "kernel_ms_median": round(sorted(kernel_ms)[len(kernel_ms) // 2], 4)},
             "verified_sample": verified,
         }
         if not args.no_cpu_baseline:

@@ -166,7 +166,7 @@ const char* nova_error_string(int err);
 
 /* ---- diagnostics (profiling only; not part of the drop-in surface) ------
  * variant: 0 production, 1 ablation (no table lookups -- WRONG CRCs, timing
- * only), 2 non-temporal data loads.  Process-wide. */
+ * only), 2 default-policy (cached) data loads instead of nt.  Process-wide. */
 void nova_diag_set_variant(int variant);
 /* variant 4: the streaming kernel writes {begin, end, XCC id} per wave
  * (s_memrealtime ticks, 100 MHz) to dev_stamps[3*wave ...]. */
@@ -176,6 +176,13 @@ void nova_diag_set_stamps(uint64_t* dev_stamps);
 void nova_diag_set_static_pct(int steal_probes);
 /* Streaming kernel: consecutive blocks per lane group per round (default 1). */
 void nova_diag_set_blocks_per_group(int bpg);
+/* Read-ceiling probe: variant = loads in flight per lane (2,4,8,16)
+ * | 0x100 nt policy | 0x200 1024-thread workgroups (else 256).  out_dev holds
+ * one u32 per launched thread. */
+int nova_diag_read_ceiling(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
+                           int variant, void* stream);
+/* Waves per workgroup for both batch kernels (1..16; 0 = per-kernel default). */
+void nova_diag_set_stream_waves(int waves);
 /* Units kernel: blocks per claimed wave chunk (1..16, default 8; 0 = default). */
 void nova_diag_set_chunk_blocks(int blocks);
 /* Plain coalesced streaming read of `bytes` (multiple of 16) with `wgs`

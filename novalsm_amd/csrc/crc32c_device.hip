@@ -99,18 +99,21 @@ typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
 // Kernel variants (diagnostics / tuning; 0 = production).
 constexpr int kVarNoLookup = 1;  // ablation: stream step without table lookups
-constexpr int kVarNT = 2;        // non-temporal (nt) data loads
+constexpr int kVarCached = 2;    // default-policy data loads (production uses nt)
 constexpr int kVarStamps = 4;    // record per-wave s_memrealtime stamps (diagnostics)
 constexpr int kVarStaticClaims = 8;  // stream kernel: claims without atomics (diagnostics)
 
-// 16-byte load through the global (not flat) address space.
+// 16-byte load through the global (not flat) address space.  Block bytes are
+// read exactly once, so production loads carry the nt policy: on gfx950 it
+// bypasses L1 and streams ~9% faster than the default policy at every block
+// size measured (tools/ceiling.py).
 template <int VAR = 0>
 __device__ __forceinline__ uint4 gload16(uint64_t addr) {
   u32x4 v;
-  if constexpr ((VAR & kVarNT) != 0)
-    v = __builtin_nontemporal_load(reinterpret_cast<gu32x4*>(addr));
-  else
+  if constexpr ((VAR & kVarCached) != 0)
     v = *reinterpret_cast<gu32x4*>(addr);
+  else
+    v = __builtin_nontemporal_load(reinterpret_cast<gu32x4*>(addr));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -324,10 +327,10 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
   {
     const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
     uint4* d = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += kThreads) d[i] = s[i];
+    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += blockDim.x) d[i] = s[i];
     const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
     uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
-    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += kThreads) d2[i] = s2[i];
+    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += blockDim.x) d2[i] = s2[i];
   }
   __syncthreads();
 
@@ -351,6 +354,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
   // implicit.  (Static chunk assignment left the tail unbalanced, as measured
   // for the streaming kernel in DESIGN.md 3.3.)
   const uint32_t nwg = gridDim.x;
+  const uint32_t nwaves = blockDim.x >> 6;
   uint32_t victim = blockIdx.x, tried = 0;
   uint64_t chunk = (uint64_t)wave * nwg + blockIdx.x;
   auto next_chunk = [&]() -> uint64_t {
@@ -360,7 +364,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
         idx = __hip_atomic_fetch_add(p.sched + victim * 16, 1u, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
       idx = __builtin_amdgcn_readfirstlane(idx);
-      const uint64_t c = ((uint64_t)idx + kWaves) * nwg + victim;
+      const uint64_t c = ((uint64_t)idx + nwaves) * nwg + victim;
       if (c < p.n_chunks) return c;
       if (++tried >= p.steal_limit + 1) return ~0ull;
       victim = (victim + 1) % nwg;
@@ -539,10 +543,10 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   {
     const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
     uint4* d = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += kThreads) d[i] = s[i];
+    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += blockDim.x) d[i] = s[i];
     const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
     uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
-    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += kThreads) d2[i] = s2[i];
+    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += blockDim.x) d2[i] = s2[i];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -550,7 +554,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   const int q = lane & (G - 1);
   const int grp = lane / G;
   constexpr int kGroups = 64 / G;
-  const uint64_t wid = (uint64_t)blockIdx.x * kWaves + wave;
+  const uint32_t nwaves = blockDim.x >> 6;  // waves per workgroup (tunable)
+  const uint64_t wid = (uint64_t)blockIdx.x * nwaves + wave;
   const uint64_t n = p.n_blocks;
   const uint64_t R = (n + (uint64_t)kGroups * p.bpg - 1) / ((uint64_t)kGroups * p.bpg);  // rounds
   const uint32_t KG = p.len / (64 * G);            // 4-swath steps per block (even, >= 2)
@@ -605,7 +610,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   uint32_t static_idx = 0;
   auto claim = [&](uint32_t v) {
     if constexpr ((VAR & kVarStaticClaims) != 0) {
-      req_old = wave + kWaves * (++static_idx) - kWaves;  // wave k takes k, k+16, ...
+      req_old = wave + nwaves * (++static_idx) - nwaves;  // wave k takes k, k+nw, ...
       return;
     }
     uint64_t save;
@@ -620,7 +625,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   };
   // round for claim index idx of workgroup v, or ~0 if v's rounds are exhausted
   auto round_of = [&](uint32_t v, uint32_t idx) -> uint64_t {
-    const uint64_t r = ((uint64_t)idx + kWaves) * nwg + v;  // first kWaves claims are implicit
+    const uint64_t r = ((uint64_t)idx + nwaves) * nwg + v;  // first nwaves claims are implicit
     return r < R ? r : ~0ull;
   };
   // Collect the pending claim; on an exhausted range move to the next victim
@@ -834,6 +839,31 @@ __global__ void __launch_bounds__(256) read_stream_kernel(const uint8_t* base, u
   out[tid] = acc;
 }
 
+// Diagnostic: read-ceiling probe.  U 16-byte loads per lane issued before any
+// use, default or nt policy, for measuring how much memory-level parallelism
+// the chip needs to approach its read peak.
+template <int U, int NT>
+__global__ void __launch_bounds__(1024) read_ceiling_kernel(const uint8_t* base, uint64_t n16,
+                                                            uint32_t* out) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  uint64_t i = tid;
+  const uint64_t b = (uint64_t)base;
+  for (; i + (U - 1) * nth < n16; i += U * nth) {
+    uint4 a[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) a[k] = gload16<NT ? 0 : kVarCached>(b + 16 * (i + k * nth));
+#pragma unroll
+    for (int k = 0; k < U; k++) acc ^= a[k].x ^ a[k].y ^ a[k].z ^ a[k].w;
+  }
+  for (; i < n16; i += nth) {
+    const uint4 a = gload16(b + 16 * i);
+    acc ^= a.x ^ a.y ^ a.z ^ a.w;
+  }
+  out[tid] = acc;
+}
+
 // ---- host: per-device tables ----------------------------------------------
 
 struct DevTables {
@@ -859,6 +889,17 @@ std::atomic<int> g_tune_g{0};
 std::atomic<int> g_tune_var{0};
 std::atomic<int> g_tune_bpg{0};
 std::atomic<int> g_tune_chunk{0};
+std::atomic<int> g_tune_waves{0};  // waves per workgroup override (0 = per-kernel default)
+
+// Waves per workgroup.  The tables fill the CU's LDS, so a CU runs exactly one
+// workgroup; fewer waves keep fewer HBM reads in flight per CU, which the
+// streaming kernel prefers (tools/ceiling.py: 8 waves 2-3% faster than 16).
+constexpr int kStreamWaves = 8;
+constexpr int kUnitsWaves = 12;  // config 3 sweep: 12 > 16 > 8
+int waves_per_wg(int def) {
+  const int w = g_tune_waves.load();
+  return (w > 0 && w <= kWaves) ? w : def;
+}
 std::atomic<uint64_t*> g_diag_stamps{nullptr};
 std::atomic<uint32_t> g_tune_seg{0};
 
@@ -963,9 +1004,10 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_mode<kLogWrite>())) return;
   if ((t->err = set_lds_attrs_mode<kLogVerify>())) return;
   if ((t->err = set_lds_attrs_mode<kStore, kVarNoLookup>())) return;
-  if ((t->err = set_lds_attrs_mode<kStore, kVarNT>())) return;
+  if ((t->err = set_lds_attrs_mode<kStore, kVarCached>())) return;
   if ((t->err = set_lds_attrs_stream<0>())) return;
   if ((t->err = set_lds_attrs_stream<kVarNoLookup>())) return;
+  if ((t->err = set_lds_attrs_stream<kVarCached>())) return;
   if ((t->err = set_lds_attrs_stream<kVarStamps>())) return;
   if ((t->err = set_lds_attrs_stream<kVarStamps | kVarStaticClaims>())) return;
 }
@@ -989,8 +1031,10 @@ int gindex(int G) { return G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4
 // Measured on MI355X for BASELINE config 3 (mixed 4/16/64 KiB, unaligned):
 // G = 16 lanes per 16 KiB segment was best among G 4..16 x seg 4..32 KiB.
 void plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int* G, uint32_t* seg) {
+  // Variable batches: 16 lanes per unit, 32 KiB segments (config 3 sweep,
+  // profiles/r01_sweep_config3_nt.log: 79.9% vs 77.3% at 16 KiB).
   int g = uniform ? 8 : 16;
-  uint32_t s = uniform ? 0u : 16384u;
+  uint32_t s = uniform ? 0u : 32768u;
   (void)n_blocks;
   (void)bytes_per_block;
   const int tg = g_tune_g.load();
@@ -1002,13 +1046,13 @@ void plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int* G, uin
 }
 
 template <int MODE, int VAR>
-int launch_g(int G, dim3 grid, size_t lds, hipStream_t stream, const CrcParams& p) {
+int launch_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
   switch (G) {
-    case 1: hipLaunchKernelGGL((crc32c_units_kernel<1, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
-    case 2: hipLaunchKernelGGL((crc32c_units_kernel<2, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
-    case 4: hipLaunchKernelGGL((crc32c_units_kernel<4, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
-    case 8: hipLaunchKernelGGL((crc32c_units_kernel<8, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
-    default: hipLaunchKernelGGL((crc32c_units_kernel<16, MODE, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    case 1: hipLaunchKernelGGL((crc32c_units_kernel<1, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 2: hipLaunchKernelGGL((crc32c_units_kernel<2, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 4: hipLaunchKernelGGL((crc32c_units_kernel<4, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 8: hipLaunchKernelGGL((crc32c_units_kernel<8, MODE, VAR>), grid, block, lds, stream, p); break;
+    default: hipLaunchKernelGGL((crc32c_units_kernel<16, MODE, VAR>), grid, block, lds, stream, p); break;
   }
   return (int)hipGetLastError();
 }
@@ -1024,7 +1068,8 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
     p.chunk = (ch > 0 && ch <= 16) ? (uint32_t)ch : 8u;
   }
   p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
-  uint64_t wgs = (p.n_chunks + kWaves - 1) / kWaves;
+  const uint64_t nwaves = waves_per_wg(kUnitsWaves);
+  uint64_t wgs = (p.n_chunks + nwaves - 1) / nwaves;
   if (wgs > (uint64_t)t->cus) wgs = t->cus;
   if (wgs > 256) wgs = 256;
   if (wgs == 0) return 0;
@@ -1038,20 +1083,22 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   if (e != hipSuccess) return (int)e;
   const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   const size_t lds = kMainBytes + levels * kTreeBytes + kWaves * kWaveScratch;
+  const dim3 block(64 * nwaves);
   const int var = g_tune_var.load();
-  if (MODE == kStore && var == kVarNoLookup) return launch_g<kStore, kVarNoLookup>(G, dim3(wgs), lds, stream, p);
-  if (MODE == kStore && var == kVarNT) return launch_g<kStore, kVarNT>(G, dim3(wgs), lds, stream, p);
-  return launch_g<MODE, 0>(G, dim3(wgs), lds, stream, p);
+  if (MODE == kStore && var == kVarNoLookup) return launch_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
+  if (MODE == kStore && var == kVarCached) return launch_g<kStore, kVarCached>(G, dim3(wgs), block, lds, stream, p);
+  return launch_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
 }
 
 template <int VAR>
 int launch_stream_g(int G, dim3 grid, size_t lds, hipStream_t stream, const CrcParams& p) {
+  const dim3 block(64 * waves_per_wg(kStreamWaves));
   switch (G) {
-    case 1: hipLaunchKernelGGL((crc32c_stream_kernel<1, VAR>), grid, dim3(kThreads), lds, stream, p); break;
-    case 2: hipLaunchKernelGGL((crc32c_stream_kernel<2, VAR>), grid, dim3(kThreads), lds, stream, p); break;
-    case 4: hipLaunchKernelGGL((crc32c_stream_kernel<4, VAR>), grid, dim3(kThreads), lds, stream, p); break;
-    case 8: hipLaunchKernelGGL((crc32c_stream_kernel<8, VAR>), grid, dim3(kThreads), lds, stream, p); break;
-    default: hipLaunchKernelGGL((crc32c_stream_kernel<16, VAR>), grid, dim3(kThreads), lds, stream, p); break;
+    case 1: hipLaunchKernelGGL((crc32c_stream_kernel<1, VAR>), grid, block, lds, stream, p); break;
+    case 2: hipLaunchKernelGGL((crc32c_stream_kernel<2, VAR>), grid, block, lds, stream, p); break;
+    case 4: hipLaunchKernelGGL((crc32c_stream_kernel<4, VAR>), grid, block, lds, stream, p); break;
+    case 8: hipLaunchKernelGGL((crc32c_stream_kernel<8, VAR>), grid, block, lds, stream, p); break;
+    default: hipLaunchKernelGGL((crc32c_stream_kernel<16, VAR>), grid, block, lds, stream, p); break;
   }
   return (int)hipGetLastError();
 }
@@ -1088,14 +1135,13 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   p.bpg = stream_bpg(G, p.len);
   const uint64_t groups = 64 / G;
   const uint64_t rounds = (p.n_blocks + groups * p.bpg - 1) / (groups * p.bpg);
-  uint64_t wgs = (rounds + kWaves - 1) / kWaves;
+  const uint64_t nwaves = waves_per_wg(kStreamWaves);
+  uint64_t wgs = (rounds + nwaves - 1) / nwaves;
   if (wgs > (uint64_t)t->cus) wgs = t->cus;
-  const uint64_t waves = wgs * kWaves;
   if (wgs > 256) wgs = 256;
   {
     const int sl = g_tune_static_pct.load();
     p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;  // 8 probes = one victim per XCD
-    p.bpg = stream_bpg(G, p.len);
   }
   // per-launch claim counters, zeroed on the launch stream (no host sync)
   const uint64_t slot = g_sched_ticket.fetch_add(1) % kSchedSlots;
@@ -1105,6 +1151,7 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   const size_t lds = kMainBytes + levels * kTreeBytes;
   if (g_tune_var.load() == kVarNoLookup) return launch_stream_g<kVarNoLookup>(G, dim3(wgs), lds, stream, p);
+  if (g_tune_var.load() == kVarCached) return launch_stream_g<kVarCached>(G, dim3(wgs), lds, stream, p);
   if (g_tune_var.load() == kVarStamps) {
     p.stamps = g_diag_stamps.load();
     return launch_stream_g<kVarStamps>(G, dim3(wgs), lds, stream, p);
@@ -1121,7 +1168,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   DevTables* t = tables(&err);
   if (!t) return err;
   if (p.n_blocks == 0) return 0;
-  if (mode == kStore && uniform && !g_tune_seg.load() && g_tune_var.load() != kVarNT) {
+  if (mode == kStore && uniform && !g_tune_seg.load()) {
     const int sg = stream_lanes(p);
     if (sg) return launch_stream(sg, p, t, stream);
   }
@@ -1264,7 +1311,7 @@ int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_u
   p.len = (uint32_t)bytes_per_block;
   p.stride = bytes_per_block;
   p.n_blocks = n_blocks;
-  const int sg = (g_tune_seg.load() || g_tune_var.load() == kVarNT) ? 0 : stream_lanes(p);
+  const int sg = g_tune_seg.load() ? 0 : stream_lanes(p);
   if (sg) {
     if (lanes_per_unit) *lanes_per_unit = sg;
     if (seg_bytes) *seg_bytes = 0;
@@ -1286,7 +1333,7 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
   p.stride = stride;
   p.n_blocks = n_blocks;
   int sg = 0;
-  if (!variable && !g_tune_seg.load() && g_tune_var.load() != kVarNT) sg = stream_lanes(p);
+  if (!variable && !g_tune_seg.load()) sg = stream_lanes(p);
   int n;
   if (sg) {
     n = snprintf(buf, buflen,
@@ -1331,12 +1378,34 @@ void nova_diag_set_blocks_per_group(int bpg) { g_tune_bpg.store(bpg); }
 
 void nova_diag_set_chunk_blocks(int blocks) { g_tune_chunk.store(blocks); }
 
+void nova_diag_set_stream_waves(int waves) { g_tune_waves.store(waves); }
+
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {
   if (!base || !out_dev || wgs <= 0) return NOVA_E_INVAL;
   hipLaunchKernelGGL(read_stream_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream,
                      (const uint8_t*)base, (uint64_t)(bytes / 16), out_dev);
   return (int)hipGetLastError();
+}
+
+int nova_diag_read_ceiling(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
+                           int variant, void* stream) {
+  if (!base || !out_dev || wgs <= 0) return NOVA_E_INVAL;
+  const int u = variant & 0xff;
+  const bool nt = (variant & 0x100) != 0;
+  const int threads = (variant & 0x200) ? 1024 : 256;
+  const uint8_t* b = (const uint8_t*)base;
+  const uint64_t n16 = bytes / 16;
+  hipStream_t st = (hipStream_t)stream;
+#define NOVA_RC(U)                                                                        \
+  if (u == U) {                                                                           \
+    if (nt) hipLaunchKernelGGL((read_ceiling_kernel<U, 1>), dim3(wgs), dim3(threads), 0, st, b, n16, out_dev); \
+    else hipLaunchKernelGGL((read_ceiling_kernel<U, 0>), dim3(wgs), dim3(threads), 0, st, b, n16, out_dev);   \
+    return (int)hipGetLastError();                                                        \
+  }
+  NOVA_RC(2) NOVA_RC(4) NOVA_RC(8) NOVA_RC(16)
+#undef NOVA_RC
+  return NOVA_E_INVAL;
 }
 
 const char* nova_error_string(int err) {

@@ -30,6 +30,8 @@ def _reset_tuning():
     L.nova_diag_set_chunk_blocks(0)
     L.nova_diag_set_static_pct(-1)
     L.nova_diag_set_blocks_per_group(0)
+    L.nova_diag_set_stream_waves(0)
+    L.nova_diag_set_variant(0)
 
 
 def dev(torch, arr, dtype=None):
@@ -156,7 +158,8 @@ def test_strided_vs_oracle(torch_gpu, oracle, length):
     (4, 16, 0, -1), (4, 64, 0, -1), (4, 1024, 0, -1), (1, 4096, 0, -1), (16, 256, 0, -1),
     (8, 65536, 0, -1), (16, 16384, 1, 0), (16, 16384, 3, 1), (8, 8192, 16, 255),
     (4, 4096, 5, 8)])
-def test_variable_batch_vs_oracle(torch_gpu, oracle, lanes, seg, chunk, steal):
+@pytest.mark.parametrize("waves,var", [(0, 0), (7, 2)])
+def test_variable_batch_vs_oracle(torch_gpu, oracle, lanes, seg, chunk, steal, waves, var):
     """Variable-length batch through the units kernel, across unit sizes and
     the claim scheduler's chunk size / steal bound."""
     torch = torch_gpu
@@ -164,6 +167,8 @@ def test_variable_batch_vs_oracle(torch_gpu, oracle, lanes, seg, chunk, steal):
     L = C.load()
     L.nova_diag_set_chunk_blocks(chunk)
     L.nova_diag_set_static_pct(steal)
+    L.nova_diag_set_stream_waves(waves)
+    L.nova_diag_set_variant(var)
     rng = np.random.default_rng(lanes * 1000 + seg)
     n = 1500
     cls = rng.choice([1, 3, 4, 17, 600, 4096, 16384, 65536], n, p=[.03, .03, .04, .1, .1, .4,
@@ -319,9 +324,11 @@ def test_stream_kernel_shapes(torch_gpu, oracle, length, n):
         assert np.array_equal(u32(out), want), (flags, length, n)
 
 
-@pytest.mark.parametrize("lanes,bpg,steal", [(1, 1, 0), (2, 3, 1), (4, 2, 8), (8, 1, 8),
-                                             (8, 4, 0), (16, 2, 255), (16, 1, 8)])
-def test_stream_kernel_tuning_variants(torch_gpu, oracle, lanes, bpg, steal):
+@pytest.mark.parametrize("lanes,bpg,steal,waves,var", [
+    (1, 1, 0, 0, 0), (2, 3, 1, 0, 0), (4, 2, 8, 0, 0), (8, 1, 8, 0, 0), (8, 4, 0, 0, 0),
+    (16, 2, 255, 0, 0), (16, 1, 8, 0, 0), (8, 2, 8, 1, 0), (8, 2, 8, 5, 2), (16, 1, 8, 12, 0),
+    (8, 2, 8, 16, 2)])
+def test_stream_kernel_tuning_variants(torch_gpu, oracle, lanes, bpg, steal, waves, var):
     torch = torch_gpu
     import ctypes
     L = C.load()
@@ -331,6 +338,8 @@ def test_stream_kernel_tuning_variants(torch_gpu, oracle, lanes, bpg, steal):
         C.set_tuning(lanes, 0)
         L.nova_diag_set_blocks_per_group(bpg)
         L.nova_diag_set_static_pct(steal)
+        L.nova_diag_set_stream_waves(waves)
+        L.nova_diag_set_variant(var)  # 2 = default-policy loads instead of nt
         n, length = 30011, 4096
         buf = torch.empty(n * length, dtype=torch.uint8, device="cuda")
         C.fill_splitmix64(buf, 77)

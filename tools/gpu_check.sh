@@ -20,5 +20,7 @@ STEPS=${STEPS:-smoke,pytest,bench,prof}
 [[ $STEPS == *smoke* ]] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *pytest* ]] && step pytest_gpu 900 python -m pytest tests -m gpu -q -x
 [[ $STEPS == *bench* ]] && step bench 600 python bench.py
-[[ $STEPS == *prof* ]] && step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline
+[[ $STEPS == *prof* ]] && step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline
+[[ $STEPS == *cfgs* ]] && for c in 3 4 5; do step bench_config$c 600 python bench.py --config $c --no-cpu-baseline; done
+[[ $STEPS == *pmc* ]] && step pmc2 900 bash tools/pmc.sh 2
 exit 0

@@ -2,7 +2,8 @@
 """Tuning / roofline sweep in ONE process (interleaved rounds, median of rounds).
 
 Variants: lanes per unit G, segment size, kernel variant (0 production,
-1 no-lookup ablation = memory-side ceiling of the access pattern, 2 nt loads),
+1 no-lookup ablation = memory-side ceiling of the access pattern, 2 default-policy
+loads instead of nt),
 and the plain coalesced streaming-read kernel (chip read ceiling).
 Writes gpurun_out/sweep.json.
 """
@@ -24,7 +25,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--configs", default="2,4")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
     args = ap.parse_args()
@@ -87,15 +88,16 @@ def main():
             nbytes = int(lens_np.astype(np.uint64).sum())
             ref = C.batch(buf, offs, lens).clone()
 
-            def mk(g, seg, var, chunk=0):
+            def mk(g, seg, var, chunk=0, waves=0):
                 def f():
                     C.set_tuning(g, seg)
                     L.nova_diag_set_variant(var)
                     L.nova_diag_set_chunk_blocks(chunk)
+                    L.nova_diag_set_stream_waves(waves)
                     C.batch(buf, offs, lens, out=out)
                 return f
-            variants = [(g, s, 0, ch) for g in (8, 16) for s in (8192, 16384)
-                        for ch in (4, 8, 16)]
+            variants = [(16, s, v, 8, w) for s in (16384, 32768, 65536) for v in (0, 2)
+                        for w in (8, 12, 16)]
         rs_out = torch.empty(1 << 22, dtype=torch.int32, device="cuda")
         stream_variants = [8192]
         times: dict = {}
@@ -117,6 +119,7 @@ def main():
         L.nova_diag_set_static_pct(-1)
         L.nova_diag_set_blocks_per_group(0)
         L.nova_diag_set_chunk_blocks(0)
+        L.nova_diag_set_stream_waves(0)
         for key, ts in times.items():
             t = statistics.median(ts)
             b = nbytes if key[0] == "units" else (buf.numel() // 16) * 16
