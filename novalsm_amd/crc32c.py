@@ -195,13 +195,16 @@ def write_trailers(buf, offsets, sizes, type_byte: int = 0, tb_quirk: bool = Fal
     return buf
 
 
-def verify_blocks(buf, offsets, sizes, stream=None):
-    """Returns (ok uint8 tensor, n_bad int32 tensor[1])."""
+def verify_blocks(buf, offsets, sizes, stream=None, ok=None, bad=None):
+    """Returns (ok uint8 tensor, n_bad int32 tensor[1]).  A caller-supplied
+    `bad` accumulates (zero it first)."""
     import torch
     _require_gpu()
     n = int(offsets.numel())
-    ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
-    bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
+    if bad is None:
+        bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
     rc = load().nova_sstable_verify_blocks(_ptr(buf), _ptr(offsets), _ptr(sizes), n, _ptr(ok),
                                            _ptr(bad), _stream_ptr(stream))
     _check(rc, "nova_sstable_verify_blocks")
@@ -217,13 +220,15 @@ def log_write_crcs(buf, record_offsets, stream=None):
     return buf
 
 
-def log_verify_records(buf, record_offsets, stream=None):
+def log_verify_records(buf, record_offsets, stream=None, ok=None, bad=None):
     """db/log_reader.cc:251-262 per record -> (ok uint8 tensor, n_bad int32 tensor[1])."""
     import torch
     _require_gpu()
     n = int(record_offsets.numel())
-    ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
-    bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
+    if bad is None:
+        bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
     rc = load().nova_log_verify_records(_ptr(buf), _ptr(record_offsets), n, _ptr(ok), _ptr(bad),
                                         _stream_ptr(stream))
     _check(rc, "nova_log_verify_records")

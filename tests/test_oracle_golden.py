@@ -122,13 +122,18 @@ def test_splitmix64_c_matches_numpy(oracle):
 
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 65])
 def test_alignment_independence(oracle, n):
-    # util/crc32c.cc: result independent of the start alignment (probe)
+    # util/crc32c.cc: result independent of the start alignment (probe).
+    # The block is placed at byte offsets 0..15 of one 16-B aligned buffer and
+    # checksummed in place (base pointer + offset), so the oracle's alignment
+    # head (util/crc32c.cc:535-541) really runs at every misalignment.
     base = splitmix64_bytes(5, n + 16)
     want = oracle.value(base[:n].tobytes())
-    for off in range(1, 8):
-        shifted = np.zeros(n + 16, dtype=np.uint8)
-        shifted[off:off + n] = base[:n]
-        assert oracle.value(shifted[off:off + n].tobytes()) == want
+    for off in range(16):
+        shifted = np.zeros(n + 48, dtype=np.uint8)
+        a = (-shifted.ctypes.data) % 16  # first 16-B aligned index
+        shifted[a + off:a + off + n] = base[:n]
+        got = oracle.batch(shifted, [a + off], [n])
+        assert int(got[0]) == want, off
 
 
 def test_log_fixture(oracle, golden):

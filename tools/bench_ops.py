@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Throughput of the SURVEY 8(f) composites on one MI355X, same clock as bench.py
+(HIP events on the launch stream, warmup past the launch transient), each
+against the HBM roofline with its own algorithmic bytes:
+
+  trailers    nova_sstable_write_trailers over a config-3 SSTable image
+              (blocks + 5-B trailer gaps): reads sum(len), writes 5 B/block
+  verify      nova_sstable_verify_blocks over the same image with trailers:
+              reads sum(len + 5), writes 1 B/block
+  log_write   nova_log_write_crcs over a 4 GiB log image of records with
+              U[1,4096] B payloads: reads sum(1 + len) (type + payload) plus the
+              3-B length/type header, writes 4 B/record
+  log_verify  nova_log_verify_records over the same image: reads sum(7 + len)
+  parity      nova_xor_parity of k=8 fragments x 512 MiB: reads 8 x 512 MiB,
+              writes 512 MiB
+
+One JSON line per op (rank 0 only, single GPU).  Sample-verified against the
+oracle outside the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+HBM_PEAK_GBS = 8000.0
+
+
+def timed(torch, fn, steps, warmup, stream):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = [a.elapsed_time(b) for a, b in ev]
+    return sum(ms) / len(ms) / 1e3
+
+
+def log_layout(total_target: int, seed: int):
+    """Records [crc 4][len 2][type 1][payload len], len ~ U[1,4096] from
+    splitmix64(seed), packed back to back up to ~total_target bytes."""
+    from novalsm_amd.synth import splitmix64_words
+    n = total_target // (7 + 2048)
+    r = splitmix64_words(seed, 0, n)
+    lens = ((r % np.uint64(4096)) + np.uint64(1)).astype(np.uint64)
+    types = ((r >> np.uint64(20)) % np.uint64(4) + np.uint64(1)).astype(np.uint8)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1] + np.uint64(7))
+    total = int(offs[-1] + lens[-1] + np.uint64(7))
+    return offs, lens, types, total
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", default="trailers,verify,log_write,log_verify,parity")
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--n", type=int, default=1 << 20, help="blocks for trailers/verify")
+    args = ap.parse_args()
+    import torch
+    from novalsm_amd import crc32c as C
+    from tests.oracle_lib import load_oracle
+    import bench
+
+    assert C.load().nova_device_init() == 0
+    orc = load_oracle()
+    stream = torch.cuda.current_stream()
+    ops = args.ops.split(",")
+    rows = []
+
+    def emit(op, workload, alg_bytes, sec, ok, extra=None):
+        gbs = alg_bytes / sec / 1e9
+        row = {"op": op, "workload": workload, "algorithmic_bytes": int(alg_bytes),
+               "ms_per_launch": round(sec * 1e3, 4), "GBps": round(gbs, 1),
+               "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)},
+               "verified_sample": bool(ok)}
+        if extra:
+            row.update(extra)
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+
+    if "trailers" in ops or "verify" in ops:
+        n = args.n
+        _, lens_np, _ = bench.config3_layout(n, 3)
+        offs_np = np.zeros(n, np.uint64)
+        offs_np[1:] = np.cumsum(lens_np[:-1].astype(np.uint64) + np.uint64(5))
+        total = int(offs_np[-1]) + int(lens_np[-1]) + 5
+        buf = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        C.fill_splitmix64(buf, 31)
+        offs = torch.from_numpy(offs_np.view(np.int64)).cuda()
+        lens = torch.from_numpy(lens_np.view(np.int32)).cuda()
+        sum_len = int(lens_np.astype(np.uint64).sum())
+        wl = f"config3 SSTable image: {n} blocks {{4,16,64}} KiB+U[1,64], 5-B trailers"
+        sample = np.linspace(0, n - 1, 129).astype(np.int64)
+        if "trailers" in ops:
+            sec = timed(torch, lambda: C.write_trailers(buf, offs, lens, 0, True, stream=stream),
+                        args.steps, args.warmup, stream)
+            ok = True
+            for i in sample:
+                o, ln = int(offs_np[i]), int(lens_np[i])
+                blk = buf[o:o + ln + 5].cpu().numpy().tobytes()
+                ok &= orc.trailer(blk[:ln], 0, True) == blk[ln:]
+            emit("trailers", wl, sum_len + 5 * n, sec, ok)
+        if "verify" in ops:
+            C.write_trailers(buf, offs, lens, 0, False, stream=stream)  # StoC order: verifiable
+            okb = torch.empty(n, dtype=torch.uint8, device="cuda")
+            bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+            def vf():
+                bad.zero_()
+                C.verify_blocks(buf, offs, lens, stream=stream, ok=okb, bad=bad)
+            sec = timed(torch, vf, args.steps, args.warmup, stream)
+            ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
+            emit("verify", wl, sum_len + 6 * n, sec, ok)
+        del buf
+        torch.cuda.empty_cache()
+
+    if "log_write" in ops or "log_verify" in ops:
+        offs_np, lens_np, types_np, total = log_layout(4 << 30, 6)
+        n = len(offs_np)
+        buf = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        C.fill_splitmix64(buf, 41)
+        # headers: length (LE16) and type bytes, written with torch scatter
+        o = torch.from_numpy(offs_np.view(np.int64)).cuda()
+        ln = torch.from_numpy(lens_np.astype(np.int64)).cuda()
+        buf[o + 4] = (ln & 0xFF).to(torch.uint8)
+        buf[o + 5] = (ln >> 8).to(torch.uint8)
+        buf[o + 6] = torch.from_numpy(types_np).cuda()
+        sum_rec = int(lens_np.sum()) + 7 * n
+        wl = f"log image: {n} records, payload U[1,4096] B, {total / 2**30:.2f} GiB"
+        sample = np.linspace(0, n - 1, 129).astype(np.int64)
+        if "log_write" in ops:
+            sec = timed(torch, lambda: C.log_write_crcs(buf, o, stream=stream), args.steps,
+                        args.warmup, stream)
+            ok = True
+            for i in sample:
+                a, L = int(offs_np[i]), int(lens_np[i])
+                rec = buf[a:a + 7 + L].cpu().numpy()
+                want = orc.mask(orc.extend(orc.value(rec[6:7].tobytes()), rec[7:].tobytes()))
+                ok &= int.from_bytes(rec[:4].tobytes(), "little") == want
+            emit("log_write", wl, sum_rec, sec, ok)
+        if "log_verify" in ops:
+            C.log_write_crcs(buf, o, stream=stream)
+            okb = torch.empty(n, dtype=torch.uint8, device="cuda")
+            bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+            def lv():
+                bad.zero_()
+                C.log_verify_records(buf, o, stream=stream, ok=okb, bad=bad)
+            sec = timed(torch, lv, args.steps, args.warmup, stream)
+            ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
+            emit("log_verify", wl, sum_rec + n, sec, ok)
+        del buf
+        torch.cuda.empty_cache()
+
+    if "parity" in ops:
+        k, plen = 8, 512 << 20
+        buf = torch.empty(k * plen, dtype=torch.uint8, device="cuda")
+        C.fill_splitmix64(buf, 51)
+        fo = torch.arange(k, dtype=torch.int64, device="cuda") * plen
+        out = torch.empty(plen, dtype=torch.uint8, device="cuda")
+        sec = timed(torch, lambda: C.xor_parity(buf, fo, plen, out=out, stream=stream),
+                    args.steps, args.warmup, stream)
+        idx = np.linspace(0, plen - 4097, 33).astype(np.int64)
+        ok = True
+        for i in idx:
+            want = np.zeros(4096, np.uint8)
+            for f in range(k):
+                want ^= buf[f * plen + i:f * plen + i + 4096].cpu().numpy()
+            ok &= np.array_equal(out[i:i + 4096].cpu().numpy(), want)
+        emit("parity", f"{k} fragments x {plen >> 20} MiB", (k + 1) * plen, sec, ok)
+
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "bench_ops.json"), "w") as f:
+        json.dump(rows, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
