@@ -42,6 +42,8 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/nova_crc32c.h"
@@ -320,6 +322,27 @@ __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0
   return group_fold<G>(lds, c0, c1, c2, c3, q);
 }
 
+// End of a scheduled launch: the last workgroup to finish zeroes the claim
+// counters it used (words w*16 for w < gridDim.x) and the finish counter
+// (word 1), so the stream's next launch starts from zero without a memset.
+// Every claim of every workgroup has returned before that workgroup counts
+// itself finished, so nothing touches the counters afterwards.
+__device__ __forceinline__ void sched_release(uint32_t* sched) {
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    uint32_t prev = 0;
+    if (threadIdx.x == 0)
+      prev = __hip_atomic_fetch_add(sched + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __shfl(prev, 0);
+    if (prev == gridDim.x - 1) {
+      for (uint32_t w = threadIdx.x; w < gridDim.x; w += 64)
+        __hip_atomic_store(sched + w * 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0)
+        __hip_atomic_store(sched + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <int G, int MODE, int VAR = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -342,6 +365,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
   uint32_t* wpre = reinterpret_cast<uint32_t*>(lds + kMainBytes + kLevels * kTreeBytes +
                                                wave * kWaveScratch);
   uint32_t* wacc = wpre + 64;
+  uint32_t* wsort = wpre + 32;  // chunk lanes in descending unit-size order
   const uint32_t rep = (uint32_t)(lane & 31) << 2;
   const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
   const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
@@ -390,41 +414,44 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
       init = p.init ? p.init[b] : 0u;
     }
     const uint32_t ninit = raw ? 0u : ~init;
-    // Units: blocks >= seg bytes are cut into floor(n/seg) segments ("big"
-    // units, seg..2seg-1 bytes); shorter blocks are one "small" unit.  Rounds
-    // take all big units first, then the small ones, so a round rarely mixes
-    // sizes (a round lasts as long as its longest unit).
-    uint32_t nq_big = 0, nq_small = 0;
+    // Units: blocks >= seg bytes are cut into floor(n/seg) segments (seg..2seg-1
+    // bytes each); shorter blocks are one unit.  A round lasts as long as its
+    // longest unit, so the chunk's blocks are ranked by unit size, largest
+    // first, and rounds take consecutive units in that order.
+    uint32_t nq = 0;
     uint32_t small_crc = 0;
     if (valid) {
       if (n >= 4) {
-        if (p.seg == 0) nq_big = 1;
-        else if (n >= p.seg) nq_big = n / p.seg;
-        else nq_small = 1;
+        nq = (p.seg == 0 || n < p.seg) ? 1u : n / p.seg;
       } else {  // tiny block: bytewise on this lane
         uint32_t l = ninit;
         for (uint32_t i = 0; i < n; i++) l = byte_step(l, ((const uint8_t*)a)[i]);
         small_crc = raw ? l : ~l;
       }
     }
-    const uint32_t nq = nq_big + nq_small;
-    // inclusive prefixes of big and small unit counts over the chunk's lanes
-    uint32_t ib = nq_big, is = nq_small;
+    const uint32_t key = nq ? n / nq : 0u;  // bytes per unit (0: no units)
+    uint32_t rank = 0;                       // position in descending key order
 #pragma unroll
-    for (int s = 1; s < 16; s <<= 1) {
-      const uint32_t ob = __shfl_up(ib, s), os = __shfl_up(is, s);
-      if ((lane & 15) >= s) {
-        ib += ob;
-        is += os;
-      }
+    for (int k = 0; k < 16; k++) {
+      const uint32_t kk = __shfl(key, k);
+      rank += (kk > key || (kk == key && k < (lane & 15))) ? 1u : 0u;
     }
-    const uint32_t total_big = __shfl(ib, 15);
-    const uint32_t total = total_big + __shfl(is, 15);
     if (lane < 16) {
-      wpre[lane] = ib;
-      wpre[16 + lane] = is;
+      wsort[rank] = lane;
       wacc[lane] = 0;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // inclusive prefix of unit counts in rank order
+    uint32_t ib = __shfl(nq, (int)wsort[lane & 15]);
+#pragma unroll
+    for (int s = 1; s < 16; s <<= 1) {
+      const uint32_t ob = __shfl_up(ib, s);
+      if ((lane & 15) >= s) ib += ob;
+    }
+    const uint32_t total = __shfl(ib, 15);
+    if (lane < 16) wpre[lane] = ib;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -433,22 +460,20 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
     for (uint32_t r0 = 0; r0 < total; r0 += kGroups) {
       const uint32_t u = r0 + grp;
       const bool active = u < total;
-      const bool big = u < total_big;
-      const uint32_t uu = big ? u : u - total_big;
-      const uint32_t* pre = big ? wpre : wpre + 16;
-      int i = 0;
+      int r = 0;
 #pragma unroll
       for (int s = 8; s > 0; s >>= 1)
-        if (pre[i + s - 1] <= uu) i += s;
-      if (!active) i = 0;
+        if (wpre[r + s - 1] <= u) r += s;
+      if (!active) r = 0;
+      const int i = (int)wsort[r];  // lane owning the unit's block
       const uint32_t a_lo = __shfl((uint32_t)a, i);
       const uint32_t a_hi = __shfl((uint32_t)(a >> 32), i);
       const uint32_t bn = __shfl(n, i);
       const uint32_t bq = __shfl(nq, i);
       const uint32_t binit = __shfl(ninit, i);
-      const uint32_t bincl = pre[i];
+      const uint32_t bincl = wpre[r];
       const uint64_t ba = ((uint64_t)a_hi << 32) | a_lo;
-      const uint32_t j = big ? bincl - 1 - uu : 0u;  // 0 = last unit of the block
+      const uint32_t j = bincl - 1 - u;  // 0 = last unit of the block
       uint64_t u0 = 0, u1 = 0;
       uint32_t uinit = 0;
       if (active) {
@@ -519,23 +544,21 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
       }
     }
   }
+  sched_release(p.sched);
 }
 
 // Aligned uniform batches (base, stride 16-B aligned, len a multiple of 64G).
 //
-// A "round" is kGroups = 64/G consecutive blocks, one per lane group of a
-// wave.  Each wave owns a stream of rounds and walks it as ONE flat sequence
-// of 4-swath steps, so the two-register-set prefetch never stops at a block
-// boundary; the per-block fold + store runs between steps while the next
-// block's loads are in flight.
+// A "round" is kGroups*BPG consecutive blocks (BPG per lane group of a wave).
+// Each wave walks its rounds as ONE flat sequence of 4-swath steps, so the
+// two-register-set prefetch never stops at a block boundary; the per-block
+// fold + store runs between steps while the next block's loads are in flight.
 //
-// Scheduling is guided-dynamic: wave w first takes a static share of
-// `static_rounds` rounds, then tickets of shrinking size from one device-scope
-// counter (relaxed fetch_add by lane 0, requested one ticket ahead so its
-// latency hides under a whole ticket of streaming).  Per-wave timestamps showed
-// static partitioning leaves ~20% of wave time idle at the tail (XCDs and CUs
-// stream at different speeds); the tickets absorb that skew.  The counter is
-// zeroed by a memset on the launch stream before every launch.
+// Scheduling is dynamic: per-workgroup claim counters, claimed one round
+// ahead, bounded stealing at the tail (see "work distribution" below).  Per-
+// wave timestamps showed static partitioning leaves ~20% of wave time idle at
+// the tail (XCDs and CUs stream at different speeds).  The counters are left
+// zeroed by the previous launch on the stream (sched_release).
 template <int G, int VAR = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -747,6 +770,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
       p.stamps[3 * wid + 2] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
     }
   }
+  sched_release(p.sched);
 }
 
 // XOR parity block over k data fragments (ltc/stoc_file_client_impl.cpp:334-349):
@@ -872,15 +896,17 @@ struct DevTables {
   uint32_t* ft = nullptr;
   uint32_t* sh16 = nullptr;
   uint32_t* zero_word = nullptr;  // 16 zero bytes: the NULL-init stand-in
-  uint32_t* sched = nullptr;      // kSchedSlots x 256 claim counters, 64 B apart
   int cus = 0;
   int err = 0;
+  // Claim counters, one 16 KiB slot per HIP stream (256 workgroups x 64 B).
+  // Launches on one stream run in order, so no two running launches share a
+  // slot; each launch leaves its slot zeroed (sched_release).
+  std::mutex sched_mu;
+  std::unordered_map<uint64_t, uint32_t*> sched_by_stream;
 };
 
 constexpr int kMaxDevices = 64;
-constexpr int kSchedSlots = 64;  // concurrent stream-kernel launches per device (round-robin)
-constexpr int kSchedWords = 256 * 16;  // per launch: up to 256 workgroups x 64 B
-std::atomic<uint64_t> g_sched_ticket{0};
+constexpr int kSchedWords = 256 * 16;  // per stream: up to 256 workgroups x 64 B
 std::atomic<int> g_tune_static_pct{-1};  // reused: steal probe limit (-1 = default)
 DevTables g_dev[kMaxDevices];
 std::once_flag g_once[kMaxDevices];
@@ -997,7 +1023,6 @@ void init_device(int dev, DevTables* t) {
   }
   if ((t->err = upload(&t->sh16, sh))) return;
   if ((t->err = upload(&t->zero_word, std::vector<uint32_t>(4, 0u)))) return;
-  if ((t->err = upload(&t->sched, std::vector<uint32_t>(kSchedSlots * kSchedWords, 0u)))) return;
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;
@@ -1023,13 +1048,31 @@ DevTables* tables(int* err) {
   return &g_dev[dev];
 }
 
+// The calling stream's claim-counter slot, created zeroed (in stream order) on
+// first use.  hipStreamPerThread names a different stream in every thread.
+uint32_t* sched_slot(DevTables* t, hipStream_t stream) {
+  uint64_t key = (uint64_t)(uintptr_t)stream;
+  if (stream == hipStreamPerThread)
+    key = (std::hash<std::thread::id>{}(std::this_thread::get_id()) << 1) | 1u;
+  std::lock_guard<std::mutex> lk(t->sched_mu);
+  auto it = t->sched_by_stream.find(key);
+  if (it != t->sched_by_stream.end()) return it->second;
+  void* d = nullptr;
+  if (hipMalloc(&d, kSchedWords * sizeof(uint32_t)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(d, 0, kSchedWords * sizeof(uint32_t), stream) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  t->sched_by_stream.emplace(key, static_cast<uint32_t*>(d));
+  return static_cast<uint32_t*>(d);
+}
+
 int gindex(int G) { return G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4; }
 
 // Dispatcher policy (lanes per unit G, segment bytes).  Small G keeps the
 // per-unit fold cheap relative to the stream work; longer blocks are split so
 // every lane group of a wave carries about `seg` bytes.
-// Measured on MI355X for BASELINE config 3 (mixed 4/16/64 KiB, unaligned):
-// G = 16 lanes per 16 KiB segment was best among G 4..16 x seg 4..32 KiB.
+// Measured on MI355X for BASELINE config 3 (mixed 4/16/64 KiB, unaligned).
 void plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int* G, uint32_t* seg) {
   // Variable batches: 16 lanes per unit, 32 KiB segments (config 3 sweep,
   // profiles/r01_sweep_config3_nt.log: 79.9% vs 77.3% at 16 KiB).
@@ -1077,10 +1120,8 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
     const int sl = g_tune_static_pct.load();
     p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;
   }
-  const uint64_t slot = g_sched_ticket.fetch_add(1) % kSchedSlots;
-  p.sched = t->sched + slot * kSchedWords;
-  hipError_t e = hipMemsetAsync(p.sched, 0, wgs * 64, stream);
-  if (e != hipSuccess) return (int)e;
+  p.sched = sched_slot(t, stream);
+  if (!p.sched) return NOVA_E_NOMEM;
   const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   const size_t lds = kMainBytes + levels * kTreeBytes + kWaves * kWaveScratch;
   const dim3 block(64 * nwaves);
@@ -1143,11 +1184,9 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
     const int sl = g_tune_static_pct.load();
     p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;  // 8 probes = one victim per XCD
   }
-  // per-launch claim counters, zeroed on the launch stream (no host sync)
-  const uint64_t slot = g_sched_ticket.fetch_add(1) % kSchedSlots;
-  p.sched = t->sched + slot * kSchedWords;
-  hipError_t e = hipMemsetAsync(p.sched, 0, wgs * 64, stream);
-  if (e != hipSuccess) return (int)e;
+  // claim counters of this stream (left zeroed by the previous launch)
+  p.sched = sched_slot(t, stream);
+  if (!p.sched) return NOVA_E_NOMEM;
   const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   const size_t lds = kMainBytes + levels * kTreeBytes;
   if (g_tune_var.load() == kVarNoLookup) return launch_stream_g<kVarNoLookup>(G, dim3(wgs), lds, stream, p);

@@ -466,3 +466,31 @@ def test_xor_parity(torch_gpu, oracle, align, plen):
                      for f in range(k)], np.uint64)
     out = C.xor_parity(dev(torch, host), dev(torch, offs, torch.int64), plen)
     assert np.array_equal(out.cpu().numpy(), oracle.xor_parity(host, offs, plen))
+
+
+def test_claim_counters_reset_between_launches(torch_gpu, oracle):
+    """Each launch leaves its stream's claim counters zeroed for the next one
+    (no per-launch memset).  Launches of varying grid size back to back on one
+    stream, then on a second stream, alternating the stream and units kernels:
+    a stale counter would skip rounds and leave sentinel outputs behind."""
+    torch = torch_gpu
+    length = 4096
+    nmax = 60000
+    host = splitmix64_bytes(123, nmax * length + 64)
+    buf = dev(torch, host)
+    want_all = oracle.batch_strided_mt(host, length, length, nmax, threads=8)
+    rng = np.random.default_rng(5)
+    s2 = torch.cuda.Stream()
+    for it in range(40):
+        n = int(rng.choice([1, 7, 300, 5000, 20011, nmax]))
+        stream = s2 if it % 3 == 2 else None
+        out = torch.full((n,), -559038737, dtype=torch.int32, device="cuda")  # 0xDEADBEEF
+        if it % 4 == 1:  # offsets/lengths -> variable-length units kernel
+            lens = torch.full((n,), length, dtype=torch.int32, device="cuda")
+            offs = torch.arange(n, dtype=torch.int64, device="cuda") * length
+            C.batch(buf, offs, lens, out=out, stream=stream)
+        else:
+            C.batch_strided(buf, length, length, n, out=out, stream=stream)
+        if stream is not None:
+            stream.synchronize()
+        assert np.array_equal(u32(out), want_all[:n]), (it, n)
