@@ -776,48 +776,81 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
 // XOR parity block over k data fragments (ltc/stoc_file_client_impl.cpp:334-349):
 // parity[i] = XOR_f mem[frag_off[f] + i] for i < parity_len.  Like the
 // reference, every fragment contributes parity_len bytes from its start (the
-// reference loop reads past a shorter fragment's end).  Each thread makes 16
-// output bytes; a fragment's misalignment s is wave-uniform, so unaligned
-// fragments cost one extra aligned load + v_alignbyte funnel shifts.
+// reference loop reads past a shorter fragment's end).  Each thread makes kU
+// 16-byte output chunks (grid-strided), so every fragment step issues kU
+// independent loads.  A fragment's misalignment s is wave-uniform: unaligned
+// fragments cost one more aligned load per chunk + v_alignbyte funnel shifts.
+// Loads are clamped to the aligned 16 B holding the fragment's last byte, so
+// nothing past the parity region's last 16-B line is touched; lanes past the
+// end re-read the last chunk and discard it.
+constexpr int kParityU = 4;
 __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, const uint64_t* frag_off,
                                                          uint32_t n_frags, uint64_t parity_len,
                                                          uint8_t* out) {
   const uint64_t nchunks = (parity_len + 15) / 16;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += stride) {
-    uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
-    for (uint32_t f = 0; f < n_frags; f++) {
-      const uint64_t addr = (uint64_t)base + frag_off[f] + 16 * c;
-      const uint32_t s = (uint32_t)(addr & 15);
-      const uint4 lo = gload16(addr - s);
-      if (s == 0) {
-        x0 ^= lo.x; x1 ^= lo.y; x2 ^= lo.z; x3 ^= lo.w;
-      } else {
-        const uint4 hi = gload16(addr - s + 16);
-        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        const uint32_t ws = s >> 2, bs = s & 3;
-        uint32_t r[4];
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c0 < nchunks;
+       c0 += kParityU * nth) {
+    uint32_t x[kParityU][4] = {};
+    uint64_t cc[kParityU];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          // select W[k+ws], W[k+ws+1] without dynamic register indexing
-          uint32_t a = w[k], b = w[k + 1];
-          if (ws == 1) { a = w[k + 1]; b = w[k + 2]; }
-          else if (ws == 2) { a = w[k + 2]; b = w[k + 3]; }
-          else if (ws == 3) { a = w[k + 3]; b = w[k + 4]; }
-          r[k] = __builtin_amdgcn_alignbyte(b, a, bs);
+    for (int k = 0; k < kParityU; k++) {
+      const uint64_t c = c0 + k * nth;
+      cc[k] = c < nchunks ? c : nchunks - 1;
+    }
+    for (uint32_t f = 0; f < n_frags; f++) {
+      const uint64_t fa = (uint64_t)base + frag_off[f];
+      const uint32_t s = (uint32_t)(fa & 15);
+      const uint64_t fb = fa - s;                              // aligned line of byte 0
+      const uint64_t lastline = (fa + parity_len - 1) & ~15ull;  // line of the last byte
+      if (s == 0) {
+        uint4 v[kParityU];
+#pragma unroll
+        for (int k = 0; k < kParityU; k++) v[k] = gload16(fb + 16 * cc[k]);
+#pragma unroll
+        for (int k = 0; k < kParityU; k++) {
+          x[k][0] ^= v[k].x; x[k][1] ^= v[k].y; x[k][2] ^= v[k].z; x[k][3] ^= v[k].w;
         }
-        x0 ^= r[0]; x1 ^= r[1]; x2 ^= r[2]; x3 ^= r[3];
+      } else {
+        uint4 lo[kParityU], hi[kParityU];
+#pragma unroll
+        for (int k = 0; k < kParityU; k++) {
+          const uint64_t l = fb + 16 * cc[k];
+          lo[k] = gload16(l);
+          hi[k] = gload16(l + 16 <= lastline ? l + 16 : lastline);
+        }
+        const uint32_t ws = s >> 2, bs = s & 3;
+#pragma unroll
+        for (int k = 0; k < kParityU; k++) {
+          const uint32_t w[8] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w,
+                                 hi[k].x, hi[k].y, hi[k].z, hi[k].w};
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            // W[e+ws], W[e+ws+1] without dynamic register indexing
+            uint32_t a = w[e], b = w[e + 1];
+            if (ws == 1) { a = w[e + 1]; b = w[e + 2]; }
+            else if (ws == 2) { a = w[e + 2]; b = w[e + 3]; }
+            else if (ws == 3) { a = w[e + 3]; b = w[e + 4]; }
+            x[k][e] ^= __builtin_amdgcn_alignbyte(b, a, bs);
+          }
+        }
       }
     }
-    const uint64_t o = 16 * c;
-    if (o + 16 <= parity_len) {
-      *reinterpret_cast<uint4*>(out + o) = make_uint4(x0, x1, x2, x3);
-    } else {
-      const uint32_t v[4] = {x0, x1, x2, x3};
-      for (uint64_t i = o; i < parity_len; i++) out[i] = (uint8_t)(v[(i - o) >> 2] >> (8 * ((i - o) & 3)));
+#pragma unroll
+    for (int k = 0; k < kParityU; k++) {
+      const uint64_t c = c0 + k * nth;
+      if (c >= nchunks) break;
+      const uint64_t o = 16 * c;
+      if (o + 16 <= parity_len) {
+        *reinterpret_cast<uint4*>(out + o) = make_uint4(x[k][0], x[k][1], x[k][2], x[k][3]);
+      } else {
+        for (uint64_t i = o; i < parity_len; i++)
+          out[i] = (uint8_t)(x[k][(i - o) >> 2] >> (8 * ((i - o) & 3)));
+      }
     }
   }
 }
+
 
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
 __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
@@ -1321,7 +1354,7 @@ int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_fra
   DevTables* t = tables(&err);
   if (!t) return err;
   uint64_t chunks = (parity_len + 15) / 16;
-  uint64_t wgs = (chunks + 255) / 256;
+  uint64_t wgs = (chunks + 256 * kParityU - 1) / (256 * kParityU);
   const uint64_t cap = (uint64_t)t->cus * 8;
   if (wgs > cap) wgs = cap;
   hipLaunchKernelGGL(xor_parity_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream,

@@ -455,15 +455,17 @@ def test_log_records_write_verify(torch_gpu, golden, oracle):
 
 
 @pytest.mark.parametrize("align", [True, False])
-@pytest.mark.parametrize("plen", [1, 15, 16, 4096, 100003])
-def test_xor_parity(torch_gpu, oracle, align, plen):
-    """XOR parity block (ltc/stoc_file_client_impl.cpp:334-349)."""
+@pytest.mark.parametrize("plen", [1, 15, 16, 17, 4096, 16389, 100003, (1 << 20) + 3])
+@pytest.mark.parametrize("k", [1, 3, 8])
+def test_xor_parity(torch_gpu, oracle, align, plen, k):
+    """XOR parity block (ltc/stoc_file_client_impl.cpp:334-349).
+    The last fragment's parity region ends exactly at the end of the buffer."""
     torch = torch_gpu
-    rng = np.random.default_rng(plen)
-    k = 5
-    host = splitmix64_bytes(plen, k * (plen + 64) + 64)
+    rng = np.random.default_rng(plen * 10 + k)
     offs = np.array([f * (plen + 64) + (0 if align else int(rng.integers(0, 16)))
                      for f in range(k)], np.uint64)
+    total = int(offs[-1]) + plen
+    host = splitmix64_bytes(plen + k, total)
     out = C.xor_parity(dev(torch, host), dev(torch, offs, torch.int64), plen)
     assert np.array_equal(out.cpu().numpy(), oracle.xor_parity(host, offs, plen))
 
