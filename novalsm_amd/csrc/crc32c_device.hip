@@ -643,7 +643,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
         "global_atomic_add %[old], %[zoff], %[one], %[ctr] sc0\n\t"
         "s_mov_b64 exec, %[save]"
         : [old] "=&v"(req_old), [save] "=&s"(save)
-        : [zoff] "v"(v * 16u), [one] "v"(1u), [ctr] "s"(p.sched)
+        : [zoff] "v"(v * 64u), [one] "v"(1u), [ctr] "s"(p.sched)  // byte offset: counter v is word 16v
         : "memory");
   };
   // round for claim index idx of workgroup v, or ~0 if v's rounds are exhausted

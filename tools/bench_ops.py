@@ -66,6 +66,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--n", type=int, default=1 << 20, help="blocks for trailers/verify")
+    ap.add_argument("--lanes-sweep", action="store_true",
+                    help="also time each CRC op at 4/8/16 lanes per unit (tuning)")
     args = ap.parse_args()
     import torch
     from novalsm_amd import crc32c as C
@@ -77,6 +79,17 @@ def main() -> int:
     stream = torch.cuda.current_stream()
     ops = args.ops.split(",")
     rows = []
+
+    def sweep(op, fn, alg_bytes):
+        if not args.lanes_sweep:
+            return
+        for g in (4, 8, 16):
+            C.set_tuning(g, 0)  # default segment size
+            sec = timed(torch, fn, args.steps, args.warmup, stream)
+            print(json.dumps({"sweep": op, "lanes": g, "GBps": round(alg_bytes / sec / 1e9, 1),
+                              "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}),
+                  flush=True)
+        C.set_tuning(0, 0)
 
     def emit(op, workload, alg_bytes, sec, ok, extra=None):
         gbs = alg_bytes / sec / 1e9
@@ -112,6 +125,8 @@ def main() -> int:
                 blk = buf[o:o + ln + 5].cpu().numpy().tobytes()
                 ok &= orc.trailer(blk[:ln], 0, True) == blk[ln:]
             emit("trailers", wl, sum_len + 5 * n, sec, ok)
+            sweep("trailers", lambda: C.write_trailers(buf, offs, lens, 0, True, stream=stream),
+                  sum_len + 5 * n)
         if "verify" in ops:
             C.write_trailers(buf, offs, lens, 0, False, stream=stream)  # StoC order: verifiable
             okb = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -123,6 +138,7 @@ def main() -> int:
             sec = timed(torch, vf, args.steps, args.warmup, stream)
             ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
             emit("verify", wl, sum_len + 6 * n, sec, ok)
+            sweep("verify", vf, sum_len + 6 * n)
         del buf
         torch.cuda.empty_cache()
 
@@ -150,6 +166,7 @@ def main() -> int:
                 want = orc.mask(orc.extend(orc.value(rec[6:7].tobytes()), rec[7:].tobytes()))
                 ok &= int.from_bytes(rec[:4].tobytes(), "little") == want
             emit("log_write", wl, sum_rec, sec, ok)
+            sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
         if "log_verify" in ops:
             C.log_write_crcs(buf, o, stream=stream)
             okb = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -161,6 +178,7 @@ def main() -> int:
             sec = timed(torch, lv, args.steps, args.warmup, stream)
             ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
             emit("log_verify", wl, sum_rec + n, sec, ok)
+            sweep("log_verify", lv, sum_rec + n)
         del buf
         torch.cuda.empty_cache()
 
