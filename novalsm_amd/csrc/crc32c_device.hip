@@ -88,6 +88,12 @@ struct CrcParams {
   uint32_t* sched;           // stream kernel: per-workgroup claim counters, 64 B apart
   uint32_t steal_limit;      // stream kernel: max other workgroups probed when out of work
   uint32_t bpg;              // stream kernel: consecutive blocks per lane group per round
+  const uint32_t* tab_byte;  // flat kernel: one-byte step table M_1 (256 u32)
+  const uint8_t* zline;      // flat kernel: 16 zero bytes (target of masked-off loads)
+  // flat kernel: descriptor arrays are always loaded (no branch), absent ones
+  // read word 0 of zline through a zero mask; offset = offsets[i & omask] +
+  // i * stride, length = lengths[i & lmask] + len, init = init[i & imask].
+  uint64_t omask, lmask, imask;
 };
 
 // ---- device helpers --------------------------------------------------------
@@ -773,6 +779,467 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   sched_release(p.sched);
 }
 
+// ---- crc32c_flat_kernel<G, MODE> -------------------------------------------
+// Variable-length batches (any alignment and length; per-block init; all
+// modes).  Every lane group walks its own sequence of WHOLE blocks, one
+// 4-swath step (64G bytes) at a time, and the wave streams all its groups'
+// steps as one flat sequence with the next step's loads in flight while the
+// current one folds -- across block boundaries, like the stream kernel.  The
+// groups of a wave change blocks independently, so a wave never waits for its
+// longest block (the units kernel's rounds did) and no block is split.
+//
+//   * Region of a block [u0,u1): its steps end at E = u1 & ~15 (16-B aligned)
+//     and start at E - S*64G <= u0 & ~15.  Pieces before u0 read as zero (a
+//     zero register ignores leading zeros; they are not loaded), ~init is
+//     xor-ed into the bytes [u0,u0+4).  After the group fold the register at E
+//     is M4(V); the 0..15 tail bytes [E,u1) (loaded with the last step) finish
+//     it with <= 3 word steps (M4 in LDS) and <= 3 byte steps (M1 in LDS).
+//   * Blocks reach the groups through per-wave chunks of C consecutive block
+//     descriptors held one per lane, in two banks (current and next).  The
+//     groups whose block ended take the next positions of the chunk sequence
+//     (ballot + popcount), reading the descriptor from its lane (bpermute).
+//     A bank is refilled as soon as it is used up, so its loads are at least
+//     one step old when first read and never drain the data prefetch.
+//   * Chunks are claimed like the units kernel's (per-workgroup counters,
+//     bounded stealing), one claim ahead, the claim issued from inline asm
+//     with EXEC = lane 0 and collected after >= one step of loads.
+//   * Log modes: descriptors are record headers; the refill loads the offsets,
+//     the next step loads the header bytes, the one after packs them.
+struct FlatSet {
+  uint4 d0, d1, d2, d3;  // the step's four swaths (16 B per lane each)
+  uint4 t, t2;           // tail line(s) at E (valid on the block's last step)
+  uint64_t pa;           // group base address of the step
+  uint64_t u0, u1, rec;  // the block's CRC input range and its index
+  uint32_t ninit, st;    // ~init (0 in RAW mode); stored CRC (log verify)
+  bool valid, last;
+};
+
+constexpr uint64_t kNoChunk = ~0ull;
+constexpr int kFlatMaxWaves = 12;  // 3 waves per SIMD: up to 168 VGPRs, no spills
+constexpr int kFlatThreads = kFlatMaxWaves * 64;
+
+// Keep the bytes of a 16-B piece at pa that lie in [u0,u1), xor ~init in at u0.
+__device__ __forceinline__ uint4 fix_piece(uint4 d, uint64_t pa, uint64_t u0, uint64_t u1,
+                                           uint32_t ninit) {
+  d.x = fix_word(d.x, pa + 0, u0, u1, ninit);
+  d.y = fix_word(d.y, pa + 4, u0, u1, ninit);
+  d.z = fix_word(d.z, pa + 8, u0, u1, ninit);
+  d.w = fix_word(d.w, pa + 12, u0, u1, ninit);
+  return d;
+}
+
+__device__ __forceinline__ uint32_t sel5(uint32_t k, uint32_t a, uint32_t b, uint32_t c,
+                                         uint32_t d, uint32_t e) {
+  return k == 0 ? a : k == 1 ? b : k == 2 ? c : k == 3 ? d : e;
+}
+
+template <int G, int MODE, int VAR = 0>
+__global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
+  constexpr uint32_t kByteTab = kMainBytes + kLevels * kTreeBytes;
+  constexpr bool kLog = MODE == kLogWrite || MODE == kLogVerify;
+  constexpr bool kTail2 = MODE == kVerify;  // stored CRC follows the CRC input
+  constexpr uint64_t kStep = 64 * G;
+  {
+    const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
+    uint4* d = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += blockDim.x) d[i] = s[i];
+    const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
+    uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
+    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += blockDim.x) d2[i] = s2[i];
+    const uint4* s3 = reinterpret_cast<const uint4*>(p.tab_byte);
+    uint4* d3 = reinterpret_cast<uint4*>(lds + kByteTab);
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) d3[i] = s3[i];
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane & (G - 1);
+  const int grp = lane / G;
+  const uint32_t rep = (uint32_t)(lane & 31) << 2;
+  const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
+  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
+  const uint32_t extra = (MODE == kVerify) ? 1u : 0u;  // verify covers block + type byte
+  const uint64_t zl = (uint64_t)p.zline;
+  const uint64_t base = (uint64_t)p.base;
+  const uint32_t C = p.chunk;  // kGroups <= C <= 64
+  const uint32_t nwg = gridDim.x;
+  const uint32_t nwaves = blockDim.x >> 6;
+
+  // ---- chunk claims (wave-uniform) ------------------------------------------
+  // A compiler-visible atomic by lane 0.  (Issued from inline asm, as the
+  // stream kernel does, the compiler copied the result register before the
+  // atomic had returned.)  The claim for the next switch is issued in the
+  // loop body's second take and read at the next switch, a step or more later.
+  uint32_t victim = blockIdx.x, tried = 0, req = 0;
+  bool claim_due = false;  // the next switch's claim is still to be issued
+  auto claim = [&](uint32_t v) {
+    uint32_t r = 0;
+    if (lane == 0)
+      r = __hip_atomic_fetch_add(p.sched + v * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    req = r;
+  };
+  auto chunk_of = [&](uint32_t v, uint32_t idx) -> uint64_t {
+    const uint64_t c = ((uint64_t)idx + nwaves) * nwg + v;  // first nwaves chunks implicit
+    return c < p.n_chunks ? c : kNoChunk;
+  };
+  // The chunk of the claim in req (issued in the second take since the last
+  // switch, or just before in the prologue); steal if exhausted.
+  auto collect = [&]() -> uint64_t {
+    uint64_t c = chunk_of(victim, __builtin_amdgcn_readfirstlane(req));
+    while (c == kNoChunk && ++tried < p.steal_limit + 1) {
+      victim = (victim + 1) % nwg;
+      claim(victim);
+      c = chunk_of(victim, __builtin_amdgcn_readfirstlane(req));
+    }
+    return c;
+  };
+
+  // ---- descriptor banks (LDS): bank k, slot i = block chunk_k*C + i -------------
+  // A refill loads the chunk's descriptors into registers (t_*); the next take,
+  // at least one step later, writes them to the wave's LDS bank, so neither
+  // the write nor any read waits on fresh loads.  (Registers as banks made
+  // the compiler copy fresh load results between registers at once, which
+  // drained the data prefetch at every refill.)  Log modes: the next take
+  // loads the header bytes, the one after packs and writes them.
+  const uint32_t desc_base = kByteTab + 1024u + (uint32_t)wave * 2u * C * 16u;
+  auto desc_at = [&](uint32_t bank, uint32_t i) -> uint4* {
+    return reinterpret_cast<uint4*>(lds + desc_base + (bank * C + i) * 16u);
+  };
+  uint32_t t_olo = 0, t_ohi = 0, t_len = 0, t_aux = 0;      // descriptor words in flight
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0;  // log: header bytes in flight
+  int pend = 0;            // 1: LDS write due (log: header loads due), 2: log pack + write due
+  uint32_t pend_bank = 0;
+  uint64_t ch0 = kNoChunk, ch1 = kNoChunk;  // chunk held by bank 0 / 1
+  const uint32_t my = (uint32_t)lane < C ? (uint32_t)lane : C - 1;
+  auto refill = [&](uint64_t chunk, uint32_t bank) {
+    uint64_t rec = (chunk == kNoChunk ? 0 : chunk * C) + my;
+    if (rec >= p.n_blocks) rec = p.n_blocks - 1;
+    const uint64_t o = p.offsets[rec & p.omask];
+    t_olo = (uint32_t)o;
+    t_ohi = (uint32_t)(o >> 32);
+    if constexpr (!kLog) {
+      t_len = p.lengths[rec & p.lmask];
+      t_aux = p.init[rec & p.imask];
+    }
+    if (bank) ch1 = chunk;
+    else ch0 = chunk;
+    pend = 1;
+    pend_bank = bank;
+  };
+  // The descriptor pipeline runs at fixed points of the two-step loop body, so
+  // every value in it has one producer and one consumer (no register copies,
+  // which would wait on the loads): refill in the first take, LDS write in
+  // the second (log: header loads in the second, pack + write in the next
+  // first).
+  auto step_pending = [&](bool first) {
+    if constexpr (kLog) {
+      if (pend == 1 && !first) {
+        const uint8_t* h = (const uint8_t*)(base + (((uint64_t)t_ohi << 32) | t_olo));
+        h4 = h[4];
+        h5 = h[5];
+        if constexpr (MODE == kLogVerify) {
+          h0 = h[0];
+          h1 = h[1];
+          h2 = h[2];
+          h3 = h[3];
+        }
+        pend = 2;
+        return;
+      }
+      if (pend != 2 || !first) return;
+      t_len = 1u + (h4 | (h5 << 8));  // type byte + payload (db/log_format.h:27-30)
+      t_aux = h0 | (h1 << 8) | (h2 << 16) | (h3 << 24);
+    } else {
+      if (pend != 1 || first) return;
+    }
+    if ((uint32_t)lane < C) *desc_at(pend_bank, lane) = make_uint4(t_olo, t_ohi, t_len, t_aux);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    pend = 0;
+  };
+  auto complete_pending = [&]() {  // out of order (drains); only when C is small
+    step_pending(false);
+    step_pending(true);
+  };
+
+  // ---- per-group block state (load side; group-uniform values) ---------------
+  uint64_t g_u0 = 0, g_u1 = 0, g_lp = 0, g_end = 0, g_rec = 0;
+  uint32_t g_ninit = 0, g_st = 0;
+  bool g_valid = false, g_need = true;
+  uint32_t pos = 0;     // next position in the current bank
+  uint32_t cb = 0;      // current bank
+  bool dry = false;     // no more chunks for this wave
+
+  // first: the loop body's first take (the only one that switches banks and
+  // refills; positions may run past the current bank into the other one
+  // meanwhile: C >= 2 groups keeps them below 2C).
+  // Values loaded in one take and used only conditionally later are consumed
+  // here unconditionally (an empty asm reading them), so the compiler
+  // resolves their loads at a fixed point with an exact count instead of
+  // waiting for all loads wherever its paths merge.
+  auto take = [&](bool first) {
+    if (first) {
+      asm volatile("" ::"v"(req));
+      if constexpr (kLog) asm volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(h4), "v"(h5));
+    } else {
+      asm volatile("" ::"v"(t_olo), "v"(t_ohi), "v"(t_len), "v"(t_aux));
+    }
+    step_pending(first);
+    if (!first && claim_due) {
+      claim(victim);
+      claim_due = false;
+    }
+    const uint64_t needm = __ballot(g_need && q == 0);
+    const uint32_t cnt = (uint32_t)__popcll(needm);
+    if (pend && pos + cnt > C) complete_pending();  // reads the refilled bank (small C only)
+    const uint32_t rank = (uint32_t)__popcll(needm & ((1ull << (grp * G)) - 1));
+    const uint32_t s = pos + rank;
+    const bool oth = s >= C;  // past the current bank: the other one
+    const uint32_t idx = oth ? s - C : s;
+    const uint32_t bank = oth ? cb ^ 1u : cb;
+    if (g_need) {  // (no group needing a block: only the switch check below)
+      const uint4 d = *desc_at(bank, idx);
+      const uint64_t cid = bank ? ch1 : ch0;
+      const uint64_t rec = cid * C + idx;
+      const bool ok = cid != kNoChunk && rec < p.n_blocks;
+      uint64_t a = base + (((uint64_t)d.y << 32) | d.x) + rec * p.stride;
+      if (kLog) a += 6;  // CRC input starts at the type byte (db/log_writer.cc:112)
+      const uint32_t n = d.z + p.len + extra;
+      const uint32_t aux = d.w;
+      g_valid = ok;
+      g_need = false;
+      g_u0 = a;
+      g_u1 = a + n;
+      g_rec = rec;
+      // ~init goes into the data's first 4 bytes; a block shorter than 4 bytes
+      // gets it at the end instead (R ^= M_n(~init), see fold).
+      g_ninit = (raw || n < 4) ? 0u : ~(kLog ? 0u : aux);  // log records: Value(), init 0
+      g_st = aux;
+      const uint64_t E = g_u1 & ~15ull;
+      const uint64_t A0 = a & ~15ull;
+      uint64_t S = (E - A0 + kStep - 1) / kStep;
+      if (S == 0) S = 1;
+      g_end = E;
+      g_lp = E - S * kStep;
+    }
+    pos += cnt;
+    // Checked in every first take, even with no block taken: the second take
+    // may then run past the current bank by < 1 group count, never past the
+    // other one (positions < C + 2 * groups <= 2C).
+    if (first && pos >= C) {  // the current bank is used up: switch, refill it
+      pos -= C;
+      cb ^= 1u;
+      uint64_t nc = kNoChunk;
+      if (!dry) {
+        nc = collect();
+        if (nc == kNoChunk) dry = true;
+        else claim_due = true;
+      }
+      refill(nc, cb ^ 1u);
+    }
+  };
+
+  auto issue = [&](FlatSet& X) -> bool {
+    const bool v = g_valid;
+    const bool last = v && (g_lp + kStep == g_end);
+    const uint64_t A0 = g_u0 & ~15ull;
+    const bool nz = v && g_u1 > g_u0;
+    const uint64_t pa = g_lp + 16 * q;
+    const uint64_t a0 = pa, a1 = pa + 16 * G, a2 = pa + 32 * G, a3 = pa + 48 * G;
+    X.d0 = gload16<VAR>((nz && a0 >= A0) ? a0 : zl);
+    X.d1 = gload16<VAR>((nz && a1 >= A0) ? a1 : zl);
+    X.d2 = gload16<VAR>((nz && a2 >= A0) ? a2 : zl);
+    X.d3 = gload16<VAR>((nz && a3 >= A0) ? a3 : zl);
+    if constexpr (kTail2) {
+      const uint64_t ta = last ? g_end : zl;  // holds the stored CRC's first byte
+      X.t = gload16<VAR>(ta);
+      X.t2 = gload16<VAR>((last && g_u1 + 4 > g_end + 16) ? g_end + 16 : ta);
+    } else {
+      X.t = gload16<VAR>((last && nz && (g_u1 & 15)) ? g_end : zl);
+    }
+    X.pa = g_lp;
+    X.u0 = g_u0;
+    X.u1 = g_u1;
+    X.rec = g_rec;
+    X.ninit = g_ninit;
+    X.st = g_st;
+    X.valid = v;
+    X.last = last;
+    if (v) g_lp += kStep;
+    if (last) g_need = true;
+    return __ballot(v) != 0;
+  };
+
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  bool wb_on = false;  // a finished block's write is pending (lane q == 0)
+  uint64_t wb_a = 0;
+  uint32_t wb_v = 0;
+  auto fold = [&](FlatSet& Y) {
+    const uint64_t pa = Y.pa + 16 * q;
+    const uint64_t lim = Y.u0 + 4;  // pieces starting before this need masking / init
+    uint4 d0 = Y.d0, d1 = Y.d1, d2 = Y.d2, d3 = Y.d3;
+    if (pa < lim) d0 = fix_piece(d0, pa, Y.u0, Y.u1, Y.ninit);
+    if (pa + 16 * G < lim) d1 = fix_piece(d1, pa + 16 * G, Y.u0, Y.u1, Y.ninit);
+    if (pa + 32 * G < lim) d2 = fix_piece(d2, pa + 32 * G, Y.u0, Y.u1, Y.ninit);
+    if (pa + 48 * G < lim) d3 = fix_piece(d3, pa + 48 * G, Y.u0, Y.u1, Y.ninit);
+    fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+    // the tail line(s) are used only on a block's last step: consume anyway
+    asm volatile("" ::"v"(Y.t.x), "v"(Y.t.y), "v"(Y.t.z), "v"(Y.t.w));
+    if constexpr (kTail2) asm volatile("" ::"v"(Y.t2.x), "v"(Y.t2.y), "v"(Y.t2.z), "v"(Y.t2.w));
+    if (Y.last) {  // group-uniform
+      const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
+      c0 = c1 = c2 = c3 = 0;
+      const uint64_t E = Y.u1 & ~15ull;
+      const uint32_t nb = (uint32_t)(Y.u1 - E);
+      uint32_t R;
+      {
+        R = tapply(lds, 0, v);  // register at E
+        const uint32_t w0 = fix_word(Y.t.x, E + 0, Y.u0, Y.u1, Y.ninit);
+        const uint32_t w1 = fix_word(Y.t.y, E + 4, Y.u0, Y.u1, Y.ninit);
+        const uint32_t w2 = fix_word(Y.t.z, E + 8, Y.u0, Y.u1, Y.ninit);
+        const uint32_t w3 = fix_word(Y.t.w, E + 12, Y.u0, Y.u1, Y.ninit);
+        uint32_t r;
+        r = tapply(lds, 0, R ^ w0);
+        R = nb >= 4 ? r : R;
+        r = tapply(lds, 0, R ^ w1);
+        R = nb >= 8 ? r : R;
+        r = tapply(lds, 0, R ^ w2);
+        R = nb >= 12 ? r : R;
+        const uint32_t wl = sel5(nb >> 2, w0, w1, w2, w3, 0u);
+        const uint32_t nr = nb & 3u;
+        r = (R >> 8) ^ lds_u32(lds, kByteTab + ((R ^ wl) & 255u) * 4u);
+        R = nr >= 1 ? r : R;
+        r = (R >> 8) ^ lds_u32(lds, kByteTab + ((R ^ (wl >> 8)) & 255u) * 4u);
+        R = nr >= 2 ? r : R;
+        r = (R >> 8) ^ lds_u32(lds, kByteTab + ((R ^ (wl >> 16)) & 255u) * 4u);
+        R = nr >= 3 ? r : R;
+      }
+      // n < 4: the data ran from a zero register; add the init's part M_n(~init)
+      // (no loads here: a load in this branch would make the compiler drain
+      // the prefetch at the loop head).
+      const uint32_t nn = (uint32_t)(Y.u1 - Y.u0);
+      if (nn < 4 && !raw) {
+        uint32_t l = ~(kLog ? 0u : Y.st);
+        for (uint32_t i = 0; i < 3; i++) {
+          const uint32_t r = (l >> 8) ^ lds_u32(lds, kByteTab + (l & 255u) * 4u);
+          l = i < nn ? r : l;
+        }
+        R ^= l;
+      }
+      uint32_t crc = raw ? R : ~R;
+      // The memory writes wait until after the next step's loads are issued
+      // (writeback): a store here would make the compiler drain the
+      // prefetch before the store's address registers are reused.
+      wb_on = q == 0;
+      if constexpr (kLog) {
+        wb_a = Y.u0 - 6;
+        wb_v = mask_crc(crc);  // db/log_writer.cc:113
+        if constexpr (MODE == kLogVerify) {
+          wb_a = (uint64_t)(p.ok_out + Y.rec);
+          wb_v = unmask_crc(Y.st) == crc ? 1u : 0u;  // db/log_reader.cc:254-256
+        }
+      } else if constexpr (MODE == kVerify) {
+        const uint32_t k = nb >> 2;
+        const uint32_t wlo = sel5(k, Y.t.x, Y.t.y, Y.t.z, Y.t.w, Y.t2.x);
+        const uint32_t whi = sel5(k, Y.t.y, Y.t.z, Y.t.w, Y.t2.x, Y.t2.y);
+        const uint32_t stored = __builtin_amdgcn_alignbyte(whi, wlo, nb & 3u);
+        wb_a = (uint64_t)(p.ok_out + Y.rec);
+        wb_v = unmask_crc(stored) == crc ? 1u : 0u;  // table/table.cc:435-437
+      } else {
+        if (p.flags & NOVA_CRC32C_APPEND_TYPE) crc = ~byte_step(~crc, (p.flags >> 8) & 0xffu);
+        if constexpr (MODE == kTrailer) {
+          wb_a = Y.u1;
+          wb_v = mask_crc(crc);
+        } else {
+          if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
+          wb_a = (uint64_t)(p.out + Y.rec);
+          wb_v = crc;
+        }
+      }
+    }
+  };
+  auto writeback = [&]() {
+    typedef __attribute__((address_space(1))) uint8_t gu8;  // global, not flat: a flat
+    typedef __attribute__((address_space(1))) uint32_t gu32;  // store would wait on LDS too
+    if (wb_on) {
+      if constexpr (MODE == kLogWrite) {
+        gu8* h = (gu8*)wb_a;
+        h[0] = (uint8_t)wb_v;
+        h[1] = (uint8_t)(wb_v >> 8);
+        h[2] = (uint8_t)(wb_v >> 16);
+        h[3] = (uint8_t)(wb_v >> 24);
+      } else if constexpr (MODE == kLogVerify || MODE == kVerify) {
+        *(gu8*)wb_a = (uint8_t)wb_v;
+        if (!wb_v && p.n_bad) atomicAdd(p.n_bad, 1u);
+      } else if constexpr (MODE == kTrailer) {
+        gu8* d = (gu8*)wb_a;
+        d[0] = (uint8_t)(p.flags >> 8);
+        d[1] = (uint8_t)wb_v;
+        d[2] = (uint8_t)(wb_v >> 8);
+        d[3] = (uint8_t)(wb_v >> 16);
+        d[4] = (p.flags & NOVA_TRAILER_TB_QUIRK) ? (uint8_t)'!' : (uint8_t)(wb_v >> 24);
+      } else {
+        *(gu32*)wb_a = wb_v;
+      }
+      wb_on = false;
+    }
+  };
+
+  // ---- prologue: wave k's first chunk is implicit, the second is claimed ------
+  {
+    uint64_t c0 = (uint64_t)wave * nwg + blockIdx.x;
+    if (c0 >= p.n_chunks) {
+      claim(victim);
+      c0 = collect();
+    }
+    if (c0 == kNoChunk) dry = true;
+    refill(c0, 0);
+    complete_pending();
+    uint64_t c1 = kNoChunk;
+    if (!dry) {
+      claim(victim);
+      c1 = collect();
+      if (c1 == kNoChunk) dry = true;
+      else claim_due = true;
+    }
+    refill(c1, 1);
+    complete_pending();
+  }
+  // The loop starts by folding an empty set A (zeros, not valid): no data
+  // load is in flight when the loop is entered, so the compiler's wait
+  // counts at the loop head follow the steady state (an A issued before the
+  // loop made it wait for everything there, every iteration).
+  FlatSet A, B;
+  A.d0 = A.d1 = A.d2 = A.d3 = A.t = A.t2 = make_uint4(0, 0, 0, 0);
+  A.pa = A.u0 = A.u1 = A.rec = 0;
+  A.ninit = A.st = 0;
+  A.valid = A.last = false;
+  for (;;) {
+    take(true);
+    issue(B);
+    writeback();
+    fold(A);
+    // No exit here: a mid-body exit makes the CFG structurizer add a path
+    // that enters the loop head with B's loads outstanding, and the head then
+    // waits for all loads every iteration.  A B without valid groups costs
+    // one more (empty) half.
+    take(false);
+    const bool a_live = issue(A);
+    writeback();
+    fold(B);
+    if (!a_live) break;
+  }
+  writeback();
+  // The last claim (if any) must have returned before this workgroup counts
+  // itself finished: the last workgroup then zeroes the counters.
+  __builtin_amdgcn_s_waitcnt(0);
+  sched_release(p.sched);
+}
+
 // XOR parity block over k data fragments (ltc/stoc_file_client_impl.cpp:334-349):
 // parity[i] = XOR_f mem[frag_off[f] + i] for i < parity_len.  Like the
 // reference, every fragment contributes parity_len bytes from its start (the
@@ -929,6 +1396,7 @@ struct DevTables {
   uint32_t* ft = nullptr;
   uint32_t* sh16 = nullptr;
   uint32_t* zero_word = nullptr;  // 16 zero bytes: the NULL-init stand-in
+  uint32_t* byte8 = nullptr;      // M_1 byte table (flat kernel tail steps)
   int cus = 0;
   int err = 0;
   // Claim counters, one 16 KiB slot per HIP stream (256 workgroups x 64 B).
@@ -1007,6 +1475,31 @@ int set_lds_attr_stream() {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
+constexpr size_t kLdsMax = 160 * 1024;  // per CU on MI355X
+
+// Flat kernel LDS: tables + byte table; the per-wave descriptor banks
+// (2 x chunk x 16 B per wave) come on top (flat_lds_total).
+template <int G>
+constexpr size_t flat_lds() {
+  return kMainBytes + (2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16)) * kTreeBytes + 1024;
+}
+
+template <int G, int MODE, int VAR = 0>
+int set_lds_attr_flat() {
+  return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_flat_kernel<G, MODE, VAR>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+}
+
+template <int MODE, int VAR = 0>
+int set_lds_attrs_flat() {
+  int e = 0;
+  if ((e = set_lds_attr_flat<1, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_flat<2, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_flat<4, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_flat<8, MODE, VAR>())) return e;
+  return set_lds_attr_flat<16, MODE, VAR>();
+}
+
 template <int VAR = 0>
 int set_lds_attrs_stream() {
   int e = 0;
@@ -1056,6 +1549,18 @@ void init_device(int dev, DevTables* t) {
   }
   if ((t->err = upload(&t->sh16, sh))) return;
   if ((t->err = upload(&t->zero_word, std::vector<uint32_t>(4, 0u)))) return;
+  {
+    std::vector<uint32_t> b8(256);
+    for (uint32_t b = 0; b < 256; b++) b8[b] = m1(b);
+    if ((t->err = upload(&t->byte8, b8))) return;
+  }
+  if ((t->err = set_lds_attrs_flat<kStore>())) return;
+  if ((t->err = set_lds_attrs_flat<kTrailer>())) return;
+  if ((t->err = set_lds_attrs_flat<kVerify>())) return;
+  if ((t->err = set_lds_attrs_flat<kLogWrite>())) return;
+  if ((t->err = set_lds_attrs_flat<kLogVerify>())) return;
+  if ((t->err = set_lds_attrs_flat<kStore, kVarNoLookup>())) return;
+  if ((t->err = set_lds_attrs_flat<kStore, kVarCached>())) return;
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;
@@ -1102,23 +1607,115 @@ uint32_t* sched_slot(DevTables* t, hipStream_t stream) {
 
 int gindex(int G) { return G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4; }
 
-// Dispatcher policy (lanes per unit G, segment bytes).  Small G keeps the
-// per-unit fold cheap relative to the stream work; longer blocks are split so
-// every lane group of a wave carries about `seg` bytes.
-// Measured on MI355X for BASELINE config 3 (mixed 4/16/64 KiB, unaligned).
-void plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int* G, uint32_t* seg) {
-  // Variable batches: 16 lanes per unit, 32 KiB segments (config 3 sweep,
-  // profiles/r01_sweep_config3_nt.log: 79.9% vs 77.3% at 16 KiB).
-  int g = uniform ? 8 : 16;
-  uint32_t s = uniform ? 0u : 32768u;
+// Dispatcher policy for batches the streaming kernel does not take: the flat
+// kernel (seg = 0) with G lanes per block, or -- when a segment size is forced
+// through nova_crc32c_set_tuning -- the units kernel with that segment size.
+// G: a step is 64G bytes and a block's region is padded to whole steps, so
+// shorter blocks want fewer lanes; log records (U[1,4096] B) use 8.
+constexpr int kFlatWaves = 8;
+uint64_t flat_waves() {
+  const int w = waves_per_wg(kFlatWaves);
+  return w > kFlatMaxWaves ? kFlatMaxWaves : w;
+}
+void plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, int* G,
+          uint32_t* seg) {
   (void)n_blocks;
-  (void)bytes_per_block;
+  int g = 16;
+  if (mode == kLogWrite || mode == kLogVerify) g = 8;
+  else if (uniform) g = bytes_per_block < 2048 ? 4 : bytes_per_block < 8192 ? 8 : 16;
+  uint32_t s = 0;
   const int tg = g_tune_g.load();
   const uint32_t ts = g_tune_seg.load();
   if (tg == 1 || tg == 2 || tg == 4 || tg == 8 || tg == 16) g = tg;
   if (ts) s = ts & ~15u;
+  if (s == 0 && g == 1) g = 2;  // flat kernel: at most 32 groups per wave (chunk >= 2 groups <= 64)
   *G = g;
   *seg = s;
+}
+
+// Blocks per claimed chunk of the flat kernel: one per lane group (the bank
+// refill is one step old when read), four per group for log records (the
+// header bytes need two more steps); at most 64 (one per lane).
+uint64_t flat_waves();
+size_t flat_lds_g(int G);
+uint32_t flat_chunk(int G, int mode) {
+  const uint32_t groups = 64u / (uint32_t)G;
+  const bool log = mode == kLogWrite || mode == kLogVerify;
+  const int tc = g_tune_chunk.load();
+  uint32_t c = tc > 0 ? (uint32_t)tc : (log ? 4 * groups : 2 * groups);
+  // the descriptor banks must fit next to the tables
+  const uint64_t room = (kLdsMax - flat_lds_g(G)) / (flat_waves() * 2 * 16);
+  if (c > room) c = (uint32_t)room;
+  if (c > 64) c = 64;
+  if (c < 2 * groups) c = 2 * groups;  // the kernel relies on it (positions < 2C)
+  return c;
+}
+
+size_t flat_lds_g(int G) {
+  switch (G) {
+    case 1: return flat_lds<1>();
+    case 2: return flat_lds<2>();
+    case 4: return flat_lds<4>();
+    case 8: return flat_lds<8>();
+    default: return flat_lds<16>();
+  }
+}
+
+template <int MODE, int VAR>
+int launch_flat_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
+  switch (G) {
+    case 1: hipLaunchKernelGGL((crc32c_flat_kernel<1, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 2: hipLaunchKernelGGL((crc32c_flat_kernel<2, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 4: hipLaunchKernelGGL((crc32c_flat_kernel<4, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 8: hipLaunchKernelGGL((crc32c_flat_kernel<8, MODE, VAR>), grid, block, lds, stream, p); break;
+    default: hipLaunchKernelGGL((crc32c_flat_kernel<16, MODE, VAR>), grid, block, lds, stream, p); break;
+  }
+  return (int)hipGetLastError();
+}
+
+template <int MODE>
+int launch_flat(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
+  p.tab_main = t->main[gindex(G)];
+  p.tab_tree = t->tree;
+  p.tab_byte = t->byte8;
+  p.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
+  p.omask = p.lmask = p.imask = ~0ull;
+  if (p.offsets) {
+    p.stride = 0;
+  } else {  // fixed stride: offset i * stride
+    p.offsets = reinterpret_cast<const uint64_t*>(t->zero_word);
+    p.omask = 0;
+  }
+  if (p.lengths) {
+    p.len = 0;
+  } else {  // fixed length p.len (log modes read the header instead)
+    p.lengths = t->zero_word;
+    p.lmask = 0;
+  }
+  if (!p.init) {
+    p.init = t->zero_word;
+    p.imask = 0;
+  }
+  p.chunk = flat_chunk(G, MODE);
+  p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
+  const uint64_t nwaves = flat_waves();
+  uint64_t wgs = (p.n_chunks + nwaves - 1) / nwaves;
+  if (wgs > (uint64_t)t->cus) wgs = t->cus;
+  if (wgs > 256) wgs = 256;
+  if (wgs == 0) return 0;
+  {
+    const int sl = g_tune_static_pct.load();
+    p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;
+  }
+  p.sched = sched_slot(t, stream);
+  if (!p.sched) return NOVA_E_NOMEM;
+  const dim3 block(64 * nwaves);
+  const size_t lds = flat_lds_g(G) + nwaves * 2 * p.chunk * 16;
+  if (lds > kLdsMax) return NOVA_E_INVAL;
+  const int var = g_tune_var.load();
+  if (MODE == kStore && var == kVarNoLookup) return launch_flat_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
+  if (MODE == kStore && var == kVarCached) return launch_flat_g<kStore, kVarCached>(G, dim3(wgs), block, lds, stream, p);
+  return launch_flat_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
 }
 
 template <int MODE, int VAR>
@@ -1246,8 +1843,17 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   }
   int G;
   uint32_t seg;
-  plan(p.n_blocks, bytes_per_block, uniform, &G, &seg);
+  plan(p.n_blocks, bytes_per_block, uniform, mode, &G, &seg);
   p.seg = seg;
+  if (seg == 0) {
+    switch (mode) {
+      case kStore: return launch_flat<kStore>(G, p, t, stream);
+      case kTrailer: return launch_flat<kTrailer>(G, p, t, stream);
+      case kLogWrite: return launch_flat<kLogWrite>(G, p, t, stream);
+      case kLogVerify: return launch_flat<kLogVerify>(G, p, t, stream);
+      default: return launch_flat<kVerify>(G, p, t, stream);
+    }
+  }
   switch (mode) {
     case kStore: return launch_mode<kStore>(G, p, t, stream);
     case kTrailer: return launch_mode<kTrailer>(G, p, t, stream);
@@ -1391,10 +1997,10 @@ int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_u
   }
   int g;
   uint32_t s;
-  plan(n_blocks, bytes_per_block, true, &g, &s);
+  plan(n_blocks, bytes_per_block, true, kStore, &g, &s);
   if (lanes_per_unit) *lanes_per_unit = g;
   if (seg_bytes) *seg_bytes = s;
-  return 0;  // units kernel
+  return s ? 0 : 2;  // units kernel (forced segment size) : flat kernel
 }
 
 int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int variable, char* buf,
@@ -1416,10 +2022,16 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
   } else {
     int g;
     uint32_t s;
-    plan(n_blocks, len, !variable, &g, &s);
-    n = snprintf(buf, buflen,
-                 "{\"kernel\": \"crc32c_units_kernel<%d, 0>\", \"lanes_per_unit\": %d, "
-                 "\"segment_bytes\": %u}", g, g, s);
+    plan(n_blocks, len, !variable, kStore, &g, &s);
+    if (s)
+      n = snprintf(buf, buflen,
+                   "{\"kernel\": \"crc32c_units_kernel<%d, 0>\", \"lanes_per_unit\": %d, "
+                   "\"segment_bytes\": %u}", g, g, s);
+    else
+      n = snprintf(buf, buflen,
+                   "{\"kernel\": \"crc32c_flat_kernel<%d, 0>\", \"lanes_per_block\": %d, "
+                   "\"chunk_blocks\": %u, \"waves_per_wg\": %d}", g, g, flat_chunk(g, kStore),
+                   (int)flat_waves());
   }
   return n;
 }

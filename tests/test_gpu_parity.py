@@ -185,11 +185,14 @@ def test_variable_batch_vs_oracle(torch_gpu, oracle, lanes, seg, chunk, steal, w
     host = splitmix64_bytes(99, pos + 64)
     init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     buf = dev(torch, host)
-    out = C.batch(buf, dev(torch, offs, torch.int64), dev(torch, lens, torch.int32),
-                  init=dev(torch, init.view(np.int32)))
     want = oracle.batch(host, offs, lens, init)
-    bad = np.nonzero(u32(out) != want)[0]
-    assert bad.size == 0, [(int(offs[i]), int(lens[i])) for i in bad[:5]]
+    do, dl, di = (dev(torch, offs, torch.int64), dev(torch, lens, torch.int32),
+                  dev(torch, init.view(np.int32)))
+    for _ in range(3):  # the schedule is dynamic: several launches, sentinel-filled outputs
+        out = torch.full((n,), -559038737, dtype=torch.int32, device="cuda")  # 0xDEADBEEF
+        C.batch(buf, do, dl, init=di, out=out)
+        bad = np.nonzero(u32(out) != want)[0]
+        assert bad.size == 0, [(int(offs[i]), int(lens[i])) for i in bad[:5]]
     # RAW flag: linear part only; Extend(c, D) = ~(M_n(~c) ^ raw(D)) <=> raw == Extend(~0..)
     out_raw = C.batch(buf, dev(torch, offs, torch.int64), dev(torch, lens, torch.int32),
                       flags=C.RAW)
@@ -496,3 +499,75 @@ def test_claim_counters_reset_between_launches(torch_gpu, oracle):
         if stream is not None:
             stream.synchronize()
         assert np.array_equal(u32(out), want_all[:n]), (it, n)
+
+
+@pytest.mark.parametrize("lanes,chunk,waves", [
+    (0, 0, 0), (2, 0, 0), (4, 0, 0), (8, 0, 0), (16, 0, 0), (16, 9, 0), (16, 64, 0),
+    (8, 0, 3), (4, 40, 5), (16, 0, 1)])
+def test_flat_many_blocks(torch_gpu, oracle, lanes, chunk, waves):
+    """Flat kernel with enough blocks for every wave to switch descriptor
+    banks and claim chunks many times, including the stealing tail: mixed
+    tiny/empty/long blocks at random offsets (descriptors not in address
+    order), random inits, for every lane count, chunk size and wave count."""
+    torch = torch_gpu
+    C.set_tuning(lanes, 0)
+    L = C.load()
+    L.nova_diag_set_chunk_blocks(chunk)
+    L.nova_diag_set_stream_waves(waves)
+    rng = np.random.default_rng(1000 + lanes * 7 + chunk + waves)
+    n = 120000
+    lens = rng.choice([0, 1, 2, 3, 4, 5, 17, 100, 600, 1500, 4096, 9000], n,
+                      p=[.02, .02, .02, .02, .02, .05, .1, .25, .2, .1, .15, .05]).astype(np.uint32)
+    lens += (rng.integers(0, 64, n) * (lens > 5)).astype(np.uint32)
+    pos = np.cumsum(lens.astype(np.uint64) + rng.integers(0, 9, n).astype(np.uint64))
+    offs = (pos - lens.astype(np.uint64)).astype(np.uint64)
+    perm = rng.permutation(n)
+    offs, lens = offs[perm], lens[perm]
+    host = splitmix64_bytes(lanes + 3, int(pos[-1]) + 64)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    buf = dev(torch, host)
+    want = oracle.batch(host, offs, lens, init)
+    do, dl, di = (dev(torch, offs, torch.int64), dev(torch, lens, torch.int32),
+                  dev(torch, init.view(np.int32)))
+    for _ in range(3):  # the schedule is dynamic: several launches, sentinel-filled outputs
+        out = torch.full((n,), -559038737, dtype=torch.int32, device="cuda")  # 0xDEADBEEF
+        C.batch(buf, do, dl, init=di, out=out)
+        bad = np.nonzero(u32(out) != want)[0]
+        assert bad.size == 0, [(int(offs[i]), int(lens[i])) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("lanes,chunk", [(0, 0), (2, 0), (4, 0), (8, 0), (16, 0), (8, 16),
+                                         (4, 17), (16, 64)])
+def test_log_many_records(torch_gpu, oracle, lanes, chunk):
+    """Log record CRC write + verify over a log image with enough records to
+    exercise the header pipeline of the flat kernel's descriptor banks
+    (db/log_writer.cc:99-114, db/log_reader.cc:251-262), every lane count."""
+    torch = torch_gpu
+    C.set_tuning(lanes, 0)
+    C.load().nova_diag_set_chunk_blocks(chunk)
+    rng = np.random.default_rng(77 + lanes + chunk)
+    n = 60000
+    plen = rng.integers(0, 700, n).astype(np.uint64)
+    plen[rng.integers(0, n, 200)] = rng.integers(0, 3, 200)  # empty / tiny payloads
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(plen[:-1] + np.uint64(7))
+    total = int(offs[-1] + plen[-1] + np.uint64(7))
+    host = splitmix64_bytes(lanes + 11, total + 16).copy()
+    host[offs.astype(np.int64) + 4] = (plen & np.uint64(0xFF)).astype(np.uint8)
+    host[offs.astype(np.int64) + 5] = (plen >> np.uint64(8)).astype(np.uint8)
+    host[offs.astype(np.int64) + 6] = rng.integers(1, 5, n).astype(np.uint8)
+    buf = dev(torch, host)
+    doffs = dev(torch, offs, torch.int64)
+    C.log_write_crcs(buf, doffs)
+    want = host.copy()
+    oracle.log_write(want, offs)
+    got = buf.cpu().numpy()
+    assert np.array_equal(got, want)
+    ok, bad = C.log_verify_records(buf, doffs)
+    assert ok.cpu().numpy().all() and int(bad.item()) == 0
+    victims = rng.choice(n, 25, replace=False)
+    for v in victims:
+        buf[int(offs[v]) + 6] ^= 0x02
+    ok, bad = C.log_verify_records(buf, doffs)
+    assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
+    assert int(bad.item()) == len(victims)
