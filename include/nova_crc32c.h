@@ -181,8 +181,12 @@ void nova_diag_set_blocks_per_group(int bpg);
  * one u32 per launched thread. */
 int nova_diag_read_ceiling(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                            int variant, void* stream);
-/* Waves per workgroup for both batch kernels (1..16; 0 = per-kernel default). */
+/* Waves per workgroup for the batch kernels (1..16, flat kernel <= 12; 0 =
+ * per-kernel default). */
 void nova_diag_set_stream_waves(int waves);
+/* Kernel for variable-length / unaligned batches: 0 auto (units kernel),
+ * 1 units, 2 flat (per-group block streams).  Process-wide. */
+void nova_diag_set_variable_kernel(int kernel);
 /* Units kernel: blocks per claimed wave chunk (1..16, default 8; 0 = default). */
 void nova_diag_set_chunk_blocks(int blocks);
 /* Plain coalesced streaming read of `bytes` (multiple of 16) with `wgs`

@@ -1607,30 +1607,49 @@ uint32_t* sched_slot(DevTables* t, hipStream_t stream) {
 
 int gindex(int G) { return G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4; }
 
-// Dispatcher policy for batches the streaming kernel does not take: the flat
-// kernel (seg = 0) with G lanes per block, or -- when a segment size is forced
-// through nova_crc32c_set_tuning -- the units kernel with that segment size.
-// G: a step is 64G bytes and a block's region is padded to whole steps, so
-// shorter blocks want fewer lanes; log records (U[1,4096] B) use 8.
-constexpr int kFlatWaves = 8;
+// Dispatcher policy for batches the streaming kernel does not take.
+// Kernels: units (round-based, segments; the default: measured fastest on
+// config 3, SSTable-like 4 KiB+ blocks and log records) or flat
+// (per-group block streams, 3.5), chosen with nova_diag_set_variable_kernel.
+// G lanes per block/unit; segment size (units kernel; 0 = one unit per block)
+// from nova_crc32c_set_tuning or per workload:
+//   variable SSTable batches: G = 16, 32 KiB segments (config 3 sweep);
+//   log records (U[1,4096] B): G = 8, whole records;
+//   unaligned fixed-stride blocks: G by block length, whole blocks.
+constexpr int kFlatWaves = 12;  // sweep: 12 > 10 > 8 waves (more loads in flight)
 uint64_t flat_waves() {
   const int w = waves_per_wg(kFlatWaves);
   return w > kFlatMaxWaves ? kFlatMaxWaves : w;
 }
-void plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, int* G,
-          uint32_t* seg) {
+enum VarKernel { kAuto = 0, kUnitsK = 1, kFlatK = 2 };
+std::atomic<int> g_tune_kernel{0};
+struct Plan {
+  int kernel;
+  int G;
+  uint32_t seg;
+};
+Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode) {
   (void)n_blocks;
-  int g = 16;
-  if (mode == kLogWrite || mode == kLogVerify) g = 8;
-  else if (uniform) g = bytes_per_block < 2048 ? 4 : bytes_per_block < 8192 ? 8 : 16;
-  uint32_t s = 0;
+  const bool log = mode == kLogWrite || mode == kLogVerify;
+  Plan pl{kUnitsK, 16, 32768u};
+  if (log) {
+    pl.G = 8;
+    pl.seg = 0;
+  } else if (uniform) {
+    pl.G = bytes_per_block < 2048 ? 4 : bytes_per_block < 8192 ? 8 : 16;
+    pl.seg = 0;
+  }
+  const int tk = g_tune_kernel.load();
   const int tg = g_tune_g.load();
   const uint32_t ts = g_tune_seg.load();
-  if (tg == 1 || tg == 2 || tg == 4 || tg == 8 || tg == 16) g = tg;
-  if (ts) s = ts & ~15u;
-  if (s == 0 && g == 1) g = 2;  // flat kernel: at most 32 groups per wave (chunk >= 2 groups <= 64)
-  *G = g;
-  *seg = s;
+  if (tk == kFlatK && ts == 0) pl.kernel = kFlatK;
+  if (tg == 1 || tg == 2 || tg == 4 || tg == 8 || tg == 16) pl.G = tg;
+  if (ts) pl.seg = ts & ~15u;
+  if (pl.kernel == kFlatK) {
+    pl.seg = 0;
+    if (pl.G == 1) pl.G = 2;  // at most 32 groups per wave (chunk >= 2 groups <= 64)
+  }
+  return pl;
 }
 
 // Blocks per claimed chunk of the flat kernel: one per lane group (the bank
@@ -1698,7 +1717,8 @@ int launch_flat(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   }
   p.chunk = flat_chunk(G, MODE);
   p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
-  const uint64_t nwaves = flat_waves();
+  uint64_t nwaves = flat_waves();
+  while (nwaves > 1 && flat_lds_g(G) + nwaves * 2 * p.chunk * 16 > kLdsMax) nwaves--;  // G = 2
   uint64_t wgs = (p.n_chunks + nwaves - 1) / nwaves;
   if (wgs > (uint64_t)t->cus) wgs = t->cus;
   if (wgs > 256) wgs = 256;
@@ -1841,11 +1861,10 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     const int sg = stream_lanes(p);
     if (sg) return launch_stream(sg, p, t, stream);
   }
-  int G;
-  uint32_t seg;
-  plan(p.n_blocks, bytes_per_block, uniform, mode, &G, &seg);
-  p.seg = seg;
-  if (seg == 0) {
+  const Plan pl = plan(p.n_blocks, bytes_per_block, uniform, mode);
+  const int G = pl.G;
+  p.seg = pl.seg;
+  if (pl.kernel == kFlatK) {
     switch (mode) {
       case kStore: return launch_flat<kStore>(G, p, t, stream);
       case kTrailer: return launch_flat<kTrailer>(G, p, t, stream);
@@ -1995,12 +2014,10 @@ int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_u
     if (seg_bytes) *seg_bytes = 0;
     return 1;  // streaming kernel
   }
-  int g;
-  uint32_t s;
-  plan(n_blocks, bytes_per_block, true, kStore, &g, &s);
-  if (lanes_per_unit) *lanes_per_unit = g;
-  if (seg_bytes) *seg_bytes = s;
-  return s ? 0 : 2;  // units kernel (forced segment size) : flat kernel
+  const Plan pl = plan(n_blocks, bytes_per_block, true, kStore);
+  if (lanes_per_unit) *lanes_per_unit = pl.G;
+  if (seg_bytes) *seg_bytes = pl.seg;
+  return pl.kernel == kFlatK ? 2 : 0;  // flat kernel : units kernel
 }
 
 int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int variable, char* buf,
@@ -2020,13 +2037,13 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
                  sg, sg, stream_bpg(sg, (uint32_t)len),
                  g_tune_static_pct.load() < 0 ? 8 : g_tune_static_pct.load());
   } else {
-    int g;
-    uint32_t s;
-    plan(n_blocks, len, !variable, kStore, &g, &s);
-    if (s)
+    const Plan pl = plan(n_blocks, len, !variable, kStore);
+    const int g = pl.G;
+    if (pl.kernel != kFlatK)
       n = snprintf(buf, buflen,
                    "{\"kernel\": \"crc32c_units_kernel<%d, 0>\", \"lanes_per_unit\": %d, "
-                   "\"segment_bytes\": %u}", g, g, s);
+                   "\"segment_bytes\": %u, \"waves_per_wg\": %d}", g, g, pl.seg,
+                   waves_per_wg(kUnitsWaves));
     else
       n = snprintf(buf, buflen,
                    "{\"kernel\": \"crc32c_flat_kernel<%d, 0>\", \"lanes_per_block\": %d, "
@@ -2063,6 +2080,8 @@ void nova_diag_set_blocks_per_group(int bpg) { g_tune_bpg.store(bpg); }
 void nova_diag_set_chunk_blocks(int blocks) { g_tune_chunk.store(blocks); }
 
 void nova_diag_set_stream_waves(int waves) { g_tune_waves.store(waves); }
+
+void nova_diag_set_variable_kernel(int kernel) { g_tune_kernel.store(kernel); }
 
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {

@@ -32,6 +32,7 @@ def _reset_tuning():
     L.nova_diag_set_blocks_per_group(0)
     L.nova_diag_set_stream_waves(0)
     L.nova_diag_set_variant(0)
+    L.nova_diag_set_variable_kernel(0)
 
 
 def dev(torch, arr, dtype=None):
@@ -503,7 +504,7 @@ def test_claim_counters_reset_between_launches(torch_gpu, oracle):
 
 @pytest.mark.parametrize("lanes,chunk,waves", [
     (0, 0, 0), (2, 0, 0), (4, 0, 0), (8, 0, 0), (16, 0, 0), (16, 9, 0), (16, 64, 0),
-    (8, 0, 3), (4, 40, 5), (16, 0, 1)])
+    (8, 0, 3), (4, 40, 5), (16, 0, 1), (16, 0, 12), (8, 0, 10)])
 def test_flat_many_blocks(torch_gpu, oracle, lanes, chunk, waves):
     """Flat kernel with enough blocks for every wave to switch descriptor
     banks and claim chunks many times, including the stealing tail: mixed
@@ -512,6 +513,7 @@ def test_flat_many_blocks(torch_gpu, oracle, lanes, chunk, waves):
     torch = torch_gpu
     C.set_tuning(lanes, 0)
     L = C.load()
+    L.nova_diag_set_variable_kernel(2)
     L.nova_diag_set_chunk_blocks(chunk)
     L.nova_diag_set_stream_waves(waves)
     rng = np.random.default_rng(1000 + lanes * 7 + chunk + waves)
@@ -536,15 +538,17 @@ def test_flat_many_blocks(torch_gpu, oracle, lanes, chunk, waves):
         assert bad.size == 0, [(int(offs[i]), int(lens[i])) for i in bad[:5]]
 
 
-@pytest.mark.parametrize("lanes,chunk", [(0, 0), (2, 0), (4, 0), (8, 0), (16, 0), (8, 16),
-                                         (4, 17), (16, 64)])
-def test_log_many_records(torch_gpu, oracle, lanes, chunk):
+@pytest.mark.parametrize("kernel,lanes,chunk", [
+    (0, 0, 0), (1, 4, 0), (1, 16, 0), (2, 0, 0), (2, 2, 0), (2, 4, 0), (2, 8, 0), (2, 16, 0),
+    (2, 8, 16), (2, 4, 17), (2, 16, 64)])
+def test_log_many_records(torch_gpu, oracle, kernel, lanes, chunk):
     """Log record CRC write + verify over a log image with enough records to
     exercise the header pipeline of the flat kernel's descriptor banks
     (db/log_writer.cc:99-114, db/log_reader.cc:251-262), every lane count."""
     torch = torch_gpu
     C.set_tuning(lanes, 0)
     C.load().nova_diag_set_chunk_blocks(chunk)
+    C.load().nova_diag_set_variable_kernel(kernel)
     rng = np.random.default_rng(77 + lanes + chunk)
     n = 60000
     plen = rng.integers(0, 700, n).astype(np.uint64)

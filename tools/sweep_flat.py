@@ -72,15 +72,17 @@ def set_variant(C, v: str) -> None:
     """"flat:G:chunk:waves:var" | "units:G:seg:waves:var" | "auto"."""
     L = C.load()
     if v == "auto":
-        v = "flat:0:0:0:0"
+        v = "auto:0:0:0:0"
     kind, g, x, w, var = v.split(":")
     g, x, w, var = int(g), int(x), int(w), int(var)
     L.nova_diag_set_variant(var)
     L.nova_diag_set_stream_waves(w)
     if kind == "flat":
+        L.nova_diag_set_variable_kernel(2)
         C.set_tuning(g, 0)
         L.nova_diag_set_chunk_blocks(x)
     else:
+        L.nova_diag_set_variable_kernel(1 if kind == "units" else 0)
         C.set_tuning(g, x)
         L.nova_diag_set_chunk_blocks(0)
 
@@ -129,7 +131,7 @@ def main() -> int:
                    "GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 8e12, 4)}
             rows.append(row)
             print(json.dumps(row), flush=True)
-        setv("flat:0:0:0:0")
+        setv("auto")
         del keep, fn
         torch.cuda.empty_cache()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
