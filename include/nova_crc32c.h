@@ -187,6 +187,9 @@ void nova_diag_set_stream_waves(int waves);
 /* Kernel for variable-length / unaligned batches: 0 auto (units kernel),
  * 1 units, 2 flat (per-group block streams).  Process-wide. */
 void nova_diag_set_variable_kernel(int kernel);
+/* XOR parity kernel variant: chunks per thread (bits 0-3), fragments loaded
+ * together (bits 4-7), workgroups per CU (bits 8-15); 0 fields = default. */
+void nova_diag_set_parity_variant(int variant);
 /* Units kernel: blocks per claimed wave chunk (1..16, default 8; 0 = default). */
 void nova_diag_set_chunk_blocks(int blocks);
 /* Plain coalesced streaming read of `bytes` (multiple of 16) with `wgs`

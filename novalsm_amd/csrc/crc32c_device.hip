@@ -1250,45 +1250,71 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
 // Loads are clamped to the aligned 16 B holding the fragment's last byte, so
 // nothing past the parity region's last 16-B line is touched; lanes past the
 // end re-read the last chunk and discard it.
-constexpr int kParityU = 4;
+//
+// FU fragments are loaded together (U * FU loads in flight per thread) when
+// they are all 16-B aligned; a group with an unaligned fragment takes them one
+// at a time through the funnel-shift path.
+template <int U, int FU>
 __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, const uint64_t* frag_off,
                                                          uint32_t n_frags, uint64_t parity_len,
                                                          uint8_t* out) {
   const uint64_t nchunks = (parity_len + 15) / 16;
   const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c0 < nchunks;
-       c0 += kParityU * nth) {
-    uint32_t x[kParityU][4] = {};
-    uint64_t cc[kParityU];
+       c0 += U * nth) {
+    uint32_t x[U][4] = {};
+    uint64_t cc[U];
 #pragma unroll
-    for (int k = 0; k < kParityU; k++) {
+    for (int k = 0; k < U; k++) {
       const uint64_t c = c0 + k * nth;
       cc[k] = c < nchunks ? c : nchunks - 1;
     }
-    for (uint32_t f = 0; f < n_frags; f++) {
+    uint32_t f = 0;
+    for (; f + FU <= n_frags; f += FU) {
+      uint64_t fa[FU];
+      uint32_t any_s = 0;
+#pragma unroll
+      for (int i = 0; i < FU; i++) {
+        fa[i] = (uint64_t)base + frag_off[f + i];
+        any_s |= (uint32_t)(fa[i] & 15);
+      }
+      if (any_s != 0) break;  // unaligned: the per-fragment path below
+      uint4 v[FU][U];
+#pragma unroll
+      for (int i = 0; i < FU; i++)
+#pragma unroll
+        for (int k = 0; k < U; k++) v[i][k] = gload16(fa[i] + 16 * cc[k]);
+#pragma unroll
+      for (int i = 0; i < FU; i++)
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+          x[k][0] ^= v[i][k].x; x[k][1] ^= v[i][k].y; x[k][2] ^= v[i][k].z; x[k][3] ^= v[i][k].w;
+        }
+    }
+    for (; f < n_frags; f++) {
       const uint64_t fa = (uint64_t)base + frag_off[f];
       const uint32_t s = (uint32_t)(fa & 15);
       const uint64_t fb = fa - s;                              // aligned line of byte 0
       const uint64_t lastline = (fa + parity_len - 1) & ~15ull;  // line of the last byte
       if (s == 0) {
-        uint4 v[kParityU];
+        uint4 v[U];
 #pragma unroll
-        for (int k = 0; k < kParityU; k++) v[k] = gload16(fb + 16 * cc[k]);
+        for (int k = 0; k < U; k++) v[k] = gload16(fb + 16 * cc[k]);
 #pragma unroll
-        for (int k = 0; k < kParityU; k++) {
+        for (int k = 0; k < U; k++) {
           x[k][0] ^= v[k].x; x[k][1] ^= v[k].y; x[k][2] ^= v[k].z; x[k][3] ^= v[k].w;
         }
       } else {
-        uint4 lo[kParityU], hi[kParityU];
+        uint4 lo[U], hi[U];
 #pragma unroll
-        for (int k = 0; k < kParityU; k++) {
+        for (int k = 0; k < U; k++) {
           const uint64_t l = fb + 16 * cc[k];
           lo[k] = gload16(l);
           hi[k] = gload16(l + 16 <= lastline ? l + 16 : lastline);
         }
         const uint32_t ws = s >> 2, bs = s & 3;
 #pragma unroll
-        for (int k = 0; k < kParityU; k++) {
+        for (int k = 0; k < U; k++) {
           const uint32_t w[8] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w,
                                  hi[k].x, hi[k].y, hi[k].z, hi[k].w};
 #pragma unroll
@@ -1304,12 +1330,13 @@ __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, co
       }
     }
 #pragma unroll
-    for (int k = 0; k < kParityU; k++) {
+    for (int k = 0; k < U; k++) {
       const uint64_t c = c0 + k * nth;
       if (c >= nchunks) break;
       const uint64_t o = 16 * c;
       if (o + 16 <= parity_len) {
-        *reinterpret_cast<uint4*>(out + o) = make_uint4(x[k][0], x[k][1], x[k][2], x[k][3]);
+        u32x4 val = {x[k][0], x[k][1], x[k][2], x[k][3]};
+        __builtin_nontemporal_store(val, (__attribute__((address_space(1))) u32x4*)(uint64_t)(out + o));
       } else {
         for (uint64_t i = o; i < parity_len; i++)
           out[i] = (uint8_t)(x[k][(i - o) >> 2] >> (8 * ((i - o) & 3)));
@@ -1317,7 +1344,6 @@ __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, co
     }
   }
 }
-
 
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
 __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
@@ -1417,6 +1443,7 @@ std::atomic<int> g_tune_var{0};
 std::atomic<int> g_tune_bpg{0};
 std::atomic<int> g_tune_chunk{0};
 std::atomic<int> g_tune_waves{0};  // waves per workgroup override (0 = per-kernel default)
+std::atomic<int> g_tune_parity{0};  // XOR parity kernel variant (0 = default)
 
 // Waves per workgroup.  The tables fill the CU's LDS, so a CU runs exactly one
 // workgroup; fewer waves keep fewer HBM reads in flight per CU, which the
@@ -1978,14 +2005,30 @@ int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_fra
   int err = 0;
   DevTables* t = tables(&err);
   if (!t) return err;
+  // variant: U (chunks per thread) x FU (fragments loaded together), grid cap
+  // in workgroups per CU; default from the sweep in profiles.
+  const int v = g_tune_parity.load();
+  const int u = (v & 0xf) ? (v & 0xf) : 2;  // sweep (profiles/r01_parity_sweep.log): 2 x 1
+  const int fu = ((v >> 4) & 0xf) ? ((v >> 4) & 0xf) : 1;  // x 8/CU best (71%), 4 x 2: 57%
+  const int per_cu = ((v >> 8) & 0xff) ? ((v >> 8) & 0xff) : 8;
   uint64_t chunks = (parity_len + 15) / 16;
-  uint64_t wgs = (chunks + 256 * kParityU - 1) / (256 * kParityU);
-  const uint64_t cap = (uint64_t)t->cus * 8;
+  uint64_t wgs = (chunks + 256 * (uint64_t)u - 1) / (256 * (uint64_t)u);
+  const uint64_t cap = (uint64_t)t->cus * per_cu;
   if (wgs > cap) wgs = cap;
-  hipLaunchKernelGGL(xor_parity_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream,
-                     (const uint8_t*)base, frag_offsets, (uint32_t)n_frags, (uint64_t)parity_len,
-                     (uint8_t*)out);
-  return (int)hipGetLastError();
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t* b = (const uint8_t*)base;
+  const uint32_t nf = (uint32_t)n_frags;
+  const uint64_t pl = (uint64_t)parity_len;
+  uint8_t* o = (uint8_t*)out;
+#define NOVA_XP(U_, FU_)                                                                      \
+  if (u == U_ && fu == FU_) {                                                                 \
+    hipLaunchKernelGGL((xor_parity_kernel<U_, FU_>), dim3(wgs), dim3(256), 0, st, b, frag_offsets, nf, pl, o); \
+    return (int)hipGetLastError();                                                            \
+  }
+  NOVA_XP(1, 1) NOVA_XP(2, 1) NOVA_XP(4, 1) NOVA_XP(4, 2) NOVA_XP(4, 4) NOVA_XP(2, 4) NOVA_XP(2, 2)
+  NOVA_XP(8, 1) NOVA_XP(8, 2)
+#undef NOVA_XP
+  return NOVA_E_INVAL;
 }
 
 int nova_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t first_word,
@@ -2082,6 +2125,8 @@ void nova_diag_set_chunk_blocks(int blocks) { g_tune_chunk.store(blocks); }
 void nova_diag_set_stream_waves(int waves) { g_tune_waves.store(waves); }
 
 void nova_diag_set_variable_kernel(int kernel) { g_tune_kernel.store(kernel); }
+
+void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
 
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {

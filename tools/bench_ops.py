@@ -66,6 +66,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--n", type=int, default=1 << 20, help="blocks for trailers/verify")
+    ap.add_argument("--parity-sweep", default="",
+                    help="comma list of nova_diag_set_parity_variant values (tuning)")
     ap.add_argument("--lanes-sweep", action="store_true",
                     help="also time each CRC op at 4/8/16 lanes per unit (tuning)")
     args = ap.parse_args()
@@ -198,6 +200,16 @@ def main() -> int:
                 want ^= buf[f * plen + i:f * plen + i + 4096].cpu().numpy()
             ok &= np.array_equal(out[i:i + 4096].cpu().numpy(), want)
         emit("parity", f"{k} fragments x {plen >> 20} MiB", (k + 1) * plen, sec, ok)
+        if args.parity_sweep:
+            L = C.load()
+            for v in args.parity_sweep.split(","):
+                L.nova_diag_set_parity_variant(int(v, 0))
+                sec = timed(torch, lambda: C.xor_parity(buf, fo, plen, out=out, stream=stream),
+                            args.steps, args.warmup, stream)
+                gbs = (k + 1) * plen / sec / 1e9
+                print(json.dumps({"sweep": "parity", "variant": v, "GBps": round(gbs, 1),
+                                  "frac": round(gbs / HBM_PEAK_GBS, 4)}), flush=True)
+            L.nova_diag_set_parity_variant(0)
 
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "bench_ops.json"), "w") as f:
