@@ -152,7 +152,7 @@ int nova_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t first
 int nova_device_init(void);
 /* Lanes per block ("G") and segment bytes the dispatcher would pick for an
  * aligned fixed-stride batch; returns 1 for the streaming kernel, 0 for the
- * units kernel.  nova_crc32c_describe writes a JSON object naming the kernel
+ * units kernel, 2 for the flat kernel, 3 for the rounds kernel.  nova_crc32c_describe writes a JSON object naming the kernel
  * and its launch parameters (for reports and profiles). */
 int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_unit,
                      uint32_t* seg_bytes);
@@ -184,9 +184,13 @@ int nova_diag_read_ceiling(const void* base, size_t bytes, uint32_t* out_dev, in
 /* Waves per workgroup for the batch kernels (1..16, flat kernel <= 12; 0 =
  * per-kernel default). */
 void nova_diag_set_stream_waves(int waves);
-/* Kernel for variable-length / unaligned batches: 0 auto (units kernel),
- * 1 units, 2 flat (per-group block streams).  Process-wide. */
+/* Kernel for variable-length / unaligned batches: 0 auto, 1 units, 2 flat
+ * (per-group block streams), 3 rounds (sorted batch, lockstep rounds).
+ * Process-wide. */
 void nova_diag_set_variable_kernel(int kernel);
+/* Rounds kernel: take the batch in order (0), sort it by block step count
+ * first (1, a pre-pass), or sort each claimed chunk of 64 blocks (2, default). */
+void nova_diag_set_rounds_sort(int on);
 /* XOR parity kernel variant: chunks per thread (bits 0-3), fragments loaded
  * together (bits 4-7), workgroups per CU (bits 8-15); 0 fields = default. */
 void nova_diag_set_parity_variant(int variant);

@@ -83,6 +83,7 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
         "nova_diag_set_stream_waves": (None, [i32]),
         "nova_diag_set_variable_kernel": (None, [i32]),
         "nova_diag_set_parity_variant": (None, [i32]),
+        "nova_diag_set_rounds_sort": (None, [i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

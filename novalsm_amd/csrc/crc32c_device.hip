@@ -94,6 +94,8 @@ struct CrcParams {
   // read word 0 of zline through a zero mask; offset = offsets[i & omask] +
   // i * stride, length = lengths[i & lmask] + len, init = init[i & imask].
   uint64_t omask, lmask, imask;
+  const uint32_t* perm;      // rounds kernel: block index per sorted position (or null)
+  uint32_t sort_local;       // rounds kernel: sort each chunk's blocks by step count
 };
 
 // ---- device helpers --------------------------------------------------------
@@ -833,6 +835,150 @@ __device__ __forceinline__ uint32_t sel5(uint32_t k, uint32_t a, uint32_t b, uin
   return k == 0 ? a : k == 1 ? b : k == 2 ? c : k == 3 ? d : e;
 }
 
+// ---- shared by the flat and rounds kernels ---------------------------------
+// Issue one 4-swath step of a block region for this lane (pieces before the
+// block's first line, or of an invalid group, read the zero line) plus, on the
+// block's last step, its tail line(s).
+template <int G, int VAR, bool kTail2>
+__device__ __forceinline__ void load_step(FlatSet& X, uint64_t lp, uint64_t u0, uint64_t u1,
+                                          uint64_t end, bool v, bool last, uint64_t zl, int q) {
+  const uint64_t A0 = u0 & ~15ull;
+  const bool nz = v && u1 > u0;
+  const uint64_t pa = lp + 16 * q;
+  const uint64_t a0 = pa, a1 = pa + 16 * G, a2 = pa + 32 * G, a3 = pa + 48 * G;
+  X.d0 = gload16<VAR>((nz && a0 >= A0) ? a0 : zl);
+  X.d1 = gload16<VAR>((nz && a1 >= A0) ? a1 : zl);
+  X.d2 = gload16<VAR>((nz && a2 >= A0) ? a2 : zl);
+  X.d3 = gload16<VAR>((nz && a3 >= A0) ? a3 : zl);
+  if constexpr (kTail2) {
+    const uint64_t ta = last ? end : zl;  // holds the stored CRC's first byte
+    X.t = gload16<VAR>(ta);
+    X.t2 = gload16<VAR>((last && u1 + 4 > end + 16) ? end + 16 : ta);
+  } else {
+    X.t = gload16<VAR>((last && nz && (u1 & 15)) ? end : zl);
+  }
+}
+
+// Mask the head pieces of a step (bytes before u0, ~init at u0) and run it
+// through the lane's four stream registers.
+template <int G, int VAR, bool kTail2>
+__device__ __forceinline__ void fold_step(const uint8_t* lds, const FlatSet& Y, int q, uint32_t& c0,
+                                          uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t lo0,
+                                          uint32_t lo1, uint32_t lo2, uint32_t lo3) {
+  const uint64_t pa = Y.pa + 16 * q;
+  const uint64_t lim = Y.u0 + 4;  // pieces starting before this need masking / init
+  uint4 d0 = Y.d0, d1 = Y.d1, d2 = Y.d2, d3 = Y.d3;
+  if (pa < lim) d0 = fix_piece(d0, pa, Y.u0, Y.u1, Y.ninit);
+  if (pa + 16 * G < lim) d1 = fix_piece(d1, pa + 16 * G, Y.u0, Y.u1, Y.ninit);
+  if (pa + 32 * G < lim) d2 = fix_piece(d2, pa + 32 * G, Y.u0, Y.u1, Y.ninit);
+  if (pa + 48 * G < lim) d3 = fix_piece(d3, pa + 48 * G, Y.u0, Y.u1, Y.ninit);
+  fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+  // the tail line(s) are used only on a block's last step: consume anyway, so
+  // the compiler resolves their loads here with an exact count
+  asm volatile("" ::"v"(Y.t.x), "v"(Y.t.y), "v"(Y.t.z), "v"(Y.t.w));
+  if constexpr (kTail2) asm volatile("" ::"v"(Y.t2.x), "v"(Y.t2.y), "v"(Y.t2.z), "v"(Y.t2.w));
+}
+
+// A block's result from the group's pending word v (its region ended at
+// E = u1 & ~15): finish the register with the tail bytes [E,u1), add M_n(~init)
+// for blocks shorter than 4 bytes, apply the mode's epilogue.  The memory
+// write is returned (wb_*) and issued later (write_result).
+template <int MODE>
+__device__ __forceinline__ void finish_block(const uint8_t* lds, uint32_t byte_tab, const CrcParams& p,
+                                             bool raw, uint32_t v, const FlatSet& Y, uint64_t& wb_a,
+                                             uint32_t& wb_v) {
+  constexpr bool kLog = MODE == kLogWrite || MODE == kLogVerify;
+  const uint64_t E = Y.u1 & ~15ull;
+  const uint32_t nb = (uint32_t)(Y.u1 - E);
+  uint32_t R = tapply(lds, 0, v);  // register at E
+  {
+    const uint32_t w0 = fix_word(Y.t.x, E + 0, Y.u0, Y.u1, Y.ninit);
+    const uint32_t w1 = fix_word(Y.t.y, E + 4, Y.u0, Y.u1, Y.ninit);
+    const uint32_t w2 = fix_word(Y.t.z, E + 8, Y.u0, Y.u1, Y.ninit);
+    const uint32_t w3 = fix_word(Y.t.w, E + 12, Y.u0, Y.u1, Y.ninit);
+    uint32_t r;
+    r = tapply(lds, 0, R ^ w0);
+    R = nb >= 4 ? r : R;
+    r = tapply(lds, 0, R ^ w1);
+    R = nb >= 8 ? r : R;
+    r = tapply(lds, 0, R ^ w2);
+    R = nb >= 12 ? r : R;
+    const uint32_t wl = sel5(nb >> 2, w0, w1, w2, w3, 0u);
+    const uint32_t nr = nb & 3u;
+    r = (R >> 8) ^ lds_u32(lds, byte_tab + ((R ^ wl) & 255u) * 4u);
+    R = nr >= 1 ? r : R;
+    r = (R >> 8) ^ lds_u32(lds, byte_tab + ((R ^ (wl >> 8)) & 255u) * 4u);
+    R = nr >= 2 ? r : R;
+    r = (R >> 8) ^ lds_u32(lds, byte_tab + ((R ^ (wl >> 16)) & 255u) * 4u);
+    R = nr >= 3 ? r : R;
+  }
+  // n < 4: the data ran from a zero register; add the init's part M_n(~init)
+  // (no loads here: a load in this branch would make the compiler drain
+  // the prefetch at the loop head).
+  const uint32_t nn = (uint32_t)(Y.u1 - Y.u0);
+  if (nn < 4 && !raw) {
+    uint32_t l = ~(kLog ? 0u : Y.st);
+    for (uint32_t i = 0; i < 3; i++) {
+      const uint32_t r = (l >> 8) ^ lds_u32(lds, byte_tab + (l & 255u) * 4u);
+      l = i < nn ? r : l;
+    }
+    R ^= l;
+  }
+  uint32_t crc = raw ? R : ~R;
+  if constexpr (kLog) {
+    wb_a = Y.u0 - 6;
+    wb_v = mask_crc(crc);  // db/log_writer.cc:113
+    if constexpr (MODE == kLogVerify) {
+      wb_a = (uint64_t)(p.ok_out + Y.rec);
+      wb_v = unmask_crc(Y.st) == crc ? 1u : 0u;  // db/log_reader.cc:254-256
+    }
+  } else if constexpr (MODE == kVerify) {
+    const uint32_t k = nb >> 2;
+    const uint32_t wlo = sel5(k, Y.t.x, Y.t.y, Y.t.z, Y.t.w, Y.t2.x);
+    const uint32_t whi = sel5(k, Y.t.y, Y.t.z, Y.t.w, Y.t2.x, Y.t2.y);
+    const uint32_t stored = __builtin_amdgcn_alignbyte(whi, wlo, nb & 3u);
+    wb_a = (uint64_t)(p.ok_out + Y.rec);
+    wb_v = unmask_crc(stored) == crc ? 1u : 0u;  // table/table.cc:435-437
+  } else {
+    if (p.flags & NOVA_CRC32C_APPEND_TYPE) crc = ~byte_step(~crc, (p.flags >> 8) & 0xffu);
+    if constexpr (MODE == kTrailer) {
+      wb_a = Y.u1;
+      wb_v = mask_crc(crc);
+    } else {
+      if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
+      wb_a = (uint64_t)(p.out + Y.rec);
+      wb_v = crc;
+    }
+  }
+}
+
+// Issue a finished block's memory write.  Global (not flat) stores: a flat
+// store would also count as an LDS access the table lookups must wait for.
+template <int MODE>
+__device__ __forceinline__ void write_result(const CrcParams& p, uint64_t wb_a, uint32_t wb_v) {
+  typedef __attribute__((address_space(1))) uint8_t gu8;
+  typedef __attribute__((address_space(1))) uint32_t gu32;
+  if constexpr (MODE == kLogWrite) {
+    gu8* h = (gu8*)wb_a;
+    h[0] = (uint8_t)wb_v;
+    h[1] = (uint8_t)(wb_v >> 8);
+    h[2] = (uint8_t)(wb_v >> 16);
+    h[3] = (uint8_t)(wb_v >> 24);
+  } else if constexpr (MODE == kLogVerify || MODE == kVerify) {
+    *(gu8*)wb_a = (uint8_t)wb_v;
+    if (!wb_v && p.n_bad) atomicAdd(p.n_bad, 1u);
+  } else if constexpr (MODE == kTrailer) {
+    gu8* d = (gu8*)wb_a;
+    d[0] = (uint8_t)(p.flags >> 8);
+    d[1] = (uint8_t)wb_v;
+    d[2] = (uint8_t)(wb_v >> 8);
+    d[3] = (uint8_t)(wb_v >> 16);
+    d[4] = (p.flags & NOVA_TRAILER_TB_QUIRK) ? (uint8_t)'!' : (uint8_t)(wb_v >> 24);
+  } else {
+    *(gu32*)wb_a = wb_v;
+  }
+}
+
 template <int G, int MODE, int VAR = 0>
 __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1046,26 +1192,12 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
   auto issue = [&](FlatSet& X) -> bool {
     const bool v = g_valid;
     const bool last = v && (g_lp + kStep == g_end);
-    const uint64_t A0 = g_u0 & ~15ull;
-    const bool nz = v && g_u1 > g_u0;
-    const uint64_t pa = g_lp + 16 * q;
-    const uint64_t a0 = pa, a1 = pa + 16 * G, a2 = pa + 32 * G, a3 = pa + 48 * G;
-    X.d0 = gload16<VAR>((nz && a0 >= A0) ? a0 : zl);
-    X.d1 = gload16<VAR>((nz && a1 >= A0) ? a1 : zl);
-    X.d2 = gload16<VAR>((nz && a2 >= A0) ? a2 : zl);
-    X.d3 = gload16<VAR>((nz && a3 >= A0) ? a3 : zl);
-    if constexpr (kTail2) {
-      const uint64_t ta = last ? g_end : zl;  // holds the stored CRC's first byte
-      X.t = gload16<VAR>(ta);
-      X.t2 = gload16<VAR>((last && g_u1 + 4 > g_end + 16) ? g_end + 16 : ta);
-    } else {
-      X.t = gload16<VAR>((last && nz && (g_u1 & 15)) ? g_end : zl);
-    }
+    load_step<G, VAR, kTail2>(X, g_lp, g_u0, g_u1, g_end, v, last, zl, q);
     X.pa = g_lp;
     X.u0 = g_u0;
     X.u1 = g_u1;
     X.rec = g_rec;
-    X.ninit = g_ninit;
+    X.ninit = v ? g_ninit : 0u;
     X.st = g_st;
     X.valid = v;
     X.last = last;
@@ -1079,112 +1211,20 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
   uint64_t wb_a = 0;
   uint32_t wb_v = 0;
   auto fold = [&](FlatSet& Y) {
-    const uint64_t pa = Y.pa + 16 * q;
-    const uint64_t lim = Y.u0 + 4;  // pieces starting before this need masking / init
-    uint4 d0 = Y.d0, d1 = Y.d1, d2 = Y.d2, d3 = Y.d3;
-    if (pa < lim) d0 = fix_piece(d0, pa, Y.u0, Y.u1, Y.ninit);
-    if (pa + 16 * G < lim) d1 = fix_piece(d1, pa + 16 * G, Y.u0, Y.u1, Y.ninit);
-    if (pa + 32 * G < lim) d2 = fix_piece(d2, pa + 32 * G, Y.u0, Y.u1, Y.ninit);
-    if (pa + 48 * G < lim) d3 = fix_piece(d3, pa + 48 * G, Y.u0, Y.u1, Y.ninit);
-    fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
-    // the tail line(s) are used only on a block's last step: consume anyway
-    asm volatile("" ::"v"(Y.t.x), "v"(Y.t.y), "v"(Y.t.z), "v"(Y.t.w));
-    if constexpr (kTail2) asm volatile("" ::"v"(Y.t2.x), "v"(Y.t2.y), "v"(Y.t2.z), "v"(Y.t2.w));
+    fold_step<G, VAR, kTail2>(lds, Y, q, c0, c1, c2, c3, lo0, lo1, lo2, lo3);
     if (Y.last) {  // group-uniform
       const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
       c0 = c1 = c2 = c3 = 0;
-      const uint64_t E = Y.u1 & ~15ull;
-      const uint32_t nb = (uint32_t)(Y.u1 - E);
-      uint32_t R;
-      {
-        R = tapply(lds, 0, v);  // register at E
-        const uint32_t w0 = fix_word(Y.t.x, E + 0, Y.u0, Y.u1, Y.ninit);
-        const uint32_t w1 = fix_word(Y.t.y, E + 4, Y.u0, Y.u1, Y.ninit);
-        const uint32_t w2 = fix_word(Y.t.z, E + 8, Y.u0, Y.u1, Y.ninit);
-        const uint32_t w3 = fix_word(Y.t.w, E + 12, Y.u0, Y.u1, Y.ninit);
-        uint32_t r;
-        r = tapply(lds, 0, R ^ w0);
-        R = nb >= 4 ? r : R;
-        r = tapply(lds, 0, R ^ w1);
-        R = nb >= 8 ? r : R;
-        r = tapply(lds, 0, R ^ w2);
-        R = nb >= 12 ? r : R;
-        const uint32_t wl = sel5(nb >> 2, w0, w1, w2, w3, 0u);
-        const uint32_t nr = nb & 3u;
-        r = (R >> 8) ^ lds_u32(lds, kByteTab + ((R ^ wl) & 255u) * 4u);
-        R = nr >= 1 ? r : R;
-        r = (R >> 8) ^ lds_u32(lds, kByteTab + ((R ^ (wl >> 8)) & 255u) * 4u);
-        R = nr >= 2 ? r : R;
-        r = (R >> 8) ^ lds_u32(lds, kByteTab + ((R ^ (wl >> 16)) & 255u) * 4u);
-        R = nr >= 3 ? r : R;
-      }
-      // n < 4: the data ran from a zero register; add the init's part M_n(~init)
-      // (no loads here: a load in this branch would make the compiler drain
-      // the prefetch at the loop head).
-      const uint32_t nn = (uint32_t)(Y.u1 - Y.u0);
-      if (nn < 4 && !raw) {
-        uint32_t l = ~(kLog ? 0u : Y.st);
-        for (uint32_t i = 0; i < 3; i++) {
-          const uint32_t r = (l >> 8) ^ lds_u32(lds, kByteTab + (l & 255u) * 4u);
-          l = i < nn ? r : l;
-        }
-        R ^= l;
-      }
-      uint32_t crc = raw ? R : ~R;
-      // The memory writes wait until after the next step's loads are issued
-      // (writeback): a store here would make the compiler drain the
-      // prefetch before the store's address registers are reused.
+      // The memory write waits until after the next step's loads are issued
+      // (writeback): a store here would make the compiler drain the prefetch
+      // before the store's address registers are reused.
+      finish_block<MODE>(lds, kByteTab, p, raw, v, Y, wb_a, wb_v);
       wb_on = q == 0;
-      if constexpr (kLog) {
-        wb_a = Y.u0 - 6;
-        wb_v = mask_crc(crc);  // db/log_writer.cc:113
-        if constexpr (MODE == kLogVerify) {
-          wb_a = (uint64_t)(p.ok_out + Y.rec);
-          wb_v = unmask_crc(Y.st) == crc ? 1u : 0u;  // db/log_reader.cc:254-256
-        }
-      } else if constexpr (MODE == kVerify) {
-        const uint32_t k = nb >> 2;
-        const uint32_t wlo = sel5(k, Y.t.x, Y.t.y, Y.t.z, Y.t.w, Y.t2.x);
-        const uint32_t whi = sel5(k, Y.t.y, Y.t.z, Y.t.w, Y.t2.x, Y.t2.y);
-        const uint32_t stored = __builtin_amdgcn_alignbyte(whi, wlo, nb & 3u);
-        wb_a = (uint64_t)(p.ok_out + Y.rec);
-        wb_v = unmask_crc(stored) == crc ? 1u : 0u;  // table/table.cc:435-437
-      } else {
-        if (p.flags & NOVA_CRC32C_APPEND_TYPE) crc = ~byte_step(~crc, (p.flags >> 8) & 0xffu);
-        if constexpr (MODE == kTrailer) {
-          wb_a = Y.u1;
-          wb_v = mask_crc(crc);
-        } else {
-          if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
-          wb_a = (uint64_t)(p.out + Y.rec);
-          wb_v = crc;
-        }
-      }
     }
   };
   auto writeback = [&]() {
-    typedef __attribute__((address_space(1))) uint8_t gu8;  // global, not flat: a flat
-    typedef __attribute__((address_space(1))) uint32_t gu32;  // store would wait on LDS too
     if (wb_on) {
-      if constexpr (MODE == kLogWrite) {
-        gu8* h = (gu8*)wb_a;
-        h[0] = (uint8_t)wb_v;
-        h[1] = (uint8_t)(wb_v >> 8);
-        h[2] = (uint8_t)(wb_v >> 16);
-        h[3] = (uint8_t)(wb_v >> 24);
-      } else if constexpr (MODE == kLogVerify || MODE == kVerify) {
-        *(gu8*)wb_a = (uint8_t)wb_v;
-        if (!wb_v && p.n_bad) atomicAdd(p.n_bad, 1u);
-      } else if constexpr (MODE == kTrailer) {
-        gu8* d = (gu8*)wb_a;
-        d[0] = (uint8_t)(p.flags >> 8);
-        d[1] = (uint8_t)wb_v;
-        d[2] = (uint8_t)(wb_v >> 8);
-        d[3] = (uint8_t)(wb_v >> 16);
-        d[4] = (p.flags & NOVA_TRAILER_TB_QUIRK) ? (uint8_t)'!' : (uint8_t)(wb_v >> 24);
-      } else {
-        *(gu32*)wb_a = wb_v;
-      }
+      write_result<MODE>(p, wb_a, wb_v);
       wb_on = false;
     }
   };
@@ -1237,6 +1277,449 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
   // The last claim (if any) must have returned before this workgroup counts
   // itself finished: the last workgroup then zeroes the counters.
   __builtin_amdgcn_s_waitcnt(0);
+  sched_release(p.sched);
+}
+
+// ---- binning pre-pass + crc32c_rounds_kernel<G, MODE> ------------------------
+// Variable-length batches in ROUNDS: the wave's lane groups take kGroups blocks
+// at a time, all padded to the round's step count (its largest block, end-
+// aligned, so shorter blocks start later on zero pieces that leave a zero
+// register unchanged).  Every group starts and ends the round together, so the
+// per-block work (group fold, tail, epilogue) runs once per round for all
+// groups, not divergently per block as in the flat kernel; the loads stream
+// across rounds and chunks as in the stream kernel.  For the rounds to be
+// even, a pre-pass sorts the batch by step count, largest first (a counting
+// sort into 256 classes: exact below 128 steps, 16 per octave above), which
+// also hands the last, smallest work to the tail of the launch.
+
+constexpr int kBins = 256;
+
+__device__ __forceinline__ uint32_t steps_class(uint64_t S) {
+  if (S < 128) return (uint32_t)S;
+  const uint32_t lg = 63u - (uint32_t)__builtin_clzll(S);  // >= 7
+  const uint32_t c = 128u + (lg - 7u) * 16u + (uint32_t)((S >> (lg - 4)) & 15u);
+  return c > 255u ? 255u : c;
+}
+
+// Step count of block b (region [A0, E) in kStep-byte steps), as the rounds
+// kernel computes it; rank = 255 - class orders the largest first.
+template <int MODE>
+__device__ __forceinline__ uint32_t block_rank(const CrcParams& p, uint64_t b, uint64_t kStep) {
+  constexpr bool kLog = MODE == kLogWrite || MODE == kLogVerify;
+  uint64_t a = (uint64_t)p.base + p.offsets[b & p.omask] + b * p.stride;
+  uint32_t n;
+  if constexpr (kLog) {
+    const uint8_t* h = (const uint8_t*)a;
+    n = 1u + ((uint32_t)h[4] | ((uint32_t)h[5] << 8));
+    a += 6;
+  } else {
+    n = p.lengths[b & p.lmask] + p.len + (MODE == kVerify ? 1u : 0u);
+  }
+  const uint64_t E = (a + n) & ~15ull, A0 = a & ~15ull;
+  uint64_t S = (E - A0 + kStep - 1) / kStep;
+  if (S == 0) S = 1;
+  return 255u - steps_class(S);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) bin_count_kernel(CrcParams p, uint64_t kStep, uint32_t* hist) {
+  __shared__ uint32_t h[kBins];
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < p.n_blocks; b += nth)
+    atomicAdd(&h[block_rank<MODE>(p, b, kStep)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// hist -> cursor: exclusive prefix over the ranks (one workgroup of kBins threads).
+__global__ void __launch_bounds__(kBins) bin_scan_kernel(const uint32_t* hist, uint32_t* cursor) {
+  __shared__ uint32_t t[kBins];
+  const int i = threadIdx.x;
+  t[i] = hist[i];
+  __syncthreads();
+  for (int d = 1; d < kBins; d <<= 1) {
+    const uint32_t v = i >= d ? t[i - d] : 0u;
+    __syncthreads();
+    t[i] += v;
+    __syncthreads();
+  }
+  cursor[i] = t[i] - hist[i];
+}
+
+// Same grid-stride assignment as bin_count_kernel: each workgroup reserves its
+// ranges per class with one atomic, then places its blocks.
+template <int MODE>
+__global__ void __launch_bounds__(256) bin_scatter_kernel(CrcParams p, uint64_t kStep, uint32_t* cursor,
+                                                          uint32_t* perm) {
+  __shared__ uint32_t h[kBins];
+  __shared__ uint32_t base[kBins];
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < p.n_blocks; b += nth)
+    atomicAdd(&h[block_rank<MODE>(p, b, kStep)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) {
+    base[i] = h[i] ? atomicAdd(&cursor[i], h[i]) : 0u;
+    h[i] = 0;
+  }
+  __syncthreads();
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < p.n_blocks; b += nth) {
+    const uint32_t r = block_rank<MODE>(p, b, kStep);
+    perm[base[r] + atomicAdd(&h[r], 1u)] = (uint32_t)b;
+  }
+}
+
+template <int G, int MODE, int VAR = 0>
+__global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
+  constexpr uint32_t kByteTab = kMainBytes + kLevels * kTreeBytes;
+  constexpr bool kLog = MODE == kLogWrite || MODE == kLogVerify;
+  constexpr bool kTail2 = MODE == kVerify;
+  constexpr uint64_t kStep = 64 * G;
+  constexpr uint32_t kGroups = 64 / G;
+  {
+    const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
+    uint4* d = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += blockDim.x) d[i] = s[i];
+    const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
+    uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
+    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += blockDim.x) d2[i] = s2[i];
+    const uint4* s3 = reinterpret_cast<const uint4*>(p.tab_byte);
+    uint4* d3 = reinterpret_cast<uint4*>(lds + kByteTab);
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) d3[i] = s3[i];
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane & (G - 1);
+  const int grp = lane / G;
+  const uint32_t rep = (uint32_t)(lane & 31) << 2;
+  const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
+  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
+  const uint32_t extra = (MODE == kVerify) ? 1u : 0u;  // verify covers block + type byte
+  const uint64_t zl = (uint64_t)p.zline;
+  const uint64_t base = (uint64_t)p.base;
+  const uint32_t C = p.chunk;  // sorted positions per chunk: R rounds of kGroups, <= 64
+  const uint32_t R = C / kGroups;
+  const uint32_t nwg = gridDim.x;
+  const uint32_t nwaves = blockDim.x >> 6;
+
+  // ---- chunk claims (as the flat kernel) ---------------------------------------
+  uint32_t victim = blockIdx.x, tried = 0, req = 0;
+  auto claim = [&](uint32_t v) {
+    uint32_t r = 0;
+    if (lane == 0)
+      r = __hip_atomic_fetch_add(p.sched + v * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    req = r;
+  };
+  auto chunk_of = [&](uint32_t v, uint32_t idx) -> uint64_t {
+    const uint64_t c = ((uint64_t)idx + nwaves) * nwg + v;
+    return c < p.n_chunks ? c : kNoChunk;
+  };
+  auto collect = [&]() -> uint64_t {
+    uint64_t c = chunk_of(victim, __builtin_amdgcn_readfirstlane(req));
+    while (c == kNoChunk && ++tried < p.steal_limit + 1) {
+      victim = (victim + 1) % nwg;
+      claim(victim);
+      c = chunk_of(victim, __builtin_amdgcn_readfirstlane(req));
+    }
+    return c;
+  };
+
+  // ---- descriptor pipeline: lane l holds chunk slot l -----------------------------
+  // The next chunk is loaded in stages at fixed points of the two-step loop body
+  // (stage 1 in a first take, 2 in the second, 3 in the next first, 4 in the next
+  // second), each from values loaded a step or more before, into "nxt"
+  // registers holding computed values, which a bank switch copies to "cur"
+  // without waiting on any load.  A switch that finds nxt not yet ready stalls
+  // the load side (empty steps) until it is: no stage ever runs out of order.
+  constexpr uint32_t kNone = 0xffffffffu;  // no chunk (chunk ids fit 32 bits: n < 2^38)
+  uint32_t t_rec = 0, t_olo = 0, t_ohi = 0, t_len = 0, t_aux = 0;
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0;
+  uint64_t n_u0 = 0, c_u0 = 0;
+  uint32_t n_n = 0, n_rec = 0, n_aux = 0, c_n = 0, c_rec = 0, c_aux = 0;
+  uint32_t t_ok = 0, n_ok = 0, c_ok = 0;  // slot holds a block of the batch
+  uint32_t n_chunk = kNone, c_chunk = kNone, t_chunk = kNone;
+  // wave-uniform state packed in one word (fewer scalar registers)
+  constexpr uint32_t fReady = 1, fRefill = 2, fDry = 4, fDone = 8, fRoundDone = 16, fClaim = 32;
+  uint32_t fl = 0;
+  uint32_t stage = 0;  // next pipeline stage due (0: none)
+  const uint32_t my = (uint32_t)lane < C ? (uint32_t)lane : C - 1;
+  // Sort the loaded chunk's slots by step count, largest first (rank by
+  // shuffles, inverse permutation through the wave's LDS scratch), so each
+  // round's blocks have similar lengths while the chunk keeps its locality.
+  uint32_t* const sortbuf = reinterpret_cast<uint32_t*>(lds + kByteTab + 1024u) + wave * 64;
+  auto sort_nxt = [&]() {
+    n_ok = t_ok;
+    if (!p.sort_local) return;
+    uint32_t S = 0;
+    if (t_ok) {
+      const uint64_t E = (n_u0 + n_n) & ~15ull;
+      const uint64_t s64 = (E - (n_u0 & ~15ull) + kStep - 1) / kStep;
+      S = s64 == 0 ? 1u : (s64 > 0xffffffffull ? 0xffffffffu : (uint32_t)s64);
+    }
+    uint32_t rank = 0;
+    for (int j = 0; j < 64; j++) {
+      const uint32_t sj = __shfl(S, j);
+      rank += (sj > S || (sj == S && j < lane)) ? 1u : 0u;
+    }
+    sortbuf[rank] = (uint32_t)lane;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int src = (int)sortbuf[lane];
+    const uint32_t ulo = __shfl((uint32_t)n_u0, src), uhi = __shfl((uint32_t)(n_u0 >> 32), src);
+    n_u0 = ((uint64_t)uhi << 32) | ulo;
+    n_n = __shfl(n_n, src);
+    n_rec = __shfl(n_rec, src);
+    n_aux = __shfl(n_aux, src);
+    n_ok = __shfl(t_ok, src);
+  };
+  auto pipe = [&](uint32_t st) {  // run stage st (its inputs are complete or waited for)
+    if (st == 1) {
+      uint64_t pos = (uint64_t)(t_chunk == kNone ? 0u : t_chunk) * C + my;
+      t_ok = (t_chunk != kNone && (uint32_t)lane < C && pos < p.n_blocks) ? 1u : 0u;
+      if (pos >= p.n_blocks) pos = p.n_blocks - 1;
+      t_rec = p.perm ? p.perm[pos] : (uint32_t)pos;
+      stage = 2;
+    } else if (st == 2) {
+      const uint64_t o = p.offsets[t_rec & p.omask];
+      t_olo = (uint32_t)o;
+      t_ohi = (uint32_t)(o >> 32);
+      if constexpr (!kLog) {
+        t_len = p.lengths[t_rec & p.lmask];
+        t_aux = p.init[t_rec & p.imask];
+      }
+      stage = 3;
+    } else if (st == 3) {
+      const uint64_t a = base + (((uint64_t)t_ohi << 32) | t_olo) + (uint64_t)t_rec * p.stride;
+      if constexpr (kLog) {
+        const uint8_t* h = (const uint8_t*)a;
+        h4 = h[4];
+        h5 = h[5];
+        if constexpr (MODE == kLogVerify) {
+          h0 = h[0];
+          h1 = h[1];
+          h2 = h[2];
+          h3 = h[3];
+        }
+        stage = 4;
+      } else {
+        n_u0 = a;
+        n_n = t_len + p.len + extra;
+        n_rec = t_rec;
+        n_aux = t_aux;
+        n_chunk = t_chunk;
+        sort_nxt();
+        fl |= fReady;
+        stage = 0;
+      }
+    } else if (st == 4) {
+      n_u0 = base + (((uint64_t)t_ohi << 32) | t_olo) + 6;  // CRC input: type byte + payload
+      n_n = 1u + (h4 | (h5 << 8));                          // db/log_format.h:27-30
+      n_rec = t_rec;
+      n_aux = h0 | (h1 << 8) | (h2 << 16) | (h3 << 24);
+      n_chunk = t_chunk;
+      sort_nxt();
+      fl |= fReady;
+      stage = 0;
+    }
+  };
+  auto start_refill = [&](uint32_t chunk) {  // stage 1 of chunk (or none)
+    t_chunk = chunk;
+    if (chunk == kNone) {
+      n_chunk = kNone;
+      fl |= fReady;
+      stage = 0;
+    } else {
+      pipe(1);
+    }
+  };
+
+  // ---- rounds (load side; group-uniform / wave-uniform state) ---------------------
+  uint64_t g_u0 = 0, g_u1 = 0, g_lp = 0, g_end = 0, g_rec = 0;
+  uint32_t g_ninit = 0, g_st = 0;
+  bool g_valid = false;
+  uint32_t r_idx = R, r_step = 0, r_S = 0;
+  // Take the next non-empty round (switching chunks as needed).  Returns with
+  // r_S == 0 if the switch must wait for nxt (stall) or the work is done.
+  auto next_round = [&]() {
+    r_S = 0;
+    g_valid = false;
+    for (;;) {
+      if (r_idx == R) {  // chunk exhausted: switch to nxt, start loading the one after
+        if (!(fl & fReady)) return;  // stall: nxt still in the pipeline
+        c_u0 = n_u0;
+        c_n = n_n;
+        c_rec = n_rec;
+        c_aux = n_aux;
+        c_ok = n_ok;
+        c_chunk = n_chunk;
+        fl &= ~fReady;
+        r_idx = 0;
+        if (c_chunk == kNone) {
+          fl |= fDone;
+          return;
+        }
+        fl |= fRefill;
+      }
+      const uint32_t slot = r_idx * kGroups + (uint32_t)grp;
+      r_idx++;
+      const bool ok = __shfl(c_ok, (int)slot) != 0;
+      const uint32_t a_lo = __shfl((uint32_t)c_u0, (int)slot);
+      const uint32_t a_hi = __shfl((uint32_t)(c_u0 >> 32), (int)slot);
+      const uint32_t n = __shfl(c_n, (int)slot);
+      const uint32_t rec = __shfl(c_rec, (int)slot);
+      const uint32_t aux = __shfl(c_aux, (int)slot);
+      const uint64_t a = ((uint64_t)a_hi << 32) | a_lo;
+      g_valid = ok;
+      g_u0 = a;
+      g_u1 = a + n;
+      g_rec = rec;
+      // ~init goes into the data's first 4 bytes; a block shorter than 4 bytes
+      // gets it at the end instead (finish_block)
+      g_ninit = (raw || n < 4) ? 0u : ~(kLog ? 0u : aux);
+      g_st = aux;
+      g_end = g_u1 & ~15ull;
+      uint64_t S = (g_end - (a & ~15ull) + kStep - 1) / kStep;
+      if (S == 0) S = 1;
+      uint32_t m = ok ? (uint32_t)S : 0u;
+#pragma unroll
+      for (int k = 32; k >= 1; k >>= 1) m = max(m, (uint32_t)__shfl_xor(m, k));
+      r_S = m;
+      if (r_S != 0) break;  // an empty round (past the batch's end): next one
+    }
+    g_lp = g_end - (uint64_t)r_S * kStep;
+    r_step = 0;
+  };
+
+  // Values loaded in one take and used only later are consumed at fixed points
+  // (an empty asm reading them): the compiler then resolves their loads with
+  // exact counts instead of waiting for all loads where its paths merge.
+  auto take = [&](bool first) {
+    if (first) {
+      asm volatile("" ::"v"(req), "v"(t_olo), "v"(t_ohi), "v"(t_len), "v"(t_aux));
+      if (stage == 3) pipe(3);
+      if ((fl & fRefill) && stage == 0 && !(fl & fReady)) {
+        fl &= ~fRefill;
+        uint32_t nc = kNone;
+        if (!(fl & fDry)) {
+          const uint64_t c = collect();
+          if (c == kNoChunk) fl |= fDry;
+          else {
+            nc = (uint32_t)c;
+            fl |= fClaim;
+          }
+        }
+        start_refill(nc);
+      }
+    } else {
+      asm volatile("" ::"v"(t_rec));
+      if constexpr (kLog) asm volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(h4), "v"(h5));
+      if (stage == 2) pipe(2);
+      else if (stage == 4) pipe(4);
+      if (fl & fClaim) {
+        claim(victim);
+        fl &= ~fClaim;
+      }
+    }
+    if ((fl & fRoundDone) && !(fl & fDone)) {
+      next_round();
+      if (r_S != 0) fl &= ~fRoundDone;  // else: stalled (retry next take) or done
+    }
+  };
+
+  auto issue = [&](FlatSet& X) -> bool {
+    const bool live = !(fl & fDone);
+    const bool run = r_S != 0;             // a round is active (else: stalled, empty step)
+    const bool v = g_valid && run;
+    const bool last = run && r_step + 1 == r_S;  // wave-uniform
+    load_step<G, VAR, kTail2>(X, g_lp, g_u0, g_u1, g_end, v, v && last, zl, q);
+    X.pa = g_lp;
+    X.u0 = g_u0;
+    X.u1 = g_u1;
+    X.rec = g_rec;
+    // An invalid group's step (or a stalled one) reads zeros; with no init
+    // xor-ed in it leaves the group's zero registers zero for its next block.
+    X.ninit = v ? g_ninit : 0u;
+    X.st = g_st;
+    X.valid = v;
+    X.last = last;
+    if (run) {
+      g_lp += kStep;
+      if (++r_step == r_S) fl |= fRoundDone;
+    }
+    return live;
+  };
+
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  bool wb_on = false;
+  uint64_t wb_a = 0;
+  uint32_t wb_v = 0;
+  auto fold = [&](FlatSet& Y) {
+    fold_step<G, VAR, kTail2>(lds, Y, q, c0, c1, c2, c3, lo0, lo1, lo2, lo3);
+    if (Y.last) {  // wave-uniform: every group ends its block on this step
+      const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
+      c0 = c1 = c2 = c3 = 0;
+      finish_block<MODE>(lds, kByteTab, p, raw, v, Y, wb_a, wb_v);
+      wb_on = q == 0 && Y.valid;  // written after the next step's loads are issued
+    }
+  };
+  auto writeback = [&]() {
+    if (wb_on) {
+      write_result<MODE>(p, wb_a, wb_v);
+      wb_on = false;
+    }
+  };
+
+  // ---- prologue: the first chunk is implicit, the second is claimed; both are
+  // loaded synchronously (stages back to back) ----------------------------------
+  {
+    uint64_t k0 = (uint64_t)wave * nwg + blockIdx.x;
+    if (k0 >= p.n_chunks) {
+      claim(victim);
+      k0 = collect();
+    }
+    if (k0 == kNoChunk) fl |= fDry;
+    start_refill(k0 == kNoChunk ? kNone : (uint32_t)k0);
+    while (stage != 0) pipe(stage);
+    next_round();  // switches to k0 and takes its first round
+    uint64_t k1 = kNoChunk;
+    if (!(fl & fDry)) {
+      claim(victim);
+      k1 = collect();
+      if (k1 == kNoChunk) fl |= fDry;
+      else fl |= fClaim;
+    }
+    start_refill(k1 == kNoChunk ? kNone : (uint32_t)k1);
+    while (stage != 0) pipe(stage);
+    fl &= ~fRefill;
+    if (r_S == 0 && !(fl & fDone)) fl |= fRoundDone;  // k0 empty: next take moves on
+  }
+  FlatSet A, B;
+  A.d0 = A.d1 = A.d2 = A.d3 = A.t = A.t2 = make_uint4(0, 0, 0, 0);
+  A.pa = A.u0 = A.u1 = A.rec = 0;
+  A.ninit = A.st = 0;
+  A.valid = A.last = false;
+  for (;;) {
+    take(true);
+    issue(B);
+    writeback();
+    fold(A);
+    take(false);
+    const bool a_live = issue(A);
+    writeback();
+    fold(B);
+    if (!a_live) break;
+  }
+  writeback();
+  __builtin_amdgcn_s_waitcnt(0);  // the last claim has returned (see the flat kernel)
   sched_release(p.sched);
 }
 
@@ -1430,6 +1913,13 @@ struct DevTables {
   // slot; each launch leaves its slot zeroed (sched_release).
   std::mutex sched_mu;
   std::unordered_map<uint64_t, uint32_t*> sched_by_stream;
+  // Rounds kernel: per-stream scratch for the sort (2 x kBins counters + perm).
+  struct SortScratch {
+    uint32_t* hist = nullptr;
+    uint32_t* perm = nullptr;
+    size_t cap = 0;
+  };
+  std::unordered_map<uint64_t, SortScratch> sort_by_stream;
 };
 
 constexpr int kMaxDevices = 64;
@@ -1517,6 +2007,21 @@ int set_lds_attr_flat() {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
 }
 
+template <int G, int MODE, int VAR = 0>
+int set_lds_attr_rounds() {
+  return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_rounds_kernel<G, MODE, VAR>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+}
+
+template <int MODE, int VAR = 0>
+int set_lds_attrs_rounds() {
+  int e = 0;
+  if ((e = set_lds_attr_rounds<2, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_rounds<4, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_rounds<8, MODE, VAR>())) return e;
+  return set_lds_attr_rounds<16, MODE, VAR>();
+}
+
 template <int MODE, int VAR = 0>
 int set_lds_attrs_flat() {
   int e = 0;
@@ -1588,6 +2093,12 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_flat<kLogVerify>())) return;
   if ((t->err = set_lds_attrs_flat<kStore, kVarNoLookup>())) return;
   if ((t->err = set_lds_attrs_flat<kStore, kVarCached>())) return;
+  if ((t->err = set_lds_attrs_rounds<kStore>())) return;
+  if ((t->err = set_lds_attrs_rounds<kTrailer>())) return;
+  if ((t->err = set_lds_attrs_rounds<kVerify>())) return;
+  if ((t->err = set_lds_attrs_rounds<kLogWrite>())) return;
+  if ((t->err = set_lds_attrs_rounds<kLogVerify>())) return;
+  if ((t->err = set_lds_attrs_rounds<kStore, kVarNoLookup>())) return;
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;
@@ -1635,9 +2146,10 @@ uint32_t* sched_slot(DevTables* t, hipStream_t stream) {
 int gindex(int G) { return G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4; }
 
 // Dispatcher policy for batches the streaming kernel does not take.
-// Kernels: units (round-based, segments; the default: measured fastest on
-// config 3, SSTable-like 4 KiB+ blocks and log records) or flat
-// (per-group block streams, 3.5), chosen with nova_diag_set_variable_kernel.
+// Kernels: units (rounds of segments; the default
+// for SSTable batches: fastest on config 3), rounds (sorted lockstep rounds;
+// the default for log records), flat (per-group block streams; on request),
+// chosen with nova_diag_set_variable_kernel.
 // G lanes per block/unit; segment size (units kernel; 0 = one unit per block)
 // from nova_crc32c_set_tuning or per workload:
 //   variable SSTable batches: G = 16, 32 KiB segments (config 3 sweep);
@@ -1648,7 +2160,7 @@ uint64_t flat_waves() {
   const int w = waves_per_wg(kFlatWaves);
   return w > kFlatMaxWaves ? kFlatMaxWaves : w;
 }
-enum VarKernel { kAuto = 0, kUnitsK = 1, kFlatK = 2 };
+enum VarKernel { kAuto = 0, kUnitsK = 1, kFlatK = 2, kRoundsK = 3 };
 std::atomic<int> g_tune_kernel{0};
 struct Plan {
   int kernel;
@@ -1659,7 +2171,8 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode) {
   (void)n_blocks;
   const bool log = mode == kLogWrite || mode == kLogVerify;
   Plan pl{kUnitsK, 16, 32768u};
-  if (log) {
+  if (log) {  // rounds kernel: 44.8 % vs 39.0 % (units) on the 2M-record log image
+    pl.kernel = kRoundsK;
     pl.G = 8;
     pl.seg = 0;
   } else if (uniform) {
@@ -1669,10 +2182,11 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode) {
   const int tk = g_tune_kernel.load();
   const int tg = g_tune_g.load();
   const uint32_t ts = g_tune_seg.load();
-  if (tk == kFlatK && ts == 0) pl.kernel = kFlatK;
+  if (tk != kAuto) pl.kernel = tk;
+  if (ts) pl.kernel = kUnitsK;  // a forced segment size is a units-kernel setting
   if (tg == 1 || tg == 2 || tg == 4 || tg == 8 || tg == 16) pl.G = tg;
   if (ts) pl.seg = ts & ~15u;
-  if (pl.kernel == kFlatK) {
+  if (pl.kernel == kFlatK || pl.kernel == kRoundsK) {
     pl.seg = 0;
     if (pl.G == 1) pl.G = 2;  // at most 32 groups per wave (chunk >= 2 groups <= 64)
   }
@@ -1845,6 +2359,128 @@ uint32_t stream_bpg(int G, uint32_t len) {
   return b < 1 ? 1u : (b > 64 ? 64u : (uint32_t)b);
 }
 
+// Per-stream sort scratch (grown on demand; launches on one stream run in order).
+DevTables::SortScratch* sort_scratch(DevTables* t, hipStream_t stream, size_t n) {
+  uint64_t key = (uint64_t)(uintptr_t)stream;
+  if (stream == hipStreamPerThread)
+    key = (std::hash<std::thread::id>{}(std::this_thread::get_id()) << 1) | 1u;
+  std::lock_guard<std::mutex> lk(t->sched_mu);
+  DevTables::SortScratch& sc = t->sort_by_stream[key];
+  if (!sc.hist) {
+    void* d = nullptr;
+    if (hipMalloc(&d, 2 * kBins * sizeof(uint32_t)) != hipSuccess) return nullptr;
+    sc.hist = static_cast<uint32_t*>(d);
+  }
+  if (sc.cap < n) {
+    if (sc.perm) {
+      (void)hipStreamSynchronize(stream);  // the old array may still be read
+      (void)hipFree(sc.perm);
+      sc.perm = nullptr;
+      sc.cap = 0;
+    }
+    void* d = nullptr;
+    if (hipMalloc(&d, n * sizeof(uint32_t)) != hipSuccess) return nullptr;
+    sc.perm = static_cast<uint32_t*>(d);
+    sc.cap = n;
+  }
+  return &sc;
+}
+
+template <int MODE>
+int launch_sort(CrcParams& p, DevTables* t, hipStream_t stream, uint64_t kStep) {
+  DevTables::SortScratch* sc = sort_scratch(t, stream, p.n_blocks);
+  if (!sc) return NOVA_E_NOMEM;
+  hipError_t e = hipMemsetAsync(sc->hist, 0, kBins * sizeof(uint32_t), stream);
+  if (e != hipSuccess) return (int)e;
+  uint64_t wgs = (p.n_blocks + 255) / 256;
+  const uint64_t cap = (uint64_t)t->cus * 4;
+  if (wgs > cap) wgs = cap;
+  hipLaunchKernelGGL(bin_count_kernel<MODE>, dim3(wgs), dim3(256), 0, stream, p, kStep, sc->hist);
+  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(kBins), 0, stream, sc->hist, sc->hist + kBins);
+  hipLaunchKernelGGL(bin_scatter_kernel<MODE>, dim3(wgs), dim3(256), 0, stream, p, kStep,
+                     sc->hist + kBins, sc->perm);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  p.perm = sc->perm;
+  return 0;
+}
+
+std::atomic<int> g_tune_sort{2};  // rounds kernel: 0 in order, 1 whole-batch sort, 2 per chunk
+
+template <int MODE, int VAR>
+int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
+  switch (G) {
+    case 2: hipLaunchKernelGGL((crc32c_rounds_kernel<2, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 4: hipLaunchKernelGGL((crc32c_rounds_kernel<4, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 8: hipLaunchKernelGGL((crc32c_rounds_kernel<8, MODE, VAR>), grid, block, lds, stream, p); break;
+    default: hipLaunchKernelGGL((crc32c_rounds_kernel<16, MODE, VAR>), grid, block, lds, stream, p); break;
+  }
+  return (int)hipGetLastError();
+}
+
+template <int MODE>
+int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
+  if (G < 2) G = 2;
+  p.tab_main = t->main[gindex(G)];
+  p.tab_tree = t->tree;
+  p.tab_byte = t->byte8;
+  p.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
+  p.omask = p.lmask = p.imask = ~0ull;
+  if (p.offsets) {
+    p.stride = 0;
+  } else {
+    p.offsets = reinterpret_cast<const uint64_t*>(t->zero_word);
+    p.omask = 0;
+  }
+  if (p.lengths) {
+    p.len = 0;
+  } else {
+    p.lengths = t->zero_word;
+    p.lmask = 0;
+  }
+  if (!p.init) {
+    p.init = t->zero_word;
+    p.imask = 0;
+  }
+  p.perm = nullptr;
+  const int sort = g_tune_sort.load();  // 0 none, 1 whole batch (pre-pass), 2 per chunk
+  p.sort_local = sort == 2 ? 1u : 0u;
+  if (sort == 1 && p.n_blocks >= 1024) {
+    const int e = launch_sort<MODE>(p, t, stream, 64ull * G);
+    if (e) return e;
+  }
+  {
+    // chunk = R rounds of 64/G blocks.  Log records: 64 (the header stage
+    // needs 4 steps of pipeline).  SSTable blocks: 4 rounds, since a chunk is
+    // also the unit of the tail balance and big blocks make big chunks.
+    const uint32_t groups = 64u / (uint32_t)G;
+    const bool log = MODE == kLogWrite || MODE == kLogVerify;
+    uint32_t c = log ? 64u : 4u * groups;
+    const int tc = g_tune_chunk.load();
+    if (tc > 0) c = (uint32_t)tc;
+    c = (c / groups) * groups;
+    if (c < groups) c = groups;
+    if (c > 64) c = 64;
+    p.chunk = c;
+  }
+  p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
+  const uint64_t nwaves = flat_waves();
+  uint64_t wgs = (p.n_chunks + nwaves - 1) / nwaves;
+  if (wgs > (uint64_t)t->cus) wgs = t->cus;
+  if (wgs > 256) wgs = 256;
+  if (wgs == 0) return 0;
+  {
+    const int sl = g_tune_static_pct.load();
+    p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;
+  }
+  p.sched = sched_slot(t, stream);
+  if (!p.sched) return NOVA_E_NOMEM;
+  const dim3 block(64 * nwaves);
+  const size_t lds = flat_lds_g(G) + nwaves * 64 * 4;  // + per-wave sort scratch
+  if (MODE == kStore && g_tune_var.load() == kVarNoLookup)
+    return launch_rounds_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
+  return launch_rounds_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
+}
+
 int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   p.init_stride = p.init ? 1u : 0u;
   if (!p.init) p.init = t->zero_word;
@@ -1891,6 +2527,15 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   const Plan pl = plan(p.n_blocks, bytes_per_block, uniform, mode);
   const int G = pl.G;
   p.seg = pl.seg;
+  if (pl.kernel == kRoundsK) {
+    switch (mode) {
+      case kStore: return launch_rounds<kStore>(G, p, t, stream);
+      case kTrailer: return launch_rounds<kTrailer>(G, p, t, stream);
+      case kLogWrite: return launch_rounds<kLogWrite>(G, p, t, stream);
+      case kLogVerify: return launch_rounds<kLogVerify>(G, p, t, stream);
+      default: return launch_rounds<kVerify>(G, p, t, stream);
+    }
+  }
   if (pl.kernel == kFlatK) {
     switch (mode) {
       case kStore: return launch_flat<kStore>(G, p, t, stream);
@@ -2060,7 +2705,7 @@ int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_u
   const Plan pl = plan(n_blocks, bytes_per_block, true, kStore);
   if (lanes_per_unit) *lanes_per_unit = pl.G;
   if (seg_bytes) *seg_bytes = pl.seg;
-  return pl.kernel == kFlatK ? 2 : 0;  // flat kernel : units kernel
+  return pl.kernel == kFlatK ? 2 : pl.kernel == kRoundsK ? 3 : 0;  // flat : rounds : units
 }
 
 int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int variable, char* buf,
@@ -2082,7 +2727,12 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
   } else {
     const Plan pl = plan(n_blocks, len, !variable, kStore);
     const int g = pl.G;
-    if (pl.kernel != kFlatK)
+    if (pl.kernel == kRoundsK)
+      n = snprintf(buf, buflen,
+                   "{\"kernel\": \"crc32c_rounds_kernel<%d, 0>\", \"lanes_per_block\": %d, "
+                   "\"sort\": %d, \"waves_per_wg\": %d}", g < 2 ? 2 : g, g < 2 ? 2 : g,
+                   g_tune_sort.load(), (int)flat_waves());
+    else if (pl.kernel != kFlatK)
       n = snprintf(buf, buflen,
                    "{\"kernel\": \"crc32c_units_kernel<%d, 0>\", \"lanes_per_unit\": %d, "
                    "\"segment_bytes\": %u, \"waves_per_wg\": %d}", g, g, pl.seg,
@@ -2127,6 +2777,8 @@ void nova_diag_set_stream_waves(int waves) { g_tune_waves.store(waves); }
 void nova_diag_set_variable_kernel(int kernel) { g_tune_kernel.store(kernel); }
 
 void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
+
+void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
 
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {

@@ -33,6 +33,7 @@ def _reset_tuning():
     L.nova_diag_set_stream_waves(0)
     L.nova_diag_set_variant(0)
     L.nova_diag_set_variable_kernel(0)
+    L.nova_diag_set_rounds_sort(2)
 
 
 def dev(torch, arr, dtype=None):
@@ -502,19 +503,27 @@ def test_claim_counters_reset_between_launches(torch_gpu, oracle):
         assert np.array_equal(u32(out), want_all[:n]), (it, n)
 
 
-@pytest.mark.parametrize("lanes,chunk,waves", [
-    (0, 0, 0), (2, 0, 0), (4, 0, 0), (8, 0, 0), (16, 0, 0), (16, 9, 0), (16, 64, 0),
-    (8, 0, 3), (4, 40, 5), (16, 0, 1), (16, 0, 12), (8, 0, 10)])
-def test_flat_many_blocks(torch_gpu, oracle, lanes, chunk, waves):
-    """Flat kernel with enough blocks for every wave to switch descriptor
-    banks and claim chunks many times, including the stealing tail: mixed
-    tiny/empty/long blocks at random offsets (descriptors not in address
-    order), random inits, for every lane count, chunk size and wave count."""
+@pytest.mark.parametrize("kernel,lanes,chunk,waves", [
+    (2, 0, 0, 0), (2, 2, 0, 0), (2, 4, 0, 0), (2, 8, 0, 0), (2, 16, 0, 0), (2, 16, 9, 0),
+    (2, 16, 64, 0), (2, 8, 0, 3), (2, 4, 40, 5), (2, 16, 0, 1), (2, 16, 0, 12), (2, 8, 0, 10),
+    (3, 0, 3, 0), (3, 2, 3, 0), (3, 4, 3, 0), (3, 8, 3, 0), (3, 16, 3, 0), (3, 16, 3, 1),
+    (3, 8, 3, 5), (3, 4, 3, 12), (3, 16, 0, 0), (3, 8, 0, 7), (3, 16, 1, 0), (3, 4, 1, 0),
+    (3, 16, 4 * 4 + 3, 0), (3, 16, 64 * 4 + 2, 3), (3, 8, 8 * 4 + 3, 0), (3, 2, 32 * 4 + 3, 0)])
+def test_flat_many_blocks(torch_gpu, oracle, kernel, lanes, chunk, waves):
+    """Flat (2) and rounds (3) kernels with enough blocks for every wave to
+    switch descriptor banks and claim chunks many times, including the
+    stealing tail: mixed tiny/empty/long blocks at random offsets (descriptors
+    not in address order), random inits, for every lane count, chunk size,
+    wave count, sorted and unsorted rounds."""
     torch = torch_gpu
     C.set_tuning(lanes, 0)
     L = C.load()
-    L.nova_diag_set_variable_kernel(2)
-    L.nova_diag_set_chunk_blocks(chunk)
+    L.nova_diag_set_variable_kernel(kernel)
+    if kernel == 3:  # rounds kernel: "chunk" = chunk blocks * 4 + sort mode (3: per chunk)
+        L.nova_diag_set_rounds_sort(2 if (chunk & 3) == 3 else (chunk & 3))
+        L.nova_diag_set_chunk_blocks(chunk >> 2)
+    else:
+        L.nova_diag_set_chunk_blocks(chunk)
     L.nova_diag_set_stream_waves(waves)
     rng = np.random.default_rng(1000 + lanes * 7 + chunk + waves)
     n = 120000
@@ -540,7 +549,7 @@ def test_flat_many_blocks(torch_gpu, oracle, lanes, chunk, waves):
 
 @pytest.mark.parametrize("kernel,lanes,chunk", [
     (0, 0, 0), (1, 4, 0), (1, 16, 0), (2, 0, 0), (2, 2, 0), (2, 4, 0), (2, 8, 0), (2, 16, 0),
-    (2, 8, 16), (2, 4, 17), (2, 16, 64)])
+    (2, 8, 16), (2, 4, 17), (2, 16, 64), (3, 0, 0), (3, 2, 0), (3, 4, 0), (3, 16, 0)])
 def test_log_many_records(torch_gpu, oracle, kernel, lanes, chunk):
     """Log record CRC write + verify over a log image with enough records to
     exercise the header pipeline of the flat kernel's descriptor banks

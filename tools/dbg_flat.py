@@ -20,11 +20,15 @@ def main() -> int:
     lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 16
     chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    kernel = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    sort = int(sys.argv[5]) if len(sys.argv) > 5 else 2
     orc = load_oracle()
     L = C.load()
     assert L.nova_device_init() == 0
     C.set_tuning(lanes, 0)
     L.nova_diag_set_chunk_blocks(chunk)
+    L.nova_diag_set_variable_kernel(kernel)
+    L.nova_diag_set_rounds_sort(sort)
     print(C.describe(1, 0, 0, variable=True), flush=True)
     rng = np.random.default_rng(1000 + lanes * 7 + chunk)
     n = 120000
@@ -44,10 +48,11 @@ def main() -> int:
     want = orc.batch(host, offs, lens, init)
     want0 = orc.batch(host, offs, lens, None)
     for r in range(reps):
-        out = C.batch(buf, do, dl, init=di)
+        out = torch.full((n,), -559038737, dtype=torch.int32, device="cuda")
+        C.batch(buf, do, dl, init=di, out=out)
         got = out.cpu().numpy().view(np.uint32)
         bad = np.nonzero(got != want)[0]
-        print(f"run {r}: {bad.size} bad", flush=True)
+        print(f"run {r}: {bad.size} bad, {int((got[bad] == 0xDEADBEEF).sum())} unwritten", flush=True)
         for i in bad[:10]:
             # does the wrong value equal the CRC of some other descriptor?
             hits = np.nonzero(want == got[i])[0][:3].tolist()

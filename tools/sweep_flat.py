@@ -7,8 +7,9 @@ Workloads (all device-resident, splitmix64 data):
   sst4k  an SSTable-like image: 1M blocks of 4096 + U[0,255] B, 5-B trailer gaps
   log    a log image: 2M records, payload U[1,4096] B, 7-B headers (log write CRC)
 
-Variants: "flat:G:chunk:waves:var" (flat kernel) or "units:G:seg:waves:var"
-(units kernel, segment size forced).  var 1 = no-lookup ablation (timing only).
+Variants: "flat:G:chunk:waves:var" (flat kernel), "units:G:seg:waves:var"
+(units kernel, segment size forced) or "rounds:G:chunk*4+sort:waves:var"
+(sort 0 none, 1 batch pre-pass, 2 or 3 per chunk; chunk 0 = default).  var 1 = no-lookup ablation (timing only).
 Prints one line per (workload, variant); writes gpurun_out/sweep_flat.json.
 """
 from __future__ import annotations
@@ -81,6 +82,11 @@ def set_variant(C, v: str) -> None:
         L.nova_diag_set_variable_kernel(2)
         C.set_tuning(g, 0)
         L.nova_diag_set_chunk_blocks(x)
+    elif kind == "rounds":  # x: chunk blocks * 4 + sort mode (sort 3 = default 2)
+        L.nova_diag_set_variable_kernel(3)
+        L.nova_diag_set_rounds_sort(2 if (x & 3) == 3 else (x & 3))
+        C.set_tuning(g, 0)
+        L.nova_diag_set_chunk_blocks(x >> 2)
     else:
         L.nova_diag_set_variable_kernel(1 if kind == "units" else 0)
         C.set_tuning(g, x)
