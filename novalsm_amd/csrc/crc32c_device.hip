@@ -112,6 +112,7 @@ constexpr int kVarNoLookup = 1;  // ablation: stream step without table lookups
 constexpr int kVarCached = 2;    // default-policy data loads (production uses nt)
 constexpr int kVarStamps = 4;    // record per-wave s_memrealtime stamps (diagnostics)
 constexpr int kVarStaticClaims = 8;  // stream kernel: claims without atomics (diagnostics)
+constexpr int kVarNarrow = 16;  // flat/rounds/units: one word's lookups in flight (fold4, A/B)
 
 // 16-byte load through the global (not flat) address space.  Block bytes are
 // read exactly once, so production loads carry the nt policy: on gfx950 it
@@ -191,6 +192,55 @@ __device__ __forceinline__ void fold4(const uint8_t* lds, uint32_t& c0, uint32_t
   c3 = step<VAR>(lds, c3, d3.w, lo0, lo1, lo2, lo3);
 }
 
+// One swath into the lane's four stream registers with all 16 table lookups
+// issued before any is consumed.  Written as four step() calls, the compiler
+// serialises the four independent chains on the LDS latency (one word's four
+// lookups in flight at a time: seen in the rounds kernel's ISA); the
+// scheduling barrier keeps the reads ahead of the xors.
+template <int VAR = 0>
+__device__ __forceinline__ void swath4(const uint8_t* lds, uint32_t& c0, uint32_t& c1, uint32_t& c2,
+                                       uint32_t& c3, const uint4& d, uint32_t lo0, uint32_t lo1,
+                                       uint32_t lo2, uint32_t lo3) {
+  if constexpr ((VAR & kVarNoLookup) != 0) {
+    c0 = step<VAR>(lds, c0, d.x, lo0, lo1, lo2, lo3);
+    c1 = step<VAR>(lds, c1, d.y, lo0, lo1, lo2, lo3);
+    c2 = step<VAR>(lds, c2, d.z, lo0, lo1, lo2, lo3);
+    c3 = step<VAR>(lds, c3, d.w, lo0, lo1, lo2, lo3);
+    return;
+  }
+#define NOVA_ADDR4(c, p)                                                   \
+  const uint32_t p##0 = __builtin_amdgcn_perm(c, lo0, Sel<0>::v);          \
+  const uint32_t p##1 = __builtin_amdgcn_perm(c, lo1, Sel<1>::v);          \
+  const uint32_t p##2 = __builtin_amdgcn_perm(c, lo2, Sel<2>::v);          \
+  const uint32_t p##3 = __builtin_amdgcn_perm(c, lo3, Sel<3>::v);
+  NOVA_ADDR4(c0, a) NOVA_ADDR4(c1, b) NOVA_ADDR4(c2, e) NOVA_ADDR4(c3, f)
+#undef NOVA_ADDR4
+  const uint32_t ta0 = lds_u32(lds, a0), ta1 = lds_u32(lds, a1), ta2 = lds_u32(lds, a2),
+                 ta3 = lds_u32(lds, a3);
+  const uint32_t tb0 = lds_u32(lds, b0), tb1 = lds_u32(lds, b1), tb2 = lds_u32(lds, b2),
+                 tb3 = lds_u32(lds, b3);
+  const uint32_t te0 = lds_u32(lds, e0), te1 = lds_u32(lds, e1), te2 = lds_u32(lds, e2),
+                 te3 = lds_u32(lds, e3);
+  const uint32_t tf0 = lds_u32(lds, f0), tf1 = lds_u32(lds, f1), tf2 = lds_u32(lds, f2),
+                 tf3 = lds_u32(lds, f3);
+  __builtin_amdgcn_sched_barrier(0);
+  c0 = xor3(xor3(ta0, ta1, ta2), ta3, d.x);
+  c1 = xor3(xor3(tb0, tb1, tb2), tb3, d.y);
+  c2 = xor3(xor3(te0, te1, te2), te3, d.z);
+  c3 = xor3(xor3(tf0, tf1, tf2), tf3, d.w);
+}
+
+template <int VAR = 0>
+__device__ __forceinline__ void fold4w(const uint8_t* lds, uint32_t& c0, uint32_t& c1, uint32_t& c2,
+                                       uint32_t& c3, const uint4& d0, const uint4& d1,
+                                       const uint4& d2, const uint4& d3, uint32_t lo0, uint32_t lo1,
+                                       uint32_t lo2, uint32_t lo3) {
+  swath4<VAR>(lds, c0, c1, c2, c3, d0, lo0, lo1, lo2, lo3);
+  swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);
+  swath4<VAR>(lds, c0, c1, c2, c3, d2, lo0, lo1, lo2, lo3);
+  swath4<VAR>(lds, c0, c1, c2, c3, d3, lo0, lo1, lo2, lo3);
+}
+
 // Keep the bytes of word [wa, wa+4) that lie in [u0,u1); xor in the bytes of
 // ninit that sit at [u0, u0+4).
 __device__ __forceinline__ uint32_t fix_word(uint32_t w, uint64_t wa, uint64_t u0, uint64_t u1,
@@ -219,6 +269,50 @@ __device__ __noinline__ uint4 load_edge(uint64_t pa, uint64_t u0, uint64_t u1, u
     d.z = fix_word(d.z, pa + 8, u0, u1, ninit);
     d.w = fix_word(d.w, pa + 12, u0, u1, ninit);
   }
+  return d;
+}
+
+// Edge masking in 32-bit arithmetic.  For a 16-B piece at address a:
+//   h = u0 - a: bytes [0, h) precede the unit and are dropped, and the bytes
+//     of ~init that sit at [u0, u0+4) are xor-ed in (the piece holds a head
+//     byte iff -4 < h < 16);
+//   t = u1 - a: bytes [t, 16) follow the unit and are dropped (0 < t < 16).
+// rel32 clamps u - a to [-4, hi]; values outside keep their meaning.
+__device__ __forceinline__ int32_t rel32(uint64_t u, uint64_t a, int32_t hi) {
+  const int64_t d = (int64_t)(u - a);
+  return d < -4 ? -4 : (d > hi ? hi : (int32_t)d);
+}
+__device__ __forceinline__ bool is_head(int32_t h) { return (uint32_t)(h + 3) < 19u; }
+__device__ __forceinline__ bool is_tail(int32_t t) { return (uint32_t)(t - 1) < 15u; }
+// the word at offset 4j of a head piece: r = h - 4j
+__device__ __forceinline__ uint32_t head_word(uint32_t w, int32_t r, uint32_t ninit) {
+  const uint32_t keep = r <= 0 ? ~0u : (r >= 4 ? 0u : (~0u << (8 * r)));
+  uint32_t iv = 0;
+  if (r >= 0 && r < 4) iv = ninit << (8 * r);
+  else if (r < 0 && r > -4) iv = ninit >> (-8 * r);
+  return (w & keep) ^ iv;
+}
+__device__ __forceinline__ uint4 head_piece(uint4 d, int32_t h, uint32_t ninit) {
+  d.x = head_word(d.x, h, ninit);
+  d.y = head_word(d.y, h - 4, ninit);
+  d.z = head_word(d.z, h - 8, ninit);
+  d.w = head_word(d.w, h - 12, ninit);
+  return d;
+}
+// keep bytes [0, r) of the word at offset 4j of a tail piece (r = t - 4j)
+__device__ __forceinline__ uint32_t tail_word(uint32_t w, int32_t r) {
+  return r >= 4 ? w : (r <= 0 ? 0u : (w & ((1u << (8 * r)) - 1u)));
+}
+__device__ __forceinline__ uint4 tail_piece(uint4 d, int32_t t) {
+  d.x = tail_word(d.x, t);
+  d.y = tail_word(d.y, t - 4);
+  d.z = tail_word(d.z, t - 8);
+  d.w = tail_word(d.w, t - 12);
+  return d;
+}
+__device__ __forceinline__ uint4 edge_piece(uint4 d, int32_t h, int32_t t, uint32_t ninit) {
+  if (is_head(h)) d = head_piece(d, h, ninit);
+  if (is_tail(t)) d = tail_piece(d, t);
   return d;
 }
 
@@ -820,16 +914,6 @@ constexpr uint64_t kNoChunk = ~0ull;
 constexpr int kFlatMaxWaves = 12;  // 3 waves per SIMD: up to 168 VGPRs, no spills
 constexpr int kFlatThreads = kFlatMaxWaves * 64;
 
-// Keep the bytes of a 16-B piece at pa that lie in [u0,u1), xor ~init in at u0.
-__device__ __forceinline__ uint4 fix_piece(uint4 d, uint64_t pa, uint64_t u0, uint64_t u1,
-                                           uint32_t ninit) {
-  d.x = fix_word(d.x, pa + 0, u0, u1, ninit);
-  d.y = fix_word(d.y, pa + 4, u0, u1, ninit);
-  d.z = fix_word(d.z, pa + 8, u0, u1, ninit);
-  d.w = fix_word(d.w, pa + 12, u0, u1, ninit);
-  return d;
-}
-
 __device__ __forceinline__ uint32_t sel5(uint32_t k, uint32_t a, uint32_t b, uint32_t c,
                                          uint32_t d, uint32_t e) {
   return k == 0 ? a : k == 1 ? b : k == 2 ? c : k == 3 ? d : e;
@@ -839,17 +923,25 @@ __device__ __forceinline__ uint32_t sel5(uint32_t k, uint32_t a, uint32_t b, uin
 // Issue one 4-swath step of a block region for this lane (pieces before the
 // block's first line, or of an invalid group, read the zero line) plus, on the
 // block's last step, its tail line(s).
-template <int G, int VAR, bool kTail2>
+//
+// kLines (rounds kernel): the step grid is aligned to 16G-byte lines, so each
+// swath of a group is one aligned 16G-byte line (an unaligned grid splits
+// every group-swath over two cache lines: measured 61.5% vs 71.5% of HBM peak
+// on 4 KiB blocks).  The region then ends at Le = roundup(E, 16G) >= E; the
+// last step's last swath holds the pieces at or after E, which read the zero
+// line here and leave their lane's registers unchanged in fold_step.
+template <int G, int VAR, bool kTail2, bool kLines = false>
 __device__ __forceinline__ void load_step(FlatSet& X, uint64_t lp, uint64_t u0, uint64_t u1,
                                           uint64_t end, bool v, bool last, uint64_t zl, int q) {
   const uint64_t A0 = u0 & ~15ull;
   const bool nz = v && u1 > u0;
   const uint64_t pa = lp + 16 * q;
   const uint64_t a0 = pa, a1 = pa + 16 * G, a2 = pa + 32 * G, a3 = pa + 48 * G;
+  const bool in3 = !kLines || !last || a3 < end;
   X.d0 = gload16<VAR>((nz && a0 >= A0) ? a0 : zl);
   X.d1 = gload16<VAR>((nz && a1 >= A0) ? a1 : zl);
   X.d2 = gload16<VAR>((nz && a2 >= A0) ? a2 : zl);
-  X.d3 = gload16<VAR>((nz && a3 >= A0) ? a3 : zl);
+  X.d3 = gload16<VAR>((nz && a3 >= A0 && in3) ? a3 : zl);
   if constexpr (kTail2) {
     const uint64_t ta = last ? end : zl;  // holds the stored CRC's first byte
     X.t = gload16<VAR>(ta);
@@ -859,20 +951,38 @@ __device__ __forceinline__ void load_step(FlatSet& X, uint64_t lp, uint64_t u0, 
   }
 }
 
-// Mask the head pieces of a step (bytes before u0, ~init at u0) and run it
-// through the lane's four stream registers.
-template <int G, int VAR, bool kTail2>
+// Mask the head piece(s) of a step (bytes before u0, ~init at u0) and run it
+// through the lane's four stream registers.  A piece needs it only if it holds
+// a byte of [u0, u0+4): pieces wholly before u0 were loaded from the zero line
+// (load_step) and are zero already.  No region piece holds a byte at or after
+// u1 (regions end at E = u1 & ~15; the tail bytes come from the tail line).
+template <int G, int VAR, bool kTail2, bool kLines = false>
 __device__ __forceinline__ void fold_step(const uint8_t* lds, const FlatSet& Y, int q, uint32_t& c0,
                                           uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t lo0,
                                           uint32_t lo1, uint32_t lo2, uint32_t lo3) {
-  const uint64_t pa = Y.pa + 16 * q;
-  const uint64_t lim = Y.u0 + 4;  // pieces starting before this need masking / init
+  const int32_t h = rel32(Y.u0, Y.pa + 16 * q, 48 * G + 16);
   uint4 d0 = Y.d0, d1 = Y.d1, d2 = Y.d2, d3 = Y.d3;
-  if (pa < lim) d0 = fix_piece(d0, pa, Y.u0, Y.u1, Y.ninit);
-  if (pa + 16 * G < lim) d1 = fix_piece(d1, pa + 16 * G, Y.u0, Y.u1, Y.ninit);
-  if (pa + 32 * G < lim) d2 = fix_piece(d2, pa + 32 * G, Y.u0, Y.u1, Y.ninit);
-  if (pa + 48 * G < lim) d3 = fix_piece(d3, pa + 48 * G, Y.u0, Y.u1, Y.ninit);
-  fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+  if (is_head(h)) d0 = head_piece(d0, h, Y.ninit);
+  if (is_head(h - 16 * G)) d1 = head_piece(d1, h - 16 * G, Y.ninit);
+  if (is_head(h - 32 * G)) d2 = head_piece(d2, h - 32 * G, Y.ninit);
+  if (is_head(h - 48 * G)) d3 = head_piece(d3, h - 48 * G, Y.ninit);
+  if (kLines && Y.last) {  // wave-uniform: the region's last line may end past E
+    swath4<VAR>(lds, c0, c1, c2, c3, d0, lo0, lo1, lo2, lo3);
+    swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);
+    swath4<VAR>(lds, c0, c1, c2, c3, d2, lo0, lo1, lo2, lo3);
+    const uint32_t k0 = c0, k1 = c1, k2 = c2, k3 = c3;
+    swath4<VAR>(lds, c0, c1, c2, c3, d3, lo0, lo1, lo2, lo3);
+    if (Y.pa + 16 * q + 48 * G >= (Y.u1 & ~15ull)) {  // piece at or after E: not in the region
+      c0 = k0;
+      c1 = k1;
+      c2 = k2;
+      c3 = k3;
+    }
+  } else if constexpr ((VAR & kVarNarrow) != 0) {
+    fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+  } else {
+    fold4w<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+  }
   // the tail line(s) are used only on a block's last step: consume anyway, so
   // the compiler resolves their loads here with an exact count
   asm volatile("" ::"v"(Y.t.x), "v"(Y.t.y), "v"(Y.t.z), "v"(Y.t.w));
@@ -1547,6 +1657,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   uint32_t g_ninit = 0, g_st = 0;
   bool g_valid = false;
   uint32_t r_idx = R, r_step = 0, r_S = 0;
+  constexpr uint64_t kLine = 16 * G;  // one swath of a lane group
+  uint64_t g_le = 0;                  // the group's region end on the line grid
   // Take the next non-empty round (switching chunks as needed).  Returns with
   // r_S == 0 if the switch must wait for nxt (stall) or the work is done.
   auto next_round = [&]() {
@@ -1587,7 +1699,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       g_ninit = (raw || n < 4) ? 0u : ~(kLog ? 0u : aux);
       g_st = aux;
       g_end = g_u1 & ~15ull;
-      uint64_t S = (g_end - (a & ~15ull) + kStep - 1) / kStep;
+      // steps on the group's 16G-byte line grid: lines from the one holding
+      // the first byte to the one holding byte E-1 (load_step, kLines)
+      g_le = (g_end + (kLine - 1)) & ~(kLine - 1);
+      uint64_t S = (g_le - (a & ~(kLine - 1)) + kStep - 1) / kStep;
       if (S == 0) S = 1;
       uint32_t m = ok ? (uint32_t)S : 0u;
 #pragma unroll
@@ -1595,7 +1710,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       r_S = m;
       if (r_S != 0) break;  // an empty round (past the batch's end): next one
     }
-    g_lp = g_end - (uint64_t)r_S * kStep;
+    g_lp = g_le - (uint64_t)r_S * kStep;
     r_step = 0;
   };
 
@@ -1640,7 +1755,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     const bool run = r_S != 0;             // a round is active (else: stalled, empty step)
     const bool v = g_valid && run;
     const bool last = run && r_step + 1 == r_S;  // wave-uniform
-    load_step<G, VAR, kTail2>(X, g_lp, g_u0, g_u1, g_end, v, v && last, zl, q);
+    load_step<G, VAR, kTail2, true>(X, g_lp, g_u0, g_u1, g_end, v, v && last, zl, q);
     X.pa = g_lp;
     X.u0 = g_u0;
     X.u1 = g_u1;
@@ -1663,8 +1778,17 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   uint64_t wb_a = 0;
   uint32_t wb_v = 0;
   auto fold = [&](FlatSet& Y) {
-    fold_step<G, VAR, kTail2>(lds, Y, q, c0, c1, c2, c3, lo0, lo1, lo2, lo3);
+    fold_step<G, VAR, kTail2, true>(lds, Y, q, c0, c1, c2, c3, lo0, lo1, lo2, lo3);
     if (Y.last) {  // wave-uniform: every group ends its block on this step
+      // On the line grid lane q's pieces sit at position (q - e) mod G of the
+      // 16G-byte swaths that end at E (e = (E mod 16G) / 16); group_fold wants
+      // position p in lane p, which reads lane (p + e) mod G.
+      const uint32_t e = (uint32_t)(Y.u1 >> 4) & (uint32_t)(G - 1);
+      const int src = (grp * G) + (int)(((uint32_t)q + e) & (uint32_t)(G - 1));
+      c0 = __shfl(c0, src);
+      c1 = __shfl(c1, src);
+      c2 = __shfl(c2, src);
+      c3 = __shfl(c3, src);
       const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
       c0 = c1 = c2 = c3 = 0;
       finish_block<MODE>(lds, kByteTab, p, raw, v, Y, wb_a, wb_v);
@@ -2099,6 +2223,7 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_rounds<kLogWrite>())) return;
   if ((t->err = set_lds_attrs_rounds<kLogVerify>())) return;
   if ((t->err = set_lds_attrs_rounds<kStore, kVarNoLookup>())) return;
+  if ((t->err = set_lds_attrs_rounds<kStore, kVarNarrow>())) return;
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;
@@ -2478,6 +2603,8 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   const size_t lds = flat_lds_g(G) + nwaves * 64 * 4;  // + per-wave sort scratch
   if (MODE == kStore && g_tune_var.load() == kVarNoLookup)
     return launch_rounds_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
+  if (MODE == kStore && g_tune_var.load() == kVarNarrow)
+    return launch_rounds_g<kStore, kVarNarrow>(G, dim3(wgs), block, lds, stream, p);
   return launch_rounds_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
 }
 

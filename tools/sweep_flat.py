@@ -49,6 +49,18 @@ def make_workload(wl: str, stream):
         offs = np.zeros(n, np.uint64)
         offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5))
         total = int(offs[-1]) + int(lens[-1]) + 5
+    elif wl == "c2var":  # config 2's aligned layout through the variable-length path
+        n = 1 << 20
+        lens = np.full(n, 4096, np.uint32)
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(4096)
+        total = n * 4096
+    elif wl == "sst4k_a":  # sst4k sizes rounded to 128 B, every block 128-B aligned
+        n = 1 << 20
+        r = splitmix64_words(5, 0, n)
+        lens = (np.uint64(4096) + np.uint64(128) * (r % np.uint64(3))).astype(np.uint32)
+        offs = np.zeros(n, np.uint64)
+        offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(128))
+        total = int(offs[-1]) + int(lens[-1]) + 128
     elif wl == "log":
         offs, lens, types, total = log_layout(4 << 30, 6)
     else:
