@@ -207,8 +207,13 @@ def main() -> int:
         lens = torch.from_numpy(lens_np.view(np.int32)).to(dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
 
+        # config 3 is LevelDB's block_size sweep (mean ~28 KiB): the caller
+        # knows its block_size and passes the scheduling hint (results are
+        # identical without it; include/nova_crc32c.h)
+        hint = C.HINT_LARGE_BLOCKS
+
         def step():
-            C.batch(buf, offs, lens, out=out, stream=stream)
+            C.batch(buf, offs, lens, flags=hint, out=out, stream=stream)
         bytes_step = int(lens_np.astype(np.uint64).sum())
 
     for _ in range(args.warmup):
@@ -261,7 +266,7 @@ def main() -> int:
     if wl["kind"] == "strided":
         dispatch = C.describe(n, L, L, variable=False)
     else:
-        dispatch = C.describe(n, 0, 0, variable=True)
+        dispatch = C.describe(n, 0, 0, variable=True, large=True)
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_config{args.config}.json")
     if os.path.exists(pmc_path):

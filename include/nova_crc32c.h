@@ -45,6 +45,14 @@ extern "C" {
  * complement, i.e. Extend(c, D) == ~(M_|D|(~c) ^ raw(D)).  Used to combine
  * partial CRCs (nova_crc32c_combine).  Ignores init_or_null. */
 #define NOVA_CRC32C_RAW 0x8u
+/* Scheduling hint for variable-length batches (results are identical either
+ * way): most blocks are >= 16 KiB (e.g. a LevelDB block_size of 16-64 KiB).
+ * Long blocks are then cut into 32 KiB segments whose CRCs are combined
+ * (crc32c_units_kernel); without it blocks are checksummed whole in lockstep
+ * rounds of similar-length blocks (crc32c_rounds_kernel), the faster choice
+ * for NovaLSM's ~4 KiB data blocks.  Accepted by nova_crc32c_batch and
+ * nova_sstable_write_trailers. */
+#define NOVA_CRC32C_HINT_LARGE_BLOCKS 0x10u
 #define NOVA_CRC32C_TYPE(t) (((uint32_t)(uint8_t)(t)) << 8)
 
 /* ---- error codes (negative; positive values are hipError_t) ------------ */
@@ -153,7 +161,8 @@ int nova_device_init(void);
 /* Lanes per block ("G") and segment bytes the dispatcher would pick for an
  * aligned fixed-stride batch; returns 1 for the streaming kernel, 0 for the
  * units kernel, 2 for the flat kernel, 3 for the rounds kernel.  nova_crc32c_describe writes a JSON object naming the kernel
- * and its launch parameters (for reports and profiles). */
+ * and its launch parameters (for reports and profiles); variable: 0 fixed-stride,
+ * 1 variable-length, 2 variable-length with NOVA_CRC32C_HINT_LARGE_BLOCKS. */
 int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_unit,
                      uint32_t* seg_bytes);
 int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int variable, char* buf,

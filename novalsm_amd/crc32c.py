@@ -23,6 +23,7 @@ APPEND_TYPE = 0x1
 MASK_OUTPUT = 0x2
 TB_QUIRK = 0x4
 RAW = 0x8
+HINT_LARGE_BLOCKS = 0x10  # scheduling hint: most blocks >= 16 KiB (include/nova_crc32c.h)
 
 
 def TYPE(t: int) -> int:
@@ -189,9 +190,10 @@ def batch_strided(data, stride: int, length: int, n_blocks: int, init=None, flag
     return out
 
 
-def write_trailers(buf, offsets, sizes, type_byte: int = 0, tb_quirk: bool = False, stream=None):
+def write_trailers(buf, offsets, sizes, type_byte: int = 0, tb_quirk: bool = False, stream=None,
+                   hint_large: bool = False):
     _require_gpu()
-    flags = TYPE(type_byte) | (TB_QUIRK if tb_quirk else 0)
+    flags = TYPE(type_byte) | (TB_QUIRK if tb_quirk else 0) | (HINT_LARGE_BLOCKS if hint_large else 0)
     rc = load().nova_sstable_write_trailers(_ptr(buf), _ptr(offsets), _ptr(sizes),
                                             int(offsets.numel()), flags, _stream_ptr(stream))
     _check(rc, "nova_sstable_write_trailers")
@@ -285,10 +287,12 @@ def plan(n_blocks: int, bytes_per_block: int):
     return g.value, s.value
 
 
-def describe(n_blocks: int, length: int, stride: int, variable: bool = False) -> dict:
+def describe(n_blocks: int, length: int, stride: int, variable: bool = False,
+             large: bool = False) -> dict:
     import json
     buf = ctypes.create_string_buffer(512)
-    load().nova_crc32c_describe(n_blocks, length, stride, 1 if variable else 0, buf, 512)
+    v = (2 if large else 1) if variable else 0
+    load().nova_crc32c_describe(n_blocks, length, stride, v, buf, 512)
     return json.loads(buf.value.decode())
 
 

@@ -241,37 +241,6 @@ __device__ __forceinline__ void fold4w(const uint8_t* lds, uint32_t& c0, uint32_
   swath4<VAR>(lds, c0, c1, c2, c3, d3, lo0, lo1, lo2, lo3);
 }
 
-// Keep the bytes of word [wa, wa+4) that lie in [u0,u1); xor in the bytes of
-// ninit that sit at [u0, u0+4).
-__device__ __forceinline__ uint32_t fix_word(uint32_t w, uint64_t wa, uint64_t u0, uint64_t u1,
-                                             uint32_t ninit) {
-  int64_t lo = (int64_t)(u0 - wa);
-  int64_t hi = (int64_t)(u1 - wa);
-  lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
-  hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
-  uint32_t keep = 0;
-  if (hi > lo)
-    keep = (uint32_t)(((1ull << (8 * hi)) - 1) ^ ((1ull << (8 * lo)) - 1));
-  const int64_t d = (int64_t)(wa - u0);
-  uint32_t iv = 0;
-  if (d >= 0 && d < 4) iv = ninit >> (8 * d);
-  else if (d < 0 && d > -4) iv = ninit << (8 * -d);
-  return (w & keep) ^ iv;
-}
-
-template <int VAR = 0>
-__device__ __noinline__ uint4 load_edge(uint64_t pa, uint64_t u0, uint64_t u1, uint32_t ninit) {
-  uint4 d = make_uint4(0, 0, 0, 0);
-  if (pa + 16 > u0) {  // some byte of the piece is at or after u0 (region ends at roundup16(u1))
-    d = gload16<VAR>(pa);
-    d.x = fix_word(d.x, pa + 0, u0, u1, ninit);
-    d.y = fix_word(d.y, pa + 4, u0, u1, ninit);
-    d.z = fix_word(d.z, pa + 8, u0, u1, ninit);
-    d.w = fix_word(d.w, pa + 12, u0, u1, ninit);
-  }
-  return d;
-}
-
 // Edge masking in 32-bit arithmetic.  For a 16-B piece at address a:
 //   h = u0 - a: bytes [0, h) precede the unit and are dropped, and the bytes
 //     of ~init that sit at [u0, u0+4) are xor-ed in (the piece holds a head
@@ -352,75 +321,96 @@ __device__ __forceinline__ uint32_t group_fold(const uint8_t* lds, uint32_t c0, 
 }
 
 // Process unit [u0,u1) with G lanes; returns the pending word V of the
-// virtual message (identical in all G lanes of the group).
+// virtual message that ends at Eu = roundup16(u1) (identical in all G lanes of
+// the group).  Bytes outside [u0,u1) count as zero; t = Eu - u1 trailing pad
+// bytes are undone by the caller (M_t^-1).
+//   * Steps run on the group's 16G-byte line grid, so each swath is one
+//     aligned line (as the rounds kernel: an unaligned grid splits every
+//     group-swath over two cache lines).  The steps cover the lines from the
+//     one holding u0 to the one holding byte Eu-1.
+//   * Pieces before A0 = u0 & ~15 (first step only) read the zero line; the
+//     piece(s) holding [u0, u0+4) drop the bytes before u0 and take ~init; the
+//     piece holding u1 drops the bytes from u1 on; pieces at or after Eu (last
+//     line only) read the zero line and leave their lane's registers unchanged.
+//   * Every step's loads are issued while the previous step folds (two
+//     register sets, no copies: a copy of a load destination would force a
+//     vmcnt(0) drain); edge masking runs on the first two and the last step.
+//   * On the line grid lane q holds position (q - e) mod G of the swaths that
+//     end at Eu (e = (Eu mod 16G) / 16): the registers are rotated before the
+//     group fold.
 template <int G, int VAR = 0>
 __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0, uint64_t u1,
                                                  uint32_t ninit, int q, uint32_t lo0,
-                                                 uint32_t lo1, uint32_t lo2, uint32_t lo3) {
+                                                 uint32_t lo1, uint32_t lo2, uint32_t lo3,
+                                                 uint64_t zl) {
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  uint32_t e = 0;
   if (u1 > u0) {
+    constexpr uint64_t kStep = 64 * G, kLine = 16 * G;
     const uint64_t Eu = (u1 + 15) & ~15ull;
     const uint64_t A0 = u0 & ~15ull;
-    const uint64_t K = (Eu - A0 + 16 * G - 1) / (16 * G);
-    uint64_t pa = Eu - K * 16 * G + 16 * q;
-    const uint64_t lo_edge = u0 + 4;   // pieces starting before this touch the head
-    const uint64_t hi_edge = u1 - 16;  // pieces starting after this touch the tail
-    uint64_t j = 0;
-    // Head swaths (edge handling) until the piece is clear of the head.
-    for (; j < K && (pa < lo_edge || pa > hi_edge); ++j, pa += 16 * G) {
-      const uint4 d = load_edge<VAR>(pa, u0, u1, ninit);
-      c0 = step<VAR>(lds, c0, d.x, lo0, lo1, lo2, lo3);
-      c1 = step<VAR>(lds, c1, d.y, lo0, lo1, lo2, lo3);
-      c2 = step<VAR>(lds, c2, d.z, lo0, lo1, lo2, lo3);
-      c3 = step<VAR>(lds, c3, d.w, lo0, lo1, lo2, lo3);
-    }
-    // Body: no masking; groups of 4 swaths.  The loads of group g+1 are issued
-    // before group g is folded; the last prefetch re-reads the current group
-    // (an L2 hit) so the loop body stays one basic block and the compiler
-    // keeps the prefetch ahead of the fold with exact vmcnt counts.
-    const uint64_t body_end = hi_edge + 16 * G;  // first swath start that is not clean
-    uint64_t ngroups = 0;
-    if (j + 4 <= K && pa + 3 * 16 * G <= hi_edge) {
-      const uint64_t by_k = (K - j) / 4;
-      const uint64_t by_edge = (body_end - pa) / (4 * 16 * G);
-      ngroups = by_k < by_edge ? by_k : by_edge;
-    }
-    if (ngroups) {
-      // Two register sets, a and b, alternate without copies (a copy of a
-      // load destination would force a vmcnt(0) drain).
-      const uint64_t step_g = 4 * 16 * G;
-      uint4 a0 = gload16<VAR>(pa), a1 = gload16<VAR>(pa + 16 * G);
-      uint4 a2 = gload16<VAR>(pa + 32 * G), a3 = gload16<VAR>(pa + 48 * G);
-      for (uint64_t g = 0; g + 2 <= ngroups; g += 2) {
-        const uint64_t pb = pa + step_g;
-        const uint4 b0 = gload16<VAR>(pb), b1 = gload16<VAR>(pb + 16 * G);
-        const uint4 b2 = gload16<VAR>(pb + 32 * G), b3 = gload16<VAR>(pb + 48 * G);
-        fold4<VAR>(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
-        const uint64_t pn = (g + 2 < ngroups) ? pb + step_g : pb;
-        a0 = gload16<VAR>(pn);
-        a1 = gload16<VAR>(pn + 16 * G);
-        a2 = gload16<VAR>(pn + 32 * G);
-        a3 = gload16<VAR>(pn + 48 * G);
-        fold4<VAR>(lds, c0, c1, c2, c3, b0, b1, b2, b3, lo0, lo1, lo2, lo3);
-        pa += 2 * step_g;
+    const uint64_t Le = (Eu + kLine - 1) & ~(kLine - 1);
+    const uint64_t K4 = (Le - (A0 & ~(kLine - 1)) + kStep - 1) / kStep;  // >= 1
+    const uint64_t p0 = Le - K4 * kStep + 16 * q;  // the lane's first piece of step 0
+    e = (uint32_t)(Eu >> 4) & (uint32_t)(G - 1);
+    auto fold_at = [&](uint4 d0, uint4 d1, uint4 d2, uint4 d3, uint64_t s) {
+      const uint64_t a = p0 + s * kStep;
+      const bool last = s + 1 == K4;  // group-uniform
+      if (s <= 1 || last) {           // the only steps holding edge pieces
+        const int32_t h = rel32(u0, a, 48 * G + 16), t = rel32(u1, a, 48 * G + 16);
+        d0 = edge_piece(d0, h, t, ninit);
+        d1 = edge_piece(d1, h - 16 * G, t - 16 * G, ninit);
+        d2 = edge_piece(d2, h - 32 * G, t - 32 * G, ninit);
+        d3 = edge_piece(d3, h - 48 * G, t - 48 * G, ninit);
       }
-      if (ngroups & 1) {
-        fold4<VAR>(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
-        pa += step_g;
+      if (last) {
+        swath4<VAR>(lds, c0, c1, c2, c3, d0, lo0, lo1, lo2, lo3);
+        swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);
+        swath4<VAR>(lds, c0, c1, c2, c3, d2, lo0, lo1, lo2, lo3);
+        const uint32_t k0 = c0, k1 = c1, k2 = c2, k3 = c3;
+        swath4<VAR>(lds, c0, c1, c2, c3, d3, lo0, lo1, lo2, lo3);
+        if (a + 48 * G >= Eu) {  // past the unit's region: no step
+          c0 = k0;
+          c1 = k1;
+          c2 = k2;
+          c3 = k3;
+        }
+      } else if constexpr ((VAR & kVarNarrow) != 0) {
+        fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+      } else {
+        fold4w<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
       }
-      j += 4 * ngroups;
+    };
+    // step 0: pieces before A0 read the zero line; the last line: pieces at or
+    // after Eu read it too (they are not in the unit and may be past the buffer)
+    const uint64_t lim3 = Eu;
+    uint4 a0 = gload16<VAR>(p0 >= A0 ? p0 : zl);
+    uint4 a1 = gload16<VAR>(p0 + 16 * G >= A0 ? p0 + 16 * G : zl);
+    uint4 a2 = gload16<VAR>(p0 + 32 * G >= A0 ? p0 + 32 * G : zl);
+    uint4 a3 = gload16<VAR>((p0 + 48 * G >= A0 && p0 + 48 * G < lim3) ? p0 + 48 * G : zl);
+    uint64_t s = 0;
+    for (; s + 2 <= K4; s += 2) {
+      const uint64_t pb = p0 + (s + 1) * kStep;
+      const uint4 b0 = gload16<VAR>(pb), b1 = gload16<VAR>(pb + 16 * G);
+      const uint4 b2 = gload16<VAR>(pb + 32 * G);
+      const uint4 b3 = gload16<VAR>(pb + 48 * G < lim3 ? pb + 48 * G : zl);
+      fold_at(a0, a1, a2, a3, s);
+      // the last prefetch re-reads step s+1 (an L2 hit): one loop shape, exact
+      // vmcnt counts
+      const uint64_t pn = (s + 2 < K4) ? pb + kStep : pb;
+      a0 = gload16<VAR>(pn);
+      a1 = gload16<VAR>(pn + 16 * G);
+      a2 = gload16<VAR>(pn + 32 * G);
+      a3 = gload16<VAR>(pn + 48 * G < lim3 ? pn + 48 * G : zl);
+      fold_at(b0, b1, b2, b3, s + 1);
     }
-    // Remaining swaths (plain or tail edge).
-    for (; j < K; ++j, pa += 16 * G) {
-      uint4 d;
-      if (pa < lo_edge || pa > hi_edge) d = load_edge<VAR>(pa, u0, u1, ninit);
-      else d = gload16<VAR>(pa);
-      c0 = step<VAR>(lds, c0, d.x, lo0, lo1, lo2, lo3);
-      c1 = step<VAR>(lds, c1, d.y, lo0, lo1, lo2, lo3);
-      c2 = step<VAR>(lds, c2, d.z, lo0, lo1, lo2, lo3);
-      c3 = step<VAR>(lds, c3, d.w, lo0, lo1, lo2, lo3);
-    }
+    if (s < K4) fold_at(a0, a1, a2, a3, s);
   }
+  const int src = (threadIdx.x & 63) - q + (int)(((uint32_t)q + e) & (uint32_t)(G - 1));
+  c0 = __shfl(c0, src);
+  c1 = __shfl(c1, src);
+  c2 = __shfl(c2, src);
+  c3 = __shfl(c3, src);
   return group_fold<G>(lds, c0, c1, c2, c3, q);
 }
 
@@ -468,6 +458,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
                                                wave * kWaveScratch);
   uint32_t* wacc = wpre + 64;
   uint32_t* wsort = wpre + 32;  // chunk lanes in descending unit-size order
+  const uint64_t zl = (uint64_t)p.zline;  // 16 zero bytes
   const uint32_t rep = (uint32_t)(lane & 31) << 2;
   const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
   const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
@@ -585,7 +576,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
         u0 = first ? ba : u1 - p.seg;
         uinit = first ? binit : 0u;
       }
-      const uint32_t v = unit_pending<G, VAR>(lds, u0, u1, uinit, q, lo0, lo1, lo2, lo3);
+      const uint32_t v = unit_pending<G, VAR>(lds, u0, u1, uinit, q, lo0, lo1, lo2, lo3, zl);
       if (active && q == 0) {
         const uint32_t t = (uint32_t)((16 - (u1 & 15)) & 15);
         uint32_t c = t ? gapply(p.tab_ft + t * 1024, v) : tapply(lds, 0, v);  // M4 in LDS
@@ -1002,10 +993,14 @@ __device__ __forceinline__ void finish_block(const uint8_t* lds, uint32_t byte_t
   const uint32_t nb = (uint32_t)(Y.u1 - E);
   uint32_t R = tapply(lds, 0, v);  // register at E
   {
-    const uint32_t w0 = fix_word(Y.t.x, E + 0, Y.u0, Y.u1, Y.ninit);
-    const uint32_t w1 = fix_word(Y.t.y, E + 4, Y.u0, Y.u1, Y.ninit);
-    const uint32_t w2 = fix_word(Y.t.z, E + 8, Y.u0, Y.u1, Y.ninit);
-    const uint32_t w3 = fix_word(Y.t.w, E + 12, Y.u0, Y.u1, Y.ninit);
+    // The tail line's bytes from u1 on are never consumed below (whole words
+    // only below nb, then nb & 3 single bytes), so only the head edge (a block
+    // inside this line) and ~init need masking.
+    const int32_t ht = rel32(Y.u0, E, 16);
+    const uint32_t w0 = head_word(Y.t.x, ht, Y.ninit);
+    const uint32_t w1 = head_word(Y.t.y, ht - 4, Y.ninit);
+    const uint32_t w2 = head_word(Y.t.z, ht - 8, Y.ninit);
+    const uint32_t w3 = head_word(Y.t.w, ht - 12, Y.ninit);
     uint32_t r;
     r = tapply(lds, 0, R ^ w0);
     R = nb >= 4 ? r : R;
@@ -2230,6 +2225,7 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_mode<kLogWrite>())) return;
   if ((t->err = set_lds_attrs_mode<kLogVerify>())) return;
   if ((t->err = set_lds_attrs_mode<kStore, kVarNoLookup>())) return;
+  if ((t->err = set_lds_attrs_mode<kStore, kVarNarrow>())) return;
   if ((t->err = set_lds_attrs_mode<kStore, kVarCached>())) return;
   if ((t->err = set_lds_attrs_stream<0>())) return;
   if ((t->err = set_lds_attrs_stream<kVarNoLookup>())) return;
@@ -2271,15 +2267,11 @@ uint32_t* sched_slot(DevTables* t, hipStream_t stream) {
 int gindex(int G) { return G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4; }
 
 // Dispatcher policy for batches the streaming kernel does not take.
-// Kernels: units (rounds of segments; the default
-// for SSTable batches: fastest on config 3), rounds (sorted lockstep rounds;
-// the default for log records), flat (per-group block streams; on request),
-// chosen with nova_diag_set_variable_kernel.
-// G lanes per block/unit; segment size (units kernel; 0 = one unit per block)
-// from nova_crc32c_set_tuning or per workload:
-//   variable SSTable batches: G = 16, 32 KiB segments (config 3 sweep);
-//   log records (U[1,4096] B): G = 8, whole records;
-//   unaligned fixed-stride blocks: G by block length, whole blocks.
+// Kernels: rounds (sorted lockstep rounds of whole
+// blocks, G = 8: the default), units (rounds of 32 KiB segments, G = 16: for
+// batches of mostly >= 16 KiB blocks), flat (per-group block streams; on
+// request), chosen with nova_diag_set_variable_kernel.  Lanes per block/unit
+// and segment size can be forced with nova_crc32c_set_tuning.
 constexpr int kFlatWaves = 12;  // sweep: 12 > 10 > 8 waves (more loads in flight)
 uint64_t flat_waves() {
   const int w = waves_per_wg(kFlatWaves);
@@ -2292,17 +2284,21 @@ struct Plan {
   int G;
   uint32_t seg;
 };
-Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode) {
+// Measured (tools/sweep_flat.py, profiles/r01_sweep_lines.log):
+//   SSTable-like 4096+U[0,255] B blocks: rounds G=8 73.7 %, units 53-57 %;
+//   config 3 ({4,16,64} KiB + U[1,64]): units G=16/32 KiB segments 84.0 %,
+//     rounds 75-78 %;
+//   log records U[1,4096] B: rounds G=8, chunks of 64, 55.2 %.
+// Blocks are checksummed whole in rounds unless the caller says most are
+// >= 16 KiB (NOVA_CRC32C_HINT_LARGE_BLOCKS) or the fixed length is.
+Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, bool large) {
   (void)n_blocks;
   const bool log = mode == kLogWrite || mode == kLogVerify;
-  Plan pl{kUnitsK, 16, 32768u};
-  if (log) {  // rounds kernel: 44.8 % vs 39.0 % (units) on the 2M-record log image
-    pl.kernel = kRoundsK;
-    pl.G = 8;
-    pl.seg = 0;
-  } else if (uniform) {
-    pl.G = bytes_per_block < 2048 ? 4 : bytes_per_block < 8192 ? 8 : 16;
-    pl.seg = 0;
+  Plan pl{kRoundsK, 8, 0u};
+  if (!log && ((uniform && bytes_per_block >= 16384) || (!uniform && large))) {
+    pl.kernel = kUnitsK;
+    pl.G = 16;
+    pl.seg = 32768u;
   }
   const int tk = g_tune_kernel.load();
   const int tg = g_tune_g.load();
@@ -2422,6 +2418,7 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   p.tab_tree = t->tree;
   p.tab_ft = t->ft;
   p.tab_sh16 = t->sh16;
+  p.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
   {
     const int ch = g_tune_chunk.load();
     p.chunk = (ch > 0 && ch <= 16) ? (uint32_t)ch : 8u;
@@ -2443,6 +2440,7 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   const dim3 block(64 * nwaves);
   const int var = g_tune_var.load();
   if (MODE == kStore && var == kVarNoLookup) return launch_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
+  if (MODE == kStore && var == kVarNarrow) return launch_g<kStore, kVarNarrow>(G, dim3(wgs), block, lds, stream, p);
   if (MODE == kStore && var == kVarCached) return launch_g<kStore, kVarCached>(G, dim3(wgs), block, lds, stream, p);
   return launch_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
 }
@@ -2651,7 +2649,8 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     const int sg = stream_lanes(p);
     if (sg) return launch_stream(sg, p, t, stream);
   }
-  const Plan pl = plan(p.n_blocks, bytes_per_block, uniform, mode);
+  const Plan pl = plan(p.n_blocks, bytes_per_block, uniform, mode,
+                       (p.flags & NOVA_CRC32C_HINT_LARGE_BLOCKS) != 0);
   const int G = pl.G;
   p.seg = pl.seg;
   if (pl.kernel == kRoundsK) {
@@ -2729,7 +2728,8 @@ int nova_sstable_write_trailers(void* buf, const uint64_t* offsets, const uint32
   p.base = (const uint8_t*)buf;
   p.offsets = offsets;
   p.lengths = sizes;
-  p.flags = (flags & (0xff00u | NOVA_TRAILER_TB_QUIRK)) | NOVA_CRC32C_APPEND_TYPE;
+  p.flags = (flags & (0xff00u | NOVA_TRAILER_TB_QUIRK | NOVA_CRC32C_HINT_LARGE_BLOCKS)) |
+            NOVA_CRC32C_APPEND_TYPE;
   p.n_blocks = n_blocks;
   return run(kTrailer, p, false, 0, (hipStream_t)stream);
 }
@@ -2829,7 +2829,7 @@ int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_u
     if (seg_bytes) *seg_bytes = 0;
     return 1;  // streaming kernel
   }
-  const Plan pl = plan(n_blocks, bytes_per_block, true, kStore);
+  const Plan pl = plan(n_blocks, bytes_per_block, true, kStore, false);
   if (lanes_per_unit) *lanes_per_unit = pl.G;
   if (seg_bytes) *seg_bytes = pl.seg;
   return pl.kernel == kFlatK ? 2 : pl.kernel == kRoundsK ? 3 : 0;  // flat : rounds : units
@@ -2852,7 +2852,7 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
                  sg, sg, stream_bpg(sg, (uint32_t)len),
                  g_tune_static_pct.load() < 0 ? 8 : g_tune_static_pct.load());
   } else {
-    const Plan pl = plan(n_blocks, len, !variable, kStore);
+    const Plan pl = plan(n_blocks, len, !variable, kStore, variable == 2);
     const int g = pl.G;
     if (pl.kernel == kRoundsK)
       n = snprintf(buf, buflen,

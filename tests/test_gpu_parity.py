@@ -584,3 +584,47 @@ def test_log_many_records(torch_gpu, oracle, kernel, lanes, chunk):
     ok, bad = C.log_verify_records(buf, doffs)
     assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
     assert int(bad.item()) == len(victims)
+
+
+@pytest.mark.parametrize("mode", ["store", "trailers", "verify"])
+def test_large_blocks_hint_same_results(torch_gpu, oracle, mode):
+    """NOVA_CRC32C_HINT_LARGE_BLOCKS only changes the schedule (units kernel with
+    32 KiB segments instead of whole-block rounds): results are identical and
+    equal to the oracle on an SSTable image of mixed 100 B - 200 KiB blocks."""
+    torch = torch_gpu
+    rng = np.random.default_rng(4242)
+    n = 3000
+    lens = rng.choice([100, 4096, 16384, 65536, 200000], n, p=[.2, .3, .2, .2, .1])
+    lens = (lens + rng.integers(0, 64, n)).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5))
+    host = splitmix64_bytes(99, int(offs[-1]) + int(lens[-1]) + 5 + 64).copy()
+    do, dl = dev(torch, offs, torch.int64), dev(torch, lens, torch.int32)
+    if mode == "store":
+        want = oracle.batch(host, offs, lens, None)
+        for hint in (0, C.HINT_LARGE_BLOCKS):
+            out = torch.full((n,), -559038737, dtype=torch.int32, device="cuda")
+            C.batch(dev(torch, host), do, dl, flags=hint, out=out)
+            assert np.array_equal(u32(out), want), hint
+    elif mode == "trailers":
+        bufs = []
+        for hint in (False, True):
+            buf = dev(torch, host)
+            C.write_trailers(buf, do, dl, 0, True, hint_large=hint)
+            bufs.append(buf.cpu().numpy())
+        assert np.array_equal(bufs[0], bufs[1])
+        for i in np.linspace(0, n - 1, 40).astype(np.int64):
+            o, ln = int(offs[i]), int(lens[i])
+            assert oracle.trailer(host[o:o + ln].tobytes(), 0, True) == bufs[0][o + ln:o + ln + 5].tobytes()
+    else:
+        buf = dev(torch, host)
+        C.write_trailers(buf, do, dl, 0, False)
+        victims = rng.choice(n, 7, replace=False)
+        for v in victims:
+            buf[int(offs[v]) + 1] ^= 0x10
+        for tune in ((0, 0), (16, 32768)):  # default rounds; forced units with segments
+            C.set_tuning(*tune)
+            ok, bad = C.verify_blocks(buf, do, dl)
+            assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
+            assert int(bad.item()) == len(victims)
+        C.set_tuning(0, 0)

@@ -66,6 +66,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--n", type=int, default=1 << 20, help="blocks for trailers/verify")
+    ap.add_argument("--images", default="sst4k,cfg3",
+                    help="SSTable images for trailers/verify: sst4k (4096+U[0,255] B blocks), cfg3")
     ap.add_argument("--parity-sweep", default="",
                     help="comma list of nova_diag_set_parity_variant values (tuning)")
     ap.add_argument("--lanes-sweep", action="store_true",
@@ -105,9 +107,18 @@ def main() -> int:
         rows.append(row)
         print(json.dumps(row), flush=True)
 
-    if "trailers" in ops or "verify" in ops:
+    for image in (args.images.split(",") if ("trailers" in ops or "verify" in ops) else []):
         n = args.n
-        _, lens_np, _ = bench.config3_layout(n, 3)
+        if image == "cfg3":
+            _, lens_np, _ = bench.config3_layout(n, 3)
+            wl = f"config3 SSTable image: {n} blocks {{4,16,64}} KiB+U[1,64], 5-B trailers"
+            large = True  # the caller's block_size is >= 16 KiB: scheduling hint
+        else:
+            from novalsm_amd.synth import splitmix64_words
+            r = splitmix64_words(5, 0, n)
+            lens_np = (np.uint64(4096) + (r % np.uint64(256))).astype(np.uint32)
+            wl = f"SSTable image: {n} blocks of 4096+U[0,255] B, 5-B trailers"
+            large = False
         offs_np = np.zeros(n, np.uint64)
         offs_np[1:] = np.cumsum(lens_np[:-1].astype(np.uint64) + np.uint64(5))
         total = int(offs_np[-1]) + int(lens_np[-1]) + 5
@@ -116,19 +127,18 @@ def main() -> int:
         offs = torch.from_numpy(offs_np.view(np.int64)).cuda()
         lens = torch.from_numpy(lens_np.view(np.int32)).cuda()
         sum_len = int(lens_np.astype(np.uint64).sum())
-        wl = f"config3 SSTable image: {n} blocks {{4,16,64}} KiB+U[1,64], 5-B trailers"
         sample = np.linspace(0, n - 1, 129).astype(np.int64)
         if "trailers" in ops:
-            sec = timed(torch, lambda: C.write_trailers(buf, offs, lens, 0, True, stream=stream),
-                        args.steps, args.warmup, stream)
+            def tw():
+                C.write_trailers(buf, offs, lens, 0, True, stream=stream, hint_large=large)
+            sec = timed(torch, tw, args.steps, args.warmup, stream)
             ok = True
             for i in sample:
                 o, ln = int(offs_np[i]), int(lens_np[i])
                 blk = buf[o:o + ln + 5].cpu().numpy().tobytes()
                 ok &= orc.trailer(blk[:ln], 0, True) == blk[ln:]
-            emit("trailers", wl, sum_len + 5 * n, sec, ok)
-            sweep("trailers", lambda: C.write_trailers(buf, offs, lens, 0, True, stream=stream),
-                  sum_len + 5 * n)
+            emit("trailers", wl, sum_len + 5 * n, sec, ok, {"image": image})
+            sweep("trailers", tw, sum_len + 5 * n)
         if "verify" in ops:
             C.write_trailers(buf, offs, lens, 0, False, stream=stream)  # StoC order: verifiable
             okb = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -139,7 +149,7 @@ def main() -> int:
                 C.verify_blocks(buf, offs, lens, stream=stream, ok=okb, bad=bad)
             sec = timed(torch, vf, args.steps, args.warmup, stream)
             ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
-            emit("verify", wl, sum_len + 6 * n, sec, ok)
+            emit("verify", wl, sum_len + 6 * n, sec, ok, {"image": image})
             sweep("verify", vf, sum_len + 6 * n)
         del buf
         torch.cuda.empty_cache()
