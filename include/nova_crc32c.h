@@ -200,6 +200,9 @@ void nova_diag_set_variable_kernel(int kernel);
 /* Rounds kernel: take the batch in order (0), sort it by block step count
  * first (1, a pre-pass), or sort each claimed chunk of 64 blocks (2, default). */
 void nova_diag_set_rounds_sort(int on);
+/* Trailer writer on the rounds kernel: 1 = one pass (trailer bytes stored by
+ * the CRC kernel), 0 = two passes (default). */
+void nova_diag_set_trailer_single_pass(int on);
 /* XOR parity kernel variant: chunks per thread (bits 0-3), fragments loaded
  * together (bits 4-7), workgroups per CU (bits 8-15); 0 fields = default. */
 void nova_diag_set_parity_variant(int variant);

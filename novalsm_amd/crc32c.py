@@ -85,6 +85,7 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
         "nova_diag_set_variable_kernel": (None, [i32]),
         "nova_diag_set_parity_variant": (None, [i32]),
         "nova_diag_set_rounds_sort": (None, [i32]),
+        "nova_diag_set_trailer_single_pass": (None, [i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

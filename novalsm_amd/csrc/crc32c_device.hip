@@ -113,6 +113,7 @@ constexpr int kVarCached = 2;    // default-policy data loads (production uses n
 constexpr int kVarStamps = 4;    // record per-wave s_memrealtime stamps (diagnostics)
 constexpr int kVarStaticClaims = 8;  // stream kernel: claims without atomics (diagnostics)
 constexpr int kVarNarrow = 16;  // flat/rounds/units: one word's lookups in flight (fold4, A/B)
+constexpr int kVarWide = 32;    // stream kernel: a swath's 16 lookups in flight (fold4w, A/B)
 
 // 16-byte load through the global (not flat) address space.  Block bytes are
 // read exactly once, so production loads carry the nt policy: on gfx950 it
@@ -239,6 +240,19 @@ __device__ __forceinline__ void fold4w(const uint8_t* lds, uint32_t& c0, uint32_
   swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);
   swath4<VAR>(lds, c0, c1, c2, c3, d2, lo0, lo1, lo2, lo3);
   swath4<VAR>(lds, c0, c1, c2, c3, d3, lo0, lo1, lo2, lo3);
+}
+
+// The stream kernel's fold: fold4 (its compiled form keeps two chains' lookups
+// in flight) or, with kVarWide, fold4w.
+template <int VAR = 0>
+__device__ __forceinline__ void fold4s(const uint8_t* lds, uint32_t& c0, uint32_t& c1, uint32_t& c2,
+                                       uint32_t& c3, const uint4& d0, const uint4& d1,
+                                       const uint4& d2, const uint4& d3, uint32_t lo0, uint32_t lo1,
+                                       uint32_t lo2, uint32_t lo3) {
+  if constexpr ((VAR & kVarWide) != 0)
+    fold4w<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+  else
+    fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
 }
 
 // Edge masking in 32-bit arithmetic.  For a 16-B piece at address a:
@@ -837,7 +851,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
       const bool b_live = live;
       advance();
       if (fk == 0 && q == 0 && !raw) a0.x ^= ~init_cur;  // Extend init -> word 0
-      fold4<VAR>(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
+      fold4s<VAR>(lds, c0, c1, c2, c3, a0, a1, a2, a3, lo0, lo1, lo2, lo3);
       finish_step();
       if (!fold_live) break;
       if (!b_live && fk == 0 && fj == 0) break;
@@ -849,7 +863,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
       const bool a_live = live;
       advance();
       if (fk == 0 && q == 0 && !raw) b0.x ^= ~init_cur;
-      fold4<VAR>(lds, c0, c1, c2, c3, b0, b1, b2, b3, lo0, lo1, lo2, lo3);
+      fold4s<VAR>(lds, c0, c1, c2, c3, b0, b1, b2, b3, lo0, lo1, lo2, lo3);
       finish_step();
       if (!fold_live) break;
       if (!a_live && fk == 0 && fj == 0) break;
@@ -1947,6 +1961,28 @@ __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, co
   }
 }
 
+// Trailer writer, second pass: crc[i] = Mask(Extend(Value(block i), type))
+// from the first pass (the rounds kernel in store mode); write the 5-byte
+// trailer [type][LE32] at base + offsets[i] + sizes[i], with '!' over its last
+// byte for TableBuilder's ordering (table/table_builder.cc:202-206,
+// ltc/stoc_file_client_impl.cpp:713-719).  Inside the streaming kernel the
+// five byte stores per block cost ~12 points of HBM throughput.
+__global__ void __launch_bounds__(256) trailer_scatter_kernel(uint8_t* base, const uint64_t* offsets,
+                                                              const uint32_t* sizes,
+                                                              const uint32_t* crc, uint64_t n,
+                                                              uint32_t flags) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
+    uint8_t* d = base + offsets[i] + sizes[i];
+    const uint32_t m = crc[i];
+    d[0] = (uint8_t)(flags >> 8);
+    d[1] = (uint8_t)m;
+    d[2] = (uint8_t)(m >> 8);
+    d[3] = (uint8_t)(m >> 16);
+    d[4] = (flags & NOVA_TRAILER_TB_QUIRK) ? (uint8_t)'!' : (uint8_t)(m >> 24);
+  }
+}
+
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
 __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                        uint64_t first_word) {
@@ -2037,6 +2073,8 @@ struct DevTables {
     uint32_t* hist = nullptr;
     uint32_t* perm = nullptr;
     size_t cap = 0;
+    uint32_t* crc = nullptr;  // trailer writer: per-block masked CRCs between its passes
+    size_t crc_cap = 0;
   };
   std::unordered_map<uint64_t, SortScratch> sort_by_stream;
 };
@@ -2230,6 +2268,7 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_stream<0>())) return;
   if ((t->err = set_lds_attrs_stream<kVarNoLookup>())) return;
   if ((t->err = set_lds_attrs_stream<kVarCached>())) return;
+  if ((t->err = set_lds_attrs_stream<kVarWide>())) return;
   if ((t->err = set_lds_attrs_stream<kVarStamps>())) return;
   if ((t->err = set_lds_attrs_stream<kVarStamps | kVarStaticClaims>())) return;
 }
@@ -2509,6 +2548,28 @@ DevTables::SortScratch* sort_scratch(DevTables* t, hipStream_t stream, size_t n)
   return &sc;
 }
 
+// Per-stream u32 array for the trailer writer's two passes (grown on demand).
+uint32_t* crc_scratch(DevTables* t, hipStream_t stream, size_t n) {
+  uint64_t key = (uint64_t)(uintptr_t)stream;
+  if (stream == hipStreamPerThread)
+    key = (std::hash<std::thread::id>{}(std::this_thread::get_id()) << 1) | 1u;
+  std::lock_guard<std::mutex> lk(t->sched_mu);
+  DevTables::SortScratch& sc = t->sort_by_stream[key];
+  if (sc.crc_cap < n) {
+    if (sc.crc) {
+      (void)hipStreamSynchronize(stream);  // the old array may still be in use
+      (void)hipFree(sc.crc);
+      sc.crc = nullptr;
+      sc.crc_cap = 0;
+    }
+    void* d = nullptr;
+    if (hipMalloc(&d, n * sizeof(uint32_t)) != hipSuccess) return nullptr;
+    sc.crc = static_cast<uint32_t*>(d);
+    sc.crc_cap = n;
+  }
+  return sc.crc;
+}
+
 template <int MODE>
 int launch_sort(CrcParams& p, DevTables* t, hipStream_t stream, uint64_t kStep) {
   DevTables::SortScratch* sc = sort_scratch(t, stream, p.n_blocks);
@@ -2528,6 +2589,7 @@ int launch_sort(CrcParams& p, DevTables* t, hipStream_t stream, uint64_t kStep) 
 }
 
 std::atomic<int> g_tune_sort{2};  // rounds kernel: 0 in order, 1 whole-batch sort, 2 per chunk
+std::atomic<int> g_tune_trailer_1pass{0};  // trailer writer: 1 = single pass in the rounds kernel
 
 template <int MODE, int VAR>
 int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
@@ -2629,6 +2691,7 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   const size_t lds = kMainBytes + levels * kTreeBytes;
   if (g_tune_var.load() == kVarNoLookup) return launch_stream_g<kVarNoLookup>(G, dim3(wgs), lds, stream, p);
   if (g_tune_var.load() == kVarCached) return launch_stream_g<kVarCached>(G, dim3(wgs), lds, stream, p);
+  if (g_tune_var.load() == kVarWide) return launch_stream_g<kVarWide>(G, dim3(wgs), lds, stream, p);
   if (g_tune_var.load() == kVarStamps) {
     p.stamps = g_diag_stamps.load();
     return launch_stream_g<kVarStamps>(G, dim3(wgs), lds, stream, p);
@@ -2653,6 +2716,23 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
                        (p.flags & NOVA_CRC32C_HINT_LARGE_BLOCKS) != 0);
   const int G = pl.G;
   p.seg = pl.seg;
+  if (pl.kernel == kRoundsK && mode == kTrailer && !g_tune_trailer_1pass.load()) {
+    // Two passes: CRCs (type byte appended, masked) into a per-stream array,
+    // then the trailer bytes (trailer_scatter_kernel).
+    uint32_t* tmp = crc_scratch(t, stream, p.n_blocks);
+    if (!tmp) return NOVA_E_NOMEM;
+    CrcParams q = p;
+    q.out = tmp;
+    q.flags = (p.flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT;
+    const int e = launch_rounds<kStore>(G, q, t, stream);
+    if (e) return e;
+    uint64_t wgs = (p.n_blocks + 255) / 256;
+    const uint64_t cap = (uint64_t)t->cus * 8;
+    if (wgs > cap) wgs = cap;
+    hipLaunchKernelGGL(trailer_scatter_kernel, dim3(wgs), dim3(256), 0, stream,
+                       const_cast<uint8_t*>(p.base), p.offsets, p.lengths, tmp, p.n_blocks, p.flags);
+    return (int)hipGetLastError();
+  }
   if (pl.kernel == kRoundsK) {
     switch (mode) {
       case kStore: return launch_rounds<kStore>(G, p, t, stream);
@@ -2906,6 +2986,8 @@ void nova_diag_set_variable_kernel(int kernel) { g_tune_kernel.store(kernel); }
 void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
 
 void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
+
+void nova_diag_set_trailer_single_pass(int on) { g_tune_trailer_1pass.store(on); }
 
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {

@@ -34,6 +34,7 @@ def _reset_tuning():
     L.nova_diag_set_variant(0)
     L.nova_diag_set_variable_kernel(0)
     L.nova_diag_set_rounds_sort(2)
+    L.nova_diag_set_trailer_single_pass(0)
 
 
 def dev(torch, arr, dtype=None):
@@ -608,11 +609,13 @@ def test_large_blocks_hint_same_results(torch_gpu, oracle, mode):
             assert np.array_equal(u32(out), want), hint
     elif mode == "trailers":
         bufs = []
-        for hint in (False, True):
+        for hint, one_pass in ((False, 0), (True, 0), (False, 1)):
+            C.load().nova_diag_set_trailer_single_pass(one_pass)
             buf = dev(torch, host)
             C.write_trailers(buf, do, dl, 0, True, hint_large=hint)
             bufs.append(buf.cpu().numpy())
-        assert np.array_equal(bufs[0], bufs[1])
+        C.load().nova_diag_set_trailer_single_pass(0)
+        assert np.array_equal(bufs[0], bufs[1]) and np.array_equal(bufs[0], bufs[2])
         for i in np.linspace(0, n - 1, 40).astype(np.int64):
             o, ln = int(offs[i]), int(lens[i])
             assert oracle.trailer(host[o:o + ln].tobytes(), 0, True) == bufs[0][o + ln:o + ln + 5].tobytes()

@@ -138,6 +138,12 @@ def main() -> int:
                 blk = buf[o:o + ln + 5].cpu().numpy().tobytes()
                 ok &= orc.trailer(blk[:ln], 0, True) == blk[ln:]
             emit("trailers", wl, sum_len + 5 * n, sec, ok, {"image": image})
+            C.load().nova_diag_set_trailer_single_pass(1)  # A/B: trailer bytes stored by the CRC kernel
+            sec1 = timed(torch, tw, args.steps, args.warmup, stream)
+            C.load().nova_diag_set_trailer_single_pass(0)
+            gbs1 = (sum_len + 5 * n) / sec1 / 1e9
+            print(json.dumps({"sweep": "trailers_single_pass", "image": image, "GBps": round(gbs1, 1),
+                              "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
             sweep("trailers", tw, sum_len + 5 * n)
         if "verify" in ops:
             C.write_trailers(buf, offs, lens, 0, False, stream=stream)  # StoC order: verifiable
