@@ -1585,7 +1585,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     }
     uint32_t rank = 0;
     for (int j = 0; j < 64; j++) {
-      const uint32_t sj = __shfl(S, j);
+      // lane j's key as a wave-uniform scalar (v_readlane: no LDS round trip)
+      const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)S, j);
       rank += (sj > S || (sj == S && j < lane)) ? 1u : 0u;
     }
     sortbuf[rank] = (uint32_t)lane;
