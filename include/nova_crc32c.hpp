@@ -55,11 +55,15 @@ inline int BatchStrided(const void* base, uint64_t stride, uint32_t len, size_t 
 }
 
 // SSTable trailer writer / read-verify.
+// large_blocks: the table's block_size is >= 16 KiB (scheduling hint only,
+// NOVA_CRC32C_HINT_LARGE_BLOCKS; the trailers are identical either way).
 inline int WriteTrailers(void* buf, const uint64_t* offsets, const uint32_t* sizes, size_t n,
-                         uint8_t type, bool table_builder_quirk, void* stream = nullptr) {
+                         uint8_t type, bool table_builder_quirk, void* stream = nullptr,
+                         bool large_blocks = false) {
   return nova_sstable_write_trailers(buf, offsets, sizes, n,
                                      NOVA_CRC32C_TYPE(type) |
-                                         (table_builder_quirk ? NOVA_TRAILER_TB_QUIRK : 0u),
+                                         (table_builder_quirk ? NOVA_TRAILER_TB_QUIRK : 0u) |
+                                         (large_blocks ? NOVA_CRC32C_HINT_LARGE_BLOCKS : 0u),
                                      stream);
 }
 inline int VerifyBlocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes, size_t n,
