@@ -352,13 +352,16 @@ __device__ __forceinline__ uint32_t group_fold(const uint8_t* lds, uint32_t c0, 
 //   * On the line grid lane q holds position (q - e) mod G of the swaths that
 //     end at Eu (e = (Eu mod 16G) / 16): the registers are rotated before the
 //     group fold.
-template <int G, int VAR = 0>
+//   * pre() runs right after the first step's loads are issued (the caller's
+//     deferred work for the previous unit overlaps their latency).
+template <int G, int VAR = 0, typename Pre>
 __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0, uint64_t u1,
                                                  uint32_t ninit, int q, uint32_t lo0,
                                                  uint32_t lo1, uint32_t lo2, uint32_t lo3,
-                                                 uint64_t zl) {
+                                                 uint64_t zl, Pre&& pre) {
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
   uint32_t e = 0;
+  if (!(u1 > u0)) pre();
   if (u1 > u0) {
     constexpr uint64_t kStep = 64 * G, kLine = 16 * G;
     const uint64_t Eu = (u1 + 15) & ~15ull;
@@ -402,6 +405,7 @@ __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0
     uint4 a1 = gload16<VAR>(p0 + 16 * G >= A0 ? p0 + 16 * G : zl);
     uint4 a2 = gload16<VAR>(p0 + 32 * G >= A0 ? p0 + 32 * G : zl);
     uint4 a3 = gload16<VAR>((p0 + 48 * G >= A0 && p0 + 48 * G < lim3) ? p0 + 48 * G : zl);
+    pre();
     uint64_t s = 0;
     for (; s + 2 <= K4; s += 2) {
       const uint64_t pb = p0 + (s + 1) * kStep;
@@ -563,7 +567,27 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // -- rounds: each lane group takes one unit
+    // -- rounds: each lane group takes one unit.  A unit's contribution
+    // M_{seg*j}(M_t^-1 M4 (V)) needs table lookups in global memory; they are
+    // deferred to the next unit's first loads (finalize), so the two latencies
+    // overlap instead of adding up.
+    bool d_on = false;
+    uint32_t d_v = 0, d_t = 0;
+    uint64_t d_m = 0;
+    int d_i = 0;
+    auto finalize = [&]() {
+      if (d_on) {
+        uint32_t c = d_t ? gapply(p.tab_ft + d_t * 1024, d_v) : tapply(lds, 0, d_v);  // M4 in LDS
+        uint64_t m = d_m;  // shift in 16-byte units
+        while (m) {
+          const int bit = __builtin_ctzll(m);
+          c = gapply(p.tab_sh16 + bit * 1024, c);
+          m &= m - 1;
+        }
+        atomicXor(&wacc[d_i], c);
+        d_on = false;
+      }
+    };
     for (uint32_t r0 = 0; r0 < total; r0 += kGroups) {
       const uint32_t u = r0 + grp;
       const bool active = u < total;
@@ -590,19 +614,15 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
         u0 = first ? ba : u1 - p.seg;
         uinit = first ? binit : 0u;
       }
-      const uint32_t v = unit_pending<G, VAR>(lds, u0, u1, uinit, q, lo0, lo1, lo2, lo3, zl);
-      if (active && q == 0) {
-        const uint32_t t = (uint32_t)((16 - (u1 & 15)) & 15);
-        uint32_t c = t ? gapply(p.tab_ft + t * 1024, v) : tapply(lds, 0, v);  // M4 in LDS
-        uint64_t m = (uint64_t)(p.seg >> 4) * j;  // shift in 16-byte units
-        while (m) {
-          const int bit = __builtin_ctzll(m);
-          c = gapply(p.tab_sh16 + bit * 1024, c);
-          m &= m - 1;
-        }
-        atomicXor(&wacc[i], c);
-      }
+      const uint32_t v = unit_pending<G, VAR>(lds, u0, u1, uinit, q, lo0, lo1, lo2, lo3, zl, finalize);
+      // this unit's contribution is folded in during the next unit's first loads
+      d_on = active && q == 0;
+      d_v = v;
+      d_t = (uint32_t)((16 - (u1 & 15)) & 15);
+      d_m = (uint64_t)(p.seg >> 4) * j;
+      d_i = i;
     }
+    finalize();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
