@@ -352,16 +352,44 @@ __device__ __forceinline__ uint32_t group_fold(const uint8_t* lds, uint32_t c0, 
 //   * On the line grid lane q holds position (q - e) mod G of the swaths that
 //     end at Eu (e = (Eu mod 16G) / 16): the registers are rotated before the
 //     group fold.
-//   * pre() runs right after the first step's loads are issued (the caller's
-//     deferred work for the previous unit overlaps their latency).
+//   * Units stream back to back: a0..a3 arrive holding this unit's first step
+//     (in flight) and leave holding the next unit's [nu0, nu1) first step, issued
+//     with this unit's last prefetch.  pre() runs once this unit's loads are in
+//     flight (the caller's deferred work for the previous unit overlaps them).
+template <int G>
+__device__ __forceinline__ void unit_first_addrs(uint64_t u0, uint64_t u1, int q, uint64_t zl,
+                                                 uint64_t& x0, uint64_t& x1, uint64_t& x2,
+                                                 uint64_t& x3) {
+  constexpr uint64_t kStep = 64 * G, kLine = 16 * G;
+  const bool ne = u1 > u0;
+  const uint64_t Eu = (u1 + 15) & ~15ull;
+  const uint64_t A0 = u0 & ~15ull;
+  const uint64_t Le = (Eu + kLine - 1) & ~(kLine - 1);
+  const uint64_t K4 = ne ? (Le - (A0 & ~(kLine - 1)) + kStep - 1) / kStep : 1;
+  const uint64_t p0 = Le - K4 * kStep + 16 * q;
+  x0 = (ne && p0 >= A0) ? p0 : zl;
+  x1 = (ne && p0 + 16 * G >= A0) ? p0 + 16 * G : zl;
+  x2 = (ne && p0 + 32 * G >= A0) ? p0 + 32 * G : zl;
+  x3 = (ne && p0 + 48 * G >= A0 && p0 + 48 * G < Eu) ? p0 + 48 * G : zl;
+}
+
 template <int G, int VAR = 0, typename Pre>
 __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0, uint64_t u1,
                                                  uint32_t ninit, int q, uint32_t lo0,
                                                  uint32_t lo1, uint32_t lo2, uint32_t lo3,
-                                                 uint64_t zl, Pre&& pre) {
+                                                 uint64_t zl, Pre&& pre, uint4& a0, uint4& a1,
+                                                 uint4& a2, uint4& a3, uint64_t nu0, uint64_t nu1) {
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
   uint32_t e = 0;
-  if (!(u1 > u0)) pre();
+  uint64_t x0, x1, x2, x3;  // the next unit's first step
+  unit_first_addrs<G>(nu0, nu1, q, zl, x0, x1, x2, x3);
+  if (!(u1 > u0)) {
+    pre();
+    a0 = gload16<VAR>(x0);
+    a1 = gload16<VAR>(x1);
+    a2 = gload16<VAR>(x2);
+    a3 = gload16<VAR>(x3);
+  }
   if (u1 > u0) {
     constexpr uint64_t kStep = 64 * G, kLine = 16 * G;
     const uint64_t Eu = (u1 + 15) & ~15ull;
@@ -398,13 +426,10 @@ __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0
         fold4w<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
       }
     };
-    // step 0: pieces before A0 read the zero line; the last line: pieces at or
-    // after Eu read it too (they are not in the unit and may be past the buffer)
+    // step 0 (already in a0..a3, unit_first_addrs): pieces before A0 read the
+    // zero line; the last line: pieces at or after Eu read it too (they are not
+    // in the unit and may be past the buffer)
     const uint64_t lim3 = Eu;
-    uint4 a0 = gload16<VAR>(p0 >= A0 ? p0 : zl);
-    uint4 a1 = gload16<VAR>(p0 + 16 * G >= A0 ? p0 + 16 * G : zl);
-    uint4 a2 = gload16<VAR>(p0 + 32 * G >= A0 ? p0 + 32 * G : zl);
-    uint4 a3 = gload16<VAR>((p0 + 48 * G >= A0 && p0 + 48 * G < lim3) ? p0 + 48 * G : zl);
     pre();
     uint64_t s = 0;
     for (; s + 2 <= K4; s += 2) {
@@ -413,16 +438,22 @@ __device__ __forceinline__ uint32_t unit_pending(const uint8_t* lds, uint64_t u0
       const uint4 b2 = gload16<VAR>(pb + 32 * G);
       const uint4 b3 = gload16<VAR>(pb + 48 * G < lim3 ? pb + 48 * G : zl);
       fold_at(a0, a1, a2, a3, s);
-      // the last prefetch re-reads step s+1 (an L2 hit): one loop shape, exact
-      // vmcnt counts
-      const uint64_t pn = (s + 2 < K4) ? pb + kStep : pb;
-      a0 = gload16<VAR>(pn);
-      a1 = gload16<VAR>(pn + 16 * G);
-      a2 = gload16<VAR>(pn + 32 * G);
-      a3 = gload16<VAR>(pn + 48 * G < lim3 ? pn + 48 * G : zl);
+      // after this unit's last step the prefetch takes the next unit's first
+      const bool more = s + 2 < K4;
+      const uint64_t pn = pb + kStep;
+      a0 = gload16<VAR>(more ? pn : x0);
+      a1 = gload16<VAR>(more ? pn + 16 * G : x1);
+      a2 = gload16<VAR>(more ? pn + 32 * G : x2);
+      a3 = gload16<VAR>(more ? (pn + 48 * G < lim3 ? pn + 48 * G : zl) : x3);
       fold_at(b0, b1, b2, b3, s + 1);
     }
-    if (s < K4) fold_at(a0, a1, a2, a3, s);
+    if (s < K4) {
+      fold_at(a0, a1, a2, a3, s);
+      a0 = gload16<VAR>(x0);
+      a1 = gload16<VAR>(x1);
+      a2 = gload16<VAR>(x2);
+      a3 = gload16<VAR>(x3);
+    }
   }
   const int src = (threadIdx.x & 63) - q + (int)(((uint32_t)q + e) & (uint32_t)(G - 1));
   c0 = __shfl(c0, src);
@@ -588,39 +619,62 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
         d_on = false;
       }
     };
-    for (uint32_t r0 = 0; r0 < total; r0 += kGroups) {
+    // The group's unit of the round starting at r0: [u0,u1), its init, its
+    // index j from the block's end and the lane i owning its block.
+    struct Unit {
+      uint64_t u0, u1;
+      uint32_t init, j;
+      int i;
+      bool active;
+    };
+    auto unit_at = [&](uint32_t r0) -> Unit {
+      Unit t{0, 0, 0, 0, 0, false};
       const uint32_t u = r0 + grp;
-      const bool active = u < total;
+      t.active = u < total;
       int r = 0;
 #pragma unroll
       for (int s = 8; s > 0; s >>= 1)
         if (wpre[r + s - 1] <= u) r += s;
-      if (!active) r = 0;
-      const int i = (int)wsort[r];  // lane owning the unit's block
-      const uint32_t a_lo = __shfl((uint32_t)a, i);
-      const uint32_t a_hi = __shfl((uint32_t)(a >> 32), i);
-      const uint32_t bn = __shfl(n, i);
-      const uint32_t bq = __shfl(nq, i);
-      const uint32_t binit = __shfl(ninit, i);
+      if (!t.active) r = 0;
+      t.i = (int)wsort[r];  // lane owning the unit's block
+      const uint32_t a_lo = __shfl((uint32_t)a, t.i);
+      const uint32_t a_hi = __shfl((uint32_t)(a >> 32), t.i);
+      const uint32_t bn = __shfl(n, t.i);
+      const uint32_t bq = __shfl(nq, t.i);
+      const uint32_t binit = __shfl(ninit, t.i);
       const uint32_t bincl = wpre[r];
       const uint64_t ba = ((uint64_t)a_hi << 32) | a_lo;
-      const uint32_t j = bincl - 1 - u;  // 0 = last unit of the block
-      uint64_t u0 = 0, u1 = 0;
-      uint32_t uinit = 0;
-      if (active) {
+      t.j = bincl - 1 - u;  // 0 = last unit of the block
+      if (t.active) {
         const uint64_t E = ba + bn;
-        u1 = E - (uint64_t)p.seg * j;
-        const bool first = (j == bq - 1);
-        u0 = first ? ba : u1 - p.seg;
-        uinit = first ? binit : 0u;
+        t.u1 = E - (uint64_t)p.seg * t.j;
+        const bool first = (t.j == bq - 1);
+        t.u0 = first ? ba : t.u1 - p.seg;
+        t.init = first ? binit : 0u;
       }
-      const uint32_t v = unit_pending<G, VAR>(lds, u0, u1, uinit, q, lo0, lo1, lo2, lo3, zl, finalize);
+      return t;
+    };
+    Unit cur = unit_at(0);
+    uint4 a0, a1, a2, a3;  // the current unit's first step, in flight
+    {
+      uint64_t x0, x1, x2, x3;
+      unit_first_addrs<G>(cur.u0, cur.u1, q, zl, x0, x1, x2, x3);
+      a0 = gload16<VAR>(x0);
+      a1 = gload16<VAR>(x1);
+      a2 = gload16<VAR>(x2);
+      a3 = gload16<VAR>(x3);
+    }
+    for (uint32_t r0 = 0; r0 < total; r0 += kGroups) {
+      const Unit nxt = unit_at(r0 + kGroups);
+      const uint32_t v = unit_pending<G, VAR>(lds, cur.u0, cur.u1, cur.init, q, lo0, lo1, lo2, lo3,
+                                              zl, finalize, a0, a1, a2, a3, nxt.u0, nxt.u1);
       // this unit's contribution is folded in during the next unit's first loads
-      d_on = active && q == 0;
+      d_on = cur.active && q == 0;
       d_v = v;
-      d_t = (uint32_t)((16 - (u1 & 15)) & 15);
-      d_m = (uint64_t)(p.seg >> 4) * j;
-      d_i = i;
+      d_t = (uint32_t)((16 - (cur.u1 & 15)) & 15);
+      d_m = (uint64_t)(p.seg >> 4) * cur.j;
+      d_i = cur.i;
+      cur = nxt;
     }
     finalize();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
