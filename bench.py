@@ -302,7 +302,8 @@ def main() -> int:
                          "kernel_ms_median": round(sorted(kernel_ms)[len(kernel_ms) // 2], 4)},
             "verified_sample": verified,
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:
+            # rank 0 at N=1 only: the CPU sample is the same at every N
             th = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
             res["cpu_baseline"] = cpu_baseline(th, args.cpu_seconds)
         print(json.dumps(res), flush=True)
