@@ -34,7 +34,7 @@ def main():
         sys.exit(1)
     f_med = sorted(fetch)[len(fetch) // 2]
     w_med = sorted(write)[len(write) // 2] if write else None
-    algo = {"2": 1 << 32, "4": 1 << 34}.get(cfg)
+    algo = {"2": 1 << 32, "3": 30060563723, "4": 1 << 34}.get(cfg)  # config 3: bench.config3_layout sum
     res = {
         "config": int(cfg),
         "dispatches": len(fetch),
