@@ -314,6 +314,19 @@ __device__ __forceinline__ uint32_t unmask_crc(uint32_t m) {
   const uint32_t r = m - 0xa282ead8u;  // util/crc32c.h:34-37
   return (r >> 17) | (r << 15);
 }
+// Trailer [type][LE32 masked crc] (table/format.h:103, table/table_builder.cc:202-206):
+// one byte store plus one unaligned dword store instead of five byte stores.
+// gfx950 global memory runs in unaligned mode (the backend emits a plain
+// global_store_dword for an align-1 u32); a store that straddles a 128-B line
+// is split by the hardware.  With the TableBuilder quirk the dword's top byte is '!'.
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+__device__ __forceinline__ void store_u32_unaligned(uint8_t* d, uint32_t v) {
+  *(__attribute__((address_space(1))) u32_unaligned*)d = v;
+}
+__device__ __forceinline__ void store_trailer(uint8_t* d, uint32_t type, uint32_t m, bool quirk) {
+  *(__attribute__((address_space(1))) uint8_t*)d = (uint8_t)type;
+  store_u32_unaligned(d + 1, quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m);
+}
 
 // Fold the 4G pending stream words of a lane group (4 per lane, lane q holds
 // the words at byte offsets 16q+0,4,8,12 of each 16G-byte swath) into the
@@ -712,12 +725,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
         }
         if (MODE == kTrailer) {
           const uint32_t m = mask_crc(crc);
-          uint8_t* d = (uint8_t*)a + n;
-          d[0] = (uint8_t)(p.flags >> 8);
-          d[1] = (uint8_t)m;
-          d[2] = (uint8_t)(m >> 8);
-          d[3] = (uint8_t)(m >> 16);
-          d[4] = (p.flags & NOVA_TRAILER_TB_QUIRK) ? (uint8_t)'!' : (uint8_t)(m >> 24);
+          store_trailer((uint8_t*)a + n, (p.flags >> 8) & 0xffu, m,
+                        (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
         } else {
           if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
           p.out[b] = crc;
@@ -1152,21 +1161,12 @@ __device__ __forceinline__ void write_result(const CrcParams& p, uint64_t wb_a, 
   typedef __attribute__((address_space(1))) uint8_t gu8;
   typedef __attribute__((address_space(1))) uint32_t gu32;
   if constexpr (MODE == kLogWrite) {
-    gu8* h = (gu8*)wb_a;
-    h[0] = (uint8_t)wb_v;
-    h[1] = (uint8_t)(wb_v >> 8);
-    h[2] = (uint8_t)(wb_v >> 16);
-    h[3] = (uint8_t)(wb_v >> 24);
+    store_u32_unaligned((uint8_t*)wb_a, wb_v);
   } else if constexpr (MODE == kLogVerify || MODE == kVerify) {
     *(gu8*)wb_a = (uint8_t)wb_v;
     if (!wb_v && p.n_bad) atomicAdd(p.n_bad, 1u);
   } else if constexpr (MODE == kTrailer) {
-    gu8* d = (gu8*)wb_a;
-    d[0] = (uint8_t)(p.flags >> 8);
-    d[1] = (uint8_t)wb_v;
-    d[2] = (uint8_t)(wb_v >> 8);
-    d[3] = (uint8_t)(wb_v >> 16);
-    d[4] = (p.flags & NOVA_TRAILER_TB_QUIRK) ? (uint8_t)'!' : (uint8_t)(wb_v >> 24);
+    store_trailer((uint8_t*)wb_a, (p.flags >> 8) & 0xffu, wb_v, (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
   } else {
     *(gu32*)wb_a = wb_v;
   }
@@ -2041,20 +2041,15 @@ __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, co
 // trailer [type][LE32] at base + offsets[i] + sizes[i], with '!' over its last
 // byte for TableBuilder's ordering (table/table_builder.cc:202-206,
 // ltc/stoc_file_client_impl.cpp:713-719).  Inside the streaming kernel the
-// five byte stores per block cost ~12 points of HBM throughput.
+// trailer stores per block cost ~12 points of HBM throughput.
 __global__ void __launch_bounds__(256) trailer_scatter_kernel(uint8_t* base, const uint64_t* offsets,
                                                               const uint32_t* sizes,
                                                               const uint32_t* crc, uint64_t n,
                                                               uint32_t flags) {
   const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
-    uint8_t* d = base + offsets[i] + sizes[i];
-    const uint32_t m = crc[i];
-    d[0] = (uint8_t)(flags >> 8);
-    d[1] = (uint8_t)m;
-    d[2] = (uint8_t)(m >> 8);
-    d[3] = (uint8_t)(m >> 16);
-    d[4] = (flags & NOVA_TRAILER_TB_QUIRK) ? (uint8_t)'!' : (uint8_t)(m >> 24);
+    store_trailer(base + offsets[i] + sizes[i], (flags >> 8) & 0xffu, crc[i],
+                  (flags & NOVA_TRAILER_TB_QUIRK) != 0);
   }
 }
 
