@@ -497,18 +497,41 @@ __device__ __forceinline__ void sched_release(uint32_t* sched) {
   }
 }
 
+// Launch prologue: the LDS table image (main tables, tree levels, optional
+// byte table), contiguous in LDS, copied with 8 loads in flight per thread.
+// A plain copy loop waits on every load before issuing the next: ~20 serial
+// L2 round trips per workgroup, a fixed cost that dominated small batches.
+__device__ __forceinline__ void lds_fill_tables(uint8_t* lds, const void* tab_main,
+                                                const void* tab_tree, uint32_t tree16,
+                                                const void* tab_byte, uint32_t byte16) {
+  constexpr uint32_t kMain16 = kMainBytes / 16;
+  const uint32_t n16 = kMain16 + tree16 + byte16;
+  // per-source base addresses, rebased so that LDS index j reads base + 16 j
+  const uint64_t am = (uint64_t)tab_main;
+  const uint64_t at = (uint64_t)tab_tree - 16ull * kMain16;
+  const uint64_t ab = (uint64_t)tab_byte - 16ull * (kMain16 + tree16);
+  uint4* d = reinterpret_cast<uint4*>(lds);
+  const uint32_t nt = blockDim.x;
+  for (uint32_t i = threadIdx.x; i < n16; i += 8 * nt) {
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint32_t j = i + k * nt;
+      j = j < n16 ? j : n16 - 1;  // clamped: every load issued, stores predicated
+      const uint64_t a = j < kMain16 ? am : (j < kMain16 + tree16 ? at : ab);
+      v[k] = gload16<kVarCached>(a + 16ull * j);  // default policy: tables stay in L2
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (i + k * nt < n16) d[i + k * nt] = v[k];
+  }
+}
+
 template <int G, int MODE, int VAR = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
-  {
-    const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
-    uint4* d = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += blockDim.x) d[i] = s[i];
-    const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
-    uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
-    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += blockDim.x) d2[i] = s2[i];
-  }
+  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, nullptr, 0);
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
@@ -753,14 +776,7 @@ template <int G, int VAR = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(CrcParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
-  {
-    const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
-    uint4* d = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += blockDim.x) d[i] = s[i];
-    const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
-    uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
-    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += blockDim.x) d2[i] = s2[i];
-  }
+  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, nullptr, 0);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1180,17 +1196,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
   constexpr bool kLog = MODE == kLogWrite || MODE == kLogVerify;
   constexpr bool kTail2 = MODE == kVerify;  // stored CRC follows the CRC input
   constexpr uint64_t kStep = 64 * G;
-  {
-    const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
-    uint4* d = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += blockDim.x) d[i] = s[i];
-    const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
-    uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
-    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += blockDim.x) d2[i] = s2[i];
-    const uint4* s3 = reinterpret_cast<const uint4*>(p.tab_byte);
-    uint4* d3 = reinterpret_cast<uint4*>(lds + kByteTab);
-    for (int i = threadIdx.x; i < 64; i += blockDim.x) d3[i] = s3[i];
-  }
+  static_assert(kByteTab == kMainBytes + kLevels * kTreeBytes, "byte table follows the tree");
+  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, p.tab_byte, 64);
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
@@ -1575,17 +1582,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   constexpr bool kTail2 = MODE == kVerify;
   constexpr uint64_t kStep = 64 * G;
   constexpr uint32_t kGroups = 64 / G;
-  {
-    const uint4* s = reinterpret_cast<const uint4*>(p.tab_main);
-    uint4* d = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < (int)(kMainBytes / 16); i += blockDim.x) d[i] = s[i];
-    const uint4* s2 = reinterpret_cast<const uint4*>(p.tab_tree);
-    uint4* d2 = reinterpret_cast<uint4*>(lds + kMainBytes);
-    for (int i = threadIdx.x; i < (int)(kLevels * kTreeBytes / 16); i += blockDim.x) d2[i] = s2[i];
-    const uint4* s3 = reinterpret_cast<const uint4*>(p.tab_byte);
-    uint4* d3 = reinterpret_cast<uint4*>(lds + kByteTab);
-    for (int i = threadIdx.x; i < 64; i += blockDim.x) d3[i] = s3[i];
-  }
+  static_assert(kByteTab == kMainBytes + kLevels * kTreeBytes, "byte table follows the tree");
+  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, p.tab_byte, 64);
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
@@ -2392,6 +2390,7 @@ struct Plan {
   int kernel;
   int G;
   uint32_t seg;
+  uint32_t chunk;  // rounds kernel: blocks per claimed chunk (0: the kernel's default)
 };
 // Measured (tools/sweep_flat.py, profiles/r01_sweep_lines.log):
 //   SSTable-like 4096+U[0,255] B blocks: rounds G=8 73.7 %, units 53-57 %;
@@ -2400,10 +2399,18 @@ struct Plan {
 //   log records U[1,4096] B: rounds G=8, chunks of 64, 55.2 %.
 // Blocks are checksummed whole in rounds unless the caller says most are
 // >= 16 KiB (NOVA_CRC32C_HINT_LARGE_BLOCKS) or the fixed length is.
-Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, bool large) {
-  (void)n_blocks;
+//
+// Small batches (one SSTable per call, NovaLSM's pattern: ~4K blocks) are
+// latency-bound: a wave walks its chunk's rounds one step at a time, so the
+// launch lasts as long as the longest chunk.  Below ~2 chunks per wave slot
+// the chunks shrink (32 -> 16 -> 8 blocks), and at <= 2 blocks per wave slot
+// the groups widen to 16 lanes with 4-block chunks, halving the steps per
+// block (tools/latency.py, profiles/r01_latency.log: 4K x 4 KiB verify
+// 77 -> 31 us, 64K blocks 83 -> 70 us; 256K blocks unchanged).
+Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, bool large,
+          uint32_t cus = 256) {
   const bool log = mode == kLogWrite || mode == kLogVerify;
-  Plan pl{kRoundsK, 8, 0u};
+  Plan pl{kRoundsK, 8, 0u, 0u};
   if (!log && ((uniform && bytes_per_block >= 16384) || (!uniform && large))) {
     pl.kernel = kUnitsK;
     pl.G = 16;
@@ -2419,6 +2426,15 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, b
   if (pl.kernel == kFlatK || pl.kernel == kRoundsK) {
     pl.seg = 0;
     if (pl.G == 1) pl.G = 2;  // at most 32 groups per wave (chunk >= 2 groups <= 64)
+  }
+  if (pl.kernel == kRoundsK && !log && tk == kAuto && tg == 0 && g_tune_chunk.load() == 0) {
+    const uint64_t slots = 2ull * cus * flat_waves();  // two chunks per wave slot
+    if (n_blocks <= slots) {
+      pl.G = 16;
+      pl.chunk = 4;
+    } else {
+      pl.chunk = n_blocks >= 32 * slots ? 32u : (n_blocks >= 16 * slots ? 16u : 8u);
+    }
   }
   return pl;
 }
@@ -2673,7 +2689,7 @@ int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream
 }
 
 template <int MODE>
-int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
+int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_t chunk = 0) {
   if (G < 2) G = 2;
   p.tab_main = t->main[gindex(G)];
   p.tab_tree = t->tree;
@@ -2709,7 +2725,7 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
     // also the unit of the tail balance and big blocks make big chunks.
     const uint32_t groups = 64u / (uint32_t)G;
     const bool log = MODE == kLogWrite || MODE == kLogVerify;
-    uint32_t c = log ? 64u : 4u * groups;
+    uint32_t c = log ? 64u : (chunk ? chunk : 4u * groups);
     const int tc = g_tune_chunk.load();
     if (tc > 0) c = (uint32_t)tc;
     c = (c / groups) * groups;
@@ -2783,7 +2799,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     if (sg) return launch_stream(sg, p, t, stream);
   }
   const Plan pl = plan(p.n_blocks, bytes_per_block, uniform, mode,
-                       (p.flags & NOVA_CRC32C_HINT_LARGE_BLOCKS) != 0);
+                       (p.flags & NOVA_CRC32C_HINT_LARGE_BLOCKS) != 0, (uint32_t)t->cus);
   const int G = pl.G;
   p.seg = pl.seg;
   if (pl.kernel == kRoundsK && mode == kTrailer && !g_tune_trailer_1pass.load()) {
@@ -2794,7 +2810,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     CrcParams q = p;
     q.out = tmp;
     q.flags = (p.flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT;
-    const int e = launch_rounds<kStore>(G, q, t, stream);
+    const int e = launch_rounds<kStore>(G, q, t, stream, pl.chunk);
     if (e) return e;
     uint64_t wgs = (p.n_blocks + 255) / 256;
     const uint64_t cap = (uint64_t)t->cus * 8;
@@ -2805,11 +2821,11 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   }
   if (pl.kernel == kRoundsK) {
     switch (mode) {
-      case kStore: return launch_rounds<kStore>(G, p, t, stream);
-      case kTrailer: return launch_rounds<kTrailer>(G, p, t, stream);
+      case kStore: return launch_rounds<kStore>(G, p, t, stream, pl.chunk);
+      case kTrailer: return launch_rounds<kTrailer>(G, p, t, stream, pl.chunk);
       case kLogWrite: return launch_rounds<kLogWrite>(G, p, t, stream);
       case kLogVerify: return launch_rounds<kLogVerify>(G, p, t, stream);
-      default: return launch_rounds<kVerify>(G, p, t, stream);
+      default: return launch_rounds<kVerify>(G, p, t, stream, pl.chunk);
     }
   }
   if (pl.kernel == kFlatK) {
@@ -3007,8 +3023,9 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
     if (pl.kernel == kRoundsK)
       n = snprintf(buf, buflen,
                    "{\"kernel\": \"crc32c_rounds_kernel<%d, 0>\", \"lanes_per_block\": %d, "
-                   "\"sort\": %d, \"waves_per_wg\": %d}", g < 2 ? 2 : g, g < 2 ? 2 : g,
-                   g_tune_sort.load(), (int)flat_waves());
+                   "\"sort\": %d, \"waves_per_wg\": %d, \"chunk_blocks\": %u}", g < 2 ? 2 : g,
+                   g < 2 ? 2 : g, g_tune_sort.load(), (int)flat_waves(),
+                   pl.chunk ? pl.chunk : 4u * (64u / (uint32_t)(g < 2 ? 2 : g)));
     else if (pl.kernel != kFlatK)
       n = snprintf(buf, buflen,
                    "{\"kernel\": \"crc32c_units_kernel<%d, 0>\", \"lanes_per_unit\": %d, "
