@@ -631,3 +631,39 @@ def test_large_blocks_hint_same_results(torch_gpu, oracle, mode):
             assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
             assert int(bad.item()) == len(victims)
         C.set_tuning(0, 0)
+
+
+@pytest.mark.parametrize("n", [1, 5, 6144, 6145, 49152, 98303, 98304, 196608])
+def test_batch_size_dispatch_thresholds(torch_gpu, oracle, n):
+    """plan() sizes the rounds kernel to the batch (16-lane groups with 4-block
+    chunks up to 2 blocks per wave slot = 6144 on 256 CUs x 12 waves, then 8-,
+    16- and 32-block chunks at 16x / 32x that).  Every side of each threshold,
+    on ragged unaligned blocks, through store, trailers and verify, matches the
+    oracle; describe() names the chunk the dispatcher picked."""
+    torch = torch_gpu
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 300, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5))
+    host = splitmix64_bytes(n + 17, int(offs[-1]) + int(lens[-1]) + 5 + 64).copy()
+    do, dl = dev(torch, offs, torch.int64), dev(torch, lens, torch.int32)
+    out = C.batch(dev(torch, host), do, dl)
+    assert np.array_equal(u32(out), oracle.batch(host, offs, lens, None))
+    buf = dev(torch, host)
+    C.write_trailers(buf, do, dl, 0, False)
+    h = buf.cpu().numpy()
+    for i in np.linspace(0, n - 1, min(n, 64)).astype(np.int64):
+        o, ln = int(offs[i]), int(lens[i])
+        assert oracle.trailer(host[o:o + ln].tobytes(), 0, False) == h[o + ln:o + ln + 5].tobytes()
+    victims = rng.choice(n, min(n, 3), replace=False)
+    for v in victims:
+        if lens[v]:
+            buf[int(offs[v])] ^= 0x01
+        else:  # empty block: corrupt its stored CRC
+            buf[int(offs[v]) + 1] ^= 0x01
+    ok, bad = C.verify_blocks(buf, do, dl)
+    assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
+    assert int(bad.item()) == len(victims)
+    d = C.describe(n, 0, 0, variable=True)
+    want_chunk = 4 if n <= 6144 else (32 if n >= 196608 else 16 if n >= 98304 else 8)
+    assert d["chunk_blocks"] == want_chunk and d["lanes_per_block"] == (16 if n <= 6144 else 8)
