@@ -2513,6 +2513,10 @@ int launch_flat(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   {
     const int sl = g_tune_static_pct.load();
     p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;
+    // The first nwaves x wgs chunks are implicit (one per wave): when they cover
+    // the batch, a claim or a steal can only come back empty, and each of the
+    // 8 probes is a serial device-scope atomic (~1.5 us) on the launch's tail.
+    if (sl < 0 && p.n_chunks <= wgs * (uint64_t)nwaves) p.steal_limit = 0;
   }
   p.sched = sched_slot(t, stream);
   if (!p.sched) return NOVA_E_NOMEM;
@@ -2557,6 +2561,10 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   {
     const int sl = g_tune_static_pct.load();
     p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;
+    // The first nwaves x wgs chunks are implicit (one per wave): when they cover
+    // the batch, a claim or a steal can only come back empty, and each of the
+    // 8 probes is a serial device-scope atomic (~1.5 us) on the launch's tail.
+    if (sl < 0 && p.n_chunks <= wgs * (uint64_t)nwaves) p.steal_limit = 0;
   }
   p.sched = sched_slot(t, stream);
   if (!p.sched) return NOVA_E_NOMEM;
@@ -2742,6 +2750,10 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_
   {
     const int sl = g_tune_static_pct.load();
     p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;
+    // The first nwaves x wgs chunks are implicit (one per wave): when they cover
+    // the batch, a claim or a steal can only come back empty, and each of the
+    // 8 probes is a serial device-scope atomic (~1.5 us) on the launch's tail.
+    if (sl < 0 && p.n_chunks <= wgs * (uint64_t)nwaves) p.steal_limit = 0;
   }
   p.sched = sched_slot(t, stream);
   if (!p.sched) return NOVA_E_NOMEM;
@@ -2769,6 +2781,9 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   {
     const int sl = g_tune_static_pct.load();
     p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;  // 8 probes = one victim per XCD
+    // the first nwaves x wgs rounds are implicit: if they cover the batch no
+    // claim or steal can find work (8 serial atomics on the tail otherwise)
+    if (sl < 0 && rounds <= wgs * nwaves) p.steal_limit = 0;
   }
   // claim counters of this stream (left zeroed by the previous launch)
   p.sched = sched_slot(t, stream);
