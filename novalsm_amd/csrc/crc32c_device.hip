@@ -2817,7 +2817,11 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
                        (p.flags & NOVA_CRC32C_HINT_LARGE_BLOCKS) != 0, (uint32_t)t->cus);
   const int G = pl.G;
   p.seg = pl.seg;
-  if (pl.kernel == kRoundsK && mode == kTrailer && !g_tune_trailer_1pass.load()) {
+  // Batches that fit the implicit per-wave chunks (SSTable-sized, latency-bound)
+  // write their trailers from the CRC kernel: a second launch would add its
+  // whole fixed cost to the call.
+  const bool small = p.n_blocks <= 2ull * t->cus * flat_waves();
+  if (pl.kernel == kRoundsK && mode == kTrailer && !g_tune_trailer_1pass.load() && !small) {
     // Two passes: CRCs (type byte appended, masked) into a per-stream array,
     // then the trailer bytes (trailer_scatter_kernel).
     uint32_t* tmp = crc_scratch(t, stream, p.n_blocks);

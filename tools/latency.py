@@ -12,6 +12,7 @@ calling thread.  For batches of n SSTable-like blocks (4096+U[0,255] B each,
   dev_wall_us     nova_sstable_verify_blocks on a device-resident image, call +
                   stream sync, host wall clock (launch + kernel + sync)
   dev_kernel_us   the same launch timed with HIP events on the launch stream
+  trailers_kernel_us  nova_sstable_write_trailers on the same image (events)
   host_wall_us    image in pinned host memory: H2D copy, verify, D2H of the
                   per-block flags, sync (what an LTC with the table in its
                   RDMA-registered buffer would see)
@@ -158,6 +159,15 @@ def main() -> int:
             b.synchronize()
             evs.append(a.elapsed_time(b) * 1e3)
         assert int(bad.item()) == 0 and bool(okb.cpu().numpy().all()), "verify failed"
+        tw = []  # trailer writer (StoC order), same device-resident image
+        for i in range(min(R, 200) + 10):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            C.write_trailers(dev, offs, lens, 0, False, stream=stream)
+            b.record(stream)
+            b.synchronize()
+            if i >= 10:
+                tw.append(a.elapsed_time(b) * 1e3)
 
         # host-resident: H2D, verify, D2H flags
         def host_call():
@@ -205,6 +215,7 @@ def main() -> int:
         row = {"n_blocks": n, "bytes": sum_len, "MiB": round(sum_len / 2**20, 2),
                "dev_wall_us": round(med(walls) * 1e6, 1),
                "dev_kernel_us": round(med(evs), 1),
+               "trailers_kernel_us": round(med(tw), 1),
                "host_wall_us": round(med(hwalls) * 1e6, 1),
                "cpu_ref_us": round(med(cw) * 1e6, 1),
                "cpu_kind": kind,
