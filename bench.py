@@ -256,9 +256,15 @@ def main() -> int:
                 o, l = int(offs_np[i]), int(lens_np[i])
             blk = buf[o:o + l].cpu().numpy().tobytes()
             ok &= orc.value(blk) == int(got[i])
+        if world > 1:  # every rank learns whether any shard failed (no rank left in a barrier)
+            f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            ok = bool(f.item())
         verified = bool(ok)
         if not ok:
-            print(json.dumps({"error": "GPU CRC mismatch vs oracle"}), file=sys.stderr)
+            print(json.dumps({"error": "GPU CRC mismatch vs oracle", "rank": rank}), file=sys.stderr)
+            if world > 1:
+                dist.destroy_process_group()
             return 3
 
     value = world * bytes_step * args.steps / dt / 2**30
