@@ -105,3 +105,17 @@ def test_device_init_fails_loudly_without_gpu(lib):
     rc = lib.nova_crc32c_batch_strided(ctypes.c_void_p(16), 16, 16, 1, None,
                                        ctypes.addressof(out), 0, None)
     assert rc != 0  # no silent CPU fallback
+
+
+@pytest.mark.parametrize("n,lanes,chunk", [
+    (1, 16, 4), (6144, 16, 4), (6145, 8, 8), (98303, 8, 8), (98304, 8, 16),
+    (196607, 8, 16), (196608, 8, 32), (1 << 20, 8, 32)])
+def test_rounds_plan_sized_to_the_batch(n, lanes, chunk):
+    """Host-side dispatch (no device call): variable SSTable batches go to the
+    rounds kernel with 16-lane groups and 4-block chunks while they fit two
+    chunks per wave slot (256 CUs x 12 waves), then 8-lane groups with 8/16/32-
+    block chunks; the large-blocks hint picks the units kernel."""
+    d = C.describe(n, 0, 0, variable=True)
+    assert d["kernel"].startswith("crc32c_rounds_kernel")
+    assert (d["lanes_per_block"], d["chunk_blocks"]) == (lanes, chunk)
+    assert C.describe(n, 0, 0, variable=True, large=True)["kernel"].startswith("crc32c_units_kernel")
