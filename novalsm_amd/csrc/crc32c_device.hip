@@ -2427,6 +2427,13 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, b
     pl.seg = 0;
     if (pl.G == 1) pl.G = 2;  // at most 32 groups per wave (chunk >= 2 groups <= 64)
   }
+  if (pl.kernel == kRoundsK && log && tk == kAuto && tg == 0 && g_tune_chunk.load() == 0) {
+    // log records (~2 KiB): 16-record chunks below 32 chunks' worth per wave
+    // slot (16 MiB log: 95 -> 40 us), the default 64 only for GiB-sized logs
+    // (tools/latency_log.py, profiles/r01_latency_log.log)
+    const uint64_t slots = 2ull * cus * flat_waves();
+    pl.chunk = n_blocks >= 64 * slots ? 0u : (n_blocks >= 32 * slots ? 32u : 16u);
+  }
   if (pl.kernel == kRoundsK && !log && tk == kAuto && tg == 0 && g_tune_chunk.load() == 0) {
     const uint64_t slots = 2ull * cus * flat_waves();  // two chunks per wave slot
     if (n_blocks <= slots) {
@@ -2733,7 +2740,7 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_
     // also the unit of the tail balance and big blocks make big chunks.
     const uint32_t groups = 64u / (uint32_t)G;
     const bool log = MODE == kLogWrite || MODE == kLogVerify;
-    uint32_t c = log ? 64u : (chunk ? chunk : 4u * groups);
+    uint32_t c = chunk ? chunk : (log ? 64u : 4u * groups);
     const int tc = g_tune_chunk.load();
     if (tc > 0) c = (uint32_t)tc;
     c = (c / groups) * groups;
@@ -2842,8 +2849,8 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     switch (mode) {
       case kStore: return launch_rounds<kStore>(G, p, t, stream, pl.chunk);
       case kTrailer: return launch_rounds<kTrailer>(G, p, t, stream, pl.chunk);
-      case kLogWrite: return launch_rounds<kLogWrite>(G, p, t, stream);
-      case kLogVerify: return launch_rounds<kLogVerify>(G, p, t, stream);
+      case kLogWrite: return launch_rounds<kLogWrite>(G, p, t, stream, pl.chunk);
+      case kLogVerify: return launch_rounds<kLogVerify>(G, p, t, stream, pl.chunk);
       default: return launch_rounds<kVerify>(G, p, t, stream, pl.chunk);
     }
   }

@@ -550,7 +550,8 @@ def test_flat_many_blocks(torch_gpu, oracle, kernel, lanes, chunk, waves):
 
 @pytest.mark.parametrize("kernel,lanes,chunk", [
     (0, 0, 0), (1, 4, 0), (1, 16, 0), (2, 0, 0), (2, 2, 0), (2, 4, 0), (2, 8, 0), (2, 16, 0),
-    (2, 8, 16), (2, 4, 17), (2, 16, 64), (3, 0, 0), (3, 2, 0), (3, 4, 0), (3, 16, 0)])
+    (2, 8, 16), (2, 4, 17), (2, 16, 64), (3, 0, 0), (3, 2, 0), (3, 4, 0), (3, 16, 0),
+    (3, 8, 16), (3, 8, 32), (3, 16, 16), (3, 8, 8)])
 def test_log_many_records(torch_gpu, oracle, kernel, lanes, chunk):
     """Log record CRC write + verify over a log image with enough records to
     exercise the header pipeline of the flat kernel's descriptor banks
