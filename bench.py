@@ -2,32 +2,46 @@
 """Device-resident batched CRC32C throughput on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+                    [--secondary 3,4|none] [--settle-ms MS]
 
 One step = one pass of the hot path (a nova_crc32c_batch* call through the
 C-ABI) over one batch of synthetic SSTable blocks already resident in HBM.
-Default workload at every N: BASELINE config 2 per rank (1M x 4 KiB uniform
-blocks = 4 GiB per GPU, splitmix64 data generated on the device), weak scaling:
-rank r checksums its own shard, no data-path collective; RCCL only for the
-barrier and the max-over-ranks time.  --config 3: 1M mixed {4,16,64} KiB +
-U[1,64] B unaligned blocks (variable-length kernel).  --config 4: 1M x 16 KiB
-per rank (8M x 16 KiB over 8 GPUs).  --config 5: host-resident (pinned) 16 KiB
-blocks streamed H2D -> CRC -> D2H; reported separately, never as
-the device-resident value.
 
-Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes per
-launch (sum of block lengths) / average launch time measured
-with HIP events on the launch stream inside the timed region.
-Defaults W=50, K=200: back-to-back launches show a power-management transient
-(launches ~4-25 run up to 30% slower, then settle; tools/launches.py), so
-the timed steps start after it.
-`cpu_baseline` = the reference util/crc32c.cc (oracle/_ref, compiled from the
-reference sources) or the oracle restatement, timed on this host's cores.
+Workloads (BASELINE.json configs; per GPU, weak scaling):
+  2  1M x 4 KiB uniform blocks (4 GiB) -- the headline `value` (configs[1])
+  3  1M mixed {4,16,64} KiB + U[1,64] B unaligned blocks (~28 GiB), the
+     variable-length kernel with NOVA_CRC32C_HINT_LARGE_BLOCKS
+  4  1M x 16 KiB (16 GiB; 8M x 16 KiB over 8 GPUs)
+  5  host-resident (pinned) 16 KiB blocks streamed H2D -> CRC -> D2H; its own
+     line, never the device-resident value
+By default the line carries config 2 as `value` and configs 3 and 4 as
+`secondary` objects measured in the same run, each with its own roofline.
+
+Multi-GPU: one process per GPU.  Run under torchrun (WORLD_SIZE set) each rank
+takes its device from LOCAL_RANK; run as `python bench.py --gpus N` without
+torchrun, this process starts `torch.distributed.run` with N ranks as a CHILD
+process before anything touches the GPU, and exits with its code.  Ranks
+checksum their own shards (no data-path collective); RCCL carries only the
+barriers, the max-over-ranks time and the per-rank kernel times.
+
+Timing: a time-based settle (--settle-ms of back-to-back launches: the first
+~25 launches of a burst run up to 30% slower in a power-management transient,
+DESIGN.md 3.6), then W untimed warmup launches, then K launches bracketed by
+barrier + synchronize; `value` = bytes of all ranks / max-over-ranks wall time.
+`roofline.achieved` = algorithmic bytes per launch (sum of block lengths;
+SURVEY.md 8(d)) / the average launch time from HIP events recorded on the
+launch stream.  `cpu_baseline` = the reference util/crc32c.cc (oracle/_ref,
+compiled from the reference sources) or the oracle restatement, timed on this
+host's cores (rank 0 at N=1 only).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -70,9 +84,42 @@ def workload(cfg: int):
     raise SystemExit(f"unknown config {cfg}")
 
 
-def cpu_baseline(threads: int, seconds: float = 4.0):
+# ---- host CPU share ---------------------------------------------------------
+
+def host_cpus():
+    """(threads to use, description): the CPUs this process may run on
+    (sched_getaffinity), capped by a cgroup v2 CPU quota and by the host's
+    stated per-job CPU share (OMP_NUM_THREADS: 16 per GPU on the GPU boxes)
+    when those are set.  All three are reported."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    share = None
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "")) or None
+    except ValueError:
+        pass
+    threads = aff
+    if quota is not None:
+        threads = min(threads, int(math.ceil(quota)))
+    if share is not None:
+        threads = min(threads, share)
+    return max(1, threads), {"affinity_cpus": aff, "cgroup_quota_cpus": quota,
+                             "omp_num_threads": share}
+
+
+def cpu_baseline(seconds: float = 4.0):
     """Reference util/crc32c.cc (oracle/_ref) if built, else the oracle restatement,
-    on BASELINE config 1: 1024 x 4 KiB splitmix64(seed 1) blocks, repeated."""
+    on BASELINE config 1: 1024 x 4 KiB splitmix64(seed 1) blocks, repeated,
+    on 1 thread and on all of this process's CPUs; plus the reference's own
+    db_bench crc32c method (benchmarks/db_bench.cc:635-652: Value() over the
+    same 4 KiB of 'x' until 500 MiB, 1 thread)."""
     import ctypes
     from novalsm_amd.synth import splitmix64_bytes
     ref = os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so")
@@ -81,16 +128,18 @@ def cpu_baseline(threads: int, seconds: float = 4.0):
     out = np.empty(n, dtype=np.uint32)
     if os.path.exists(ref):
         lib = ctypes.CDLL(ref)
-        fn = lib.ref_batch_strided_mt
+        fn, dbb = lib.ref_batch_strided_mt, lib.ref_dbbench_crc32c
         kind = "reference"
     else:
         from tests.oracle_lib import load_oracle
         lib = load_oracle().lib
-        fn = lib.oracle_batch_strided_mt
+        fn, dbb = lib.oracle_batch_strided_mt, lib.oracle_dbbench_crc32c
         kind = "port"
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t,
                    ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    dbb.restype = ctypes.c_uint32
+    dbb.argtypes = [ctypes.c_int64]
 
     def rate(th):
         reps = 1
@@ -107,8 +156,13 @@ def cpu_baseline(threads: int, seconds: float = 4.0):
         dt = time.perf_counter() - t0
         return n * L * reps / dt / 2**30, reps
 
+    threads, share = host_cpus()
     one, r1 = rate(1)
     allc, r2 = rate(threads)
+    db_bytes = 500 * 1048576
+    t0 = time.perf_counter()
+    crc = dbb(db_bytes)
+    db_s = time.perf_counter() - t0
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -119,94 +173,84 @@ def cpu_baseline(threads: int, seconds: float = 4.0):
     except OSError:
         pass
     return {"value": round(allc, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "single_core": round(one, 3), "cpu": model,
+            "single_core": round(one, 3), "cpu": model, **share,
             "sample": f"BASELINE config 1: 1024 x 4 KiB splitmix64(seed 1) blocks, "
-                      f"{r2} reps on {threads} threads (+{r1} reps on 1 thread), g++ -O2"}
+                      f"{r2} reps on {threads} threads (+{r1} reps on 1 thread), g++ -O2",
+            "db_bench_crc32c": {"value": round(db_bytes / db_s / 2**30, 3), "unit": "GiB/s",
+                                "threads": 1, "crc": f"0x{crc:08x}",
+                                "sample": "benchmarks/db_bench.cc:635-652: Value(4 KiB of 'x') "
+                                          "until 500 MiB, 1 thread"}}
 
 
-def main() -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--lanes", type=int, default=0, help="lanes per unit override (tuning)")
-    ap.add_argument("--seg", type=int, default=0, help="segment bytes override (tuning)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=4.0)
-    ap.add_argument("--verify", type=int, default=1, help="sample-verify vs the oracle")
-    args = ap.parse_args()
+# ---- launcher -----------------------------------------------------------------
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start n ranks under torch.distributed.run as a child process (this
+    process has not touched the GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+# ---- one device-resident config ------------------------------------------------
+
+class Ctx:
+    def __init__(self, world, rank, dev, dist):
+        self.world, self.rank, self.dev, self.dist = world, rank, dev, dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def all_gather_f64(self, x: float):
+        import torch
+        if self.world == 1:
+            return [x]
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return [float(p.item()) for p in parts]
+
+
+def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
     import torch
-    import torch.distributed as dist
     from novalsm_amd import crc32c as C
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
-    C.load()
-    if args.lanes or args.seg:
-        C.set_tuning(args.lanes, args.seg)
-    if C.load().nova_device_init() != 0:
-        raise SystemExit("nova_device_init failed")
-
-    wl = workload(args.config)
+    wl = workload(cfg)
     stream = torch.cuda.current_stream()
     n = wl["n_blocks"]
-    seed = args.config
-
-    if wl["kind"] == "host":
-        L = wl["block_bytes"]
-        host = torch.empty(n * L, dtype=torch.uint8).pin_memory()
-        tmp = torch.empty(n * L, dtype=torch.uint8, device=dev)
-        C.fill_splitmix64(tmp, seed, first_word=rank * (n * L // 8))
-        host.copy_(tmp.cpu())
-        del tmp
-        for _ in range(max(1, args.warmup)):
-            C.stream_host(host, L, L, n)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = C.stream_host(host, L, L, n)
-        dt = time.perf_counter() - t0
-        bytes_step = n * L
-        value = bytes_step * args.steps / dt / 2**30
-        if rank == 0:
-            print(json.dumps({"metric": "GiB/s pinned-host streamed CRC32C (H2D->CRC->D2H), 16 KiB",
-                              "value": round(value, 3), "unit": "GiB/s", "n_gpus": 1,
-                              "steps": args.steps, "warmup": args.warmup,
-                              "ms_per_step": round(dt / args.steps * 1e3, 3),
-                              "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                              "dtype": "u8", "data": "synthetic (splitmix64)",
-                              "config": {"workload": wl["workload"], "n_blocks": n,
-                                         "block_bytes": L}}))
-        return 0
-
-    # ---- device-resident batch -------------------------------------------
+    seed = cfg
     if wl["kind"] == "strided":
         L = wl["block_bytes"]
         total = n * L
-        buf = torch.empty(total, dtype=torch.uint8, device=dev)
-        C.fill_splitmix64(buf, seed, first_word=rank * (total // 8))
-        out = torch.empty(n, dtype=torch.int32, device=dev)
+        buf = torch.empty(total, dtype=torch.uint8, device=ctx.dev)
+        # rank r's shard of the global batch: words [r*total/8, (r+1)*total/8)
+        C.fill_splitmix64(buf, seed, first_word=ctx.rank * (total // 8))
+        out = torch.empty(n, dtype=torch.int32, device=ctx.dev)
 
         def step():
             C.batch_strided(buf, L, L, n, out=out, stream=stream)
-        lens_np = None
-        offs_np = None
+        lens_np = offs_np = None
         bytes_step = total
+        dispatch = C.describe(n, L, L, variable=False)
     else:
         offs_np, lens_np, total = config3_layout(n, seed)
-        buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
-        C.fill_splitmix64(buf, seed, first_word=rank * (total // 8))
-        offs = torch.from_numpy(offs_np.view(np.int64)).to(dev)
-        lens = torch.from_numpy(lens_np.view(np.int32)).to(dev)
-        out = torch.empty(n, dtype=torch.int32, device=dev)
-
+        buf = torch.empty(total + 64, dtype=torch.uint8, device=ctx.dev)
+        C.fill_splitmix64(buf, seed, first_word=ctx.rank * (total // 8))
+        offs = torch.from_numpy(offs_np.view(np.int64)).to(ctx.dev)
+        lens = torch.from_numpy(lens_np.view(np.int32)).to(ctx.dev)
+        out = torch.empty(n, dtype=torch.int32, device=ctx.dev)
         # config 3 is LevelDB's block_size sweep (mean ~28 KiB): the caller
         # knows its block_size and passes the scheduling hint (results are
         # identical without it; include/nova_crc32c.h)
@@ -215,15 +259,26 @@ def main() -> int:
         def step():
             C.batch(buf, offs, lens, flags=hint, out=out, stream=stream)
         bytes_step = int(lens_np.astype(np.uint64).sum())
+        dispatch = C.describe(n, 0, 0, variable=True, large=True)
 
+    # settle: back-to-back launches for >= settle_ms (time-based), then warmup
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t_s = time.perf_counter()
+    settle_launches = 0
+    while (time.perf_counter() - t_s) * 1e3 < args.settle_ms:
+        for _ in range(8):
+            step()
+        settle_launches += 8
+        torch.cuda.synchronize()
+    settle_ms = (time.perf_counter() - t_s) * 1e3
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
+    ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -231,17 +286,15 @@ def main() -> int:
         step()
         ev[i][1].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    ctx.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dts = ctx.all_gather_f64(dt)
+    dt_max = max(dts)
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
     avg_launch_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    rank_kernel_ms = ctx.all_gather_f64(avg_launch_s * 1e3)
 
-    # ---- sample verification against the CPU oracle (outside the timed region)
+    # sample verification against the CPU oracle (outside the timed region)
     verified = None
     if args.verify:
         from tests.oracle_lib import load_oracle
@@ -251,72 +304,213 @@ def main() -> int:
         ok = True
         for i in idx:
             if wl["kind"] == "strided":
-                o, l = int(i) * L, L
+                o, ln = int(i) * L, L
             else:
-                o, l = int(offs_np[i]), int(lens_np[i])
-            blk = buf[o:o + l].cpu().numpy().tobytes()
+                o, ln = int(offs_np[i]), int(lens_np[i])
+            blk = buf[o:o + ln].cpu().numpy().tobytes()
             ok &= orc.value(blk) == int(got[i])
-        if world > 1:  # every rank learns whether any shard failed (no rank left in a barrier)
-            f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-            dist.all_reduce(f, op=dist.ReduceOp.MIN)
-            ok = bool(f.item())
-        verified = bool(ok)
-        if not ok:
-            print(json.dumps({"error": "GPU CRC mismatch vs oracle", "rank": rank}), file=sys.stderr)
-            if world > 1:
-                dist.destroy_process_group()
-            return 3
+        oks = ctx.all_gather_f64(1.0 if ok else 0.0)  # every rank learns whether any shard failed
+        verified = bool(min(oks) > 0)
 
-    value = world * bytes_step * args.steps / dt / 2**30
     achieved = bytes_step / avg_launch_s / 1e9
-    if wl["kind"] == "strided":
-        dispatch = C.describe(n, L, L, variable=False)
-    else:
-        dispatch = C.describe(n, 0, 0, variable=True, large=True)
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_config{args.config}.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            traffic = pmc.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4)}
+    roof.update(traffic_of(cfg, dispatch))
+    roof.update({"kernel_ms_avg": round(avg_launch_s * 1e3, 4),
+                 "kernel_ms_min": round(min(kernel_ms), 4),
+                 "kernel_ms_median": round(sorted(kernel_ms)[len(kernel_ms) // 2], 4)})
+    if ctx.world > 1:
+        roof["kernel_ms_avg_per_rank"] = [round(x, 4) for x in rank_kernel_ms]
+    del buf, out
+    torch.cuda.empty_cache()
+    return {
+        "config": cfg,
+        "value": round(ctx.world * bytes_step * args.steps / dt_max / 2**30, 2),
+        "unit": "GiB/s",
+        "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+        "workload": {"workload": wl["workload"], "n_blocks": n, "bytes_per_gpu": bytes_step,
+                     "dispatch": dispatch},
+        "settle": {"settle_ms": round(settle_ms, 1), "settle_launches": settle_launches},
+        "roofline": roof,
+        "verified_sample": verified,
+    }
 
+
+def traffic_of(cfg: int, dispatch: dict) -> dict:
+    """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE
+    pass (tools/pmc.sh -> profiles/pmc_config<N>.json); PMC counters cannot be
+    read from inside the timed run.  Used only when that pass profiled the
+    kernel this run dispatches."""
+    path = os.path.join("profiles", f"pmc_config{cfg}.json")
+    try:
+        with open(os.path.join(ROOT, path)) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return {"traffic": None, "traffic_source": None}
+    k = pmc.get("kernel")
+    if k and k != dispatch.get("kernel"):
+        return {"traffic": None, "traffic_source": f"{path} profiled {k}, not this dispatch"}
+    src = f"{path} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate pass"
+    if pmc.get("commit"):
+        src += f", tree {pmc['commit']}"
+    return {"traffic": pmc.get("hbm_bytes_per_launch"), "traffic_source": src + ")"}
+
+
+def run_host_config(args, ctx: Ctx) -> int:
+    import torch
+    from novalsm_amd import crc32c as C
+    wl = workload(5)
+    L, n = wl["block_bytes"], wl["n_blocks"]
+    host = torch.empty(n * L, dtype=torch.uint8).pin_memory()
+    tmp = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
+    C.fill_splitmix64(tmp, 5, first_word=ctx.rank * (n * L // 8))
+    host.copy_(tmp.cpu())
+    del tmp
+    for _ in range(max(1, args.warmup)):
+        C.stream_host(host, L, L, n)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        C.stream_host(host, L, L, n)
+    ctx.barrier()
+    dt = max(ctx.all_gather_f64(time.perf_counter() - t0))
+    value = ctx.world * n * L * args.steps / dt / 2**30
+    if ctx.rank == 0:
+        print(json.dumps({"metric": "GiB/s pinned-host streamed CRC32C (H2D->CRC->D2H), 16 KiB",
+                          "value": round(value, 3), "unit": "GiB/s", "n_gpus": ctx.world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(dt / args.steps * 1e3, 3),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                          "dtype": "u8", "data": "synthetic (splitmix64)",
+                          "config": {"workload": wl["workload"], "n_blocks": n,
+                                     "block_bytes": L}}), flush=True)
+    return 0
+
+
+def harness_check(args, world: int, rank: int) -> int:
+    """--harness-check: the launcher and collective plumbing on CPU (gloo), no
+    GPU and no measurement.  Each rank checksums a small buffer with the
+    product's host Extend and reports; rank 0 prints the world size gloo saw."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    from novalsm_amd import crc32c as C
+    data = bytes(range(256)) * 16
+    crc = C.Value(data)
+    import torch
+    t = torch.tensor([float(rank)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"harness_check": True, "n_gpus": world, "backend": "gloo",
+                          "max_rank": int(t.item()), "crc": f"0x{crc:08x}"}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--secondary", default="auto",
+                    help="configs measured after the primary one in the same run "
+                         "(comma list, 'none'; auto: 3,4 when the primary is 2)")
+    ap.add_argument("--settle-ms", type=float, default=400.0,
+                    help="time-based settle of back-to-back launches before the warmup")
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per unit override (tuning)")
+    ap.add_argument("--seg", type=int, default=0, help="segment bytes override (tuning)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0)
+    ap.add_argument("--verify", type=int, default=1, help="sample-verify vs the oracle")
+    ap.add_argument("--harness-check", action="store_true",
+                    help="CPU-only check of the rank launcher (gloo), no measurement")
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.harness_check:
+        return harness_check(args, world, rank)
+
+    import torch
+    import torch.distributed as dist
+    from novalsm_amd import crc32c as C
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()  # the world RCCL reports
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    C.load()
+    if args.lanes or args.seg:
+        C.set_tuning(args.lanes, args.seg)
+    if C.load().nova_device_init() != 0:
+        raise SystemExit("nova_device_init failed")
+    ctx = Ctx(world, rank, dev, dist)
+
+    if args.config == 5:
+        rc = run_host_config(args, ctx)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return rc
+
+    prim = run_device_config(args.config, args, ctx)
+    if args.secondary == "auto":
+        sec_cfgs = [3, 4] if args.config == 2 else []
+    elif args.secondary in ("", "none"):
+        sec_cfgs = []
+    else:
+        sec_cfgs = [int(x) for x in args.secondary.split(",") if int(x) != args.config]
+    secondary = []
+    for c in sec_cfgs:
+        if c == 5:
+            continue
+        r = run_device_config(c, args, ctx)
+        secondary.append({"metric": METRIC, **r})
+
+    rc = 0
+    if prim["verified_sample"] is False or any(s["verified_sample"] is False for s in secondary):
+        rc = 3
+        if rank == 0:
+            print(json.dumps({"error": "GPU CRC mismatch vs oracle"}), file=sys.stderr)
     if rank == 0:
         res = {
             "metric": METRIC,
-            "value": round(value, 2),
+            "value": prim["value"],
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "ms_per_step": prim["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 generated on device)",
-            "config": {"workload": wl["workload"], "n_blocks": n, "bytes_per_gpu": bytes_step,
-                       "parallelism": f"shard{world}" if world > 1 else "single",
-                       "dispatch": dispatch},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "kernel_ms_avg": round(avg_launch_s * 1e3, 4),
-                         "kernel_ms_min": round(min(kernel_ms), 4),
-                         "kernel_ms_median": round(sorted(kernel_ms)[len(kernel_ms) // 2], 4)},
-            "verified_sample": verified,
+            "config": {**prim["workload"],
+                       "parallelism": f"shard{world}" if world > 1 else "single"},
+            "settle": prim["settle"],
+            "roofline": prim["roofline"],
+            "verified_sample": prim["verified_sample"],
+            "secondary": secondary,
         }
         if not args.no_cpu_baseline and world == 1:
             # rank 0 at N=1 only: the CPU sample is the same at every N
-            th = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            res["cpu_baseline"] = cpu_baseline(th, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

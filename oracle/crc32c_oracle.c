@@ -224,6 +224,26 @@ int oracle_log_verify(const uint8_t *rec) {
   return oracle_unmask(read_le32(rec)) == oracle_value(rec + 6, 1 + len);
 }
 
+/* db/log_reader.cc:225-262 ReadPhysicalRecord's per-record checks, in order,
+ * for the record whose header starts at buf+off in a log image of buf_len
+ * bytes that begins on a 32 KiB log-block boundary (db/log_format.h:27,
+ * kBlockSize): the record must end inside its log block and the image
+ * ("bad record length", :230-240), a kZeroType record of length 0 is skipped
+ * unreported (:243-249), else the CRC is checked ("checksum mismatch",
+ * :251-262).  Returns 1 ok, 0 checksum mismatch, 2 bad record length,
+ * 3 zero record. */
+int oracle_log_check(const uint8_t *buf, uint64_t buf_len, uint64_t off) {
+  const uint64_t kBlock = 32768, kHeader = 7;
+  uint64_t end = (off / kBlock + 1) * kBlock;
+  if (end > buf_len) end = buf_len;
+  if (off + kHeader > end) return 2;
+  const uint8_t *h = buf + off;
+  uint32_t len = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
+  if (off + kHeader + len > end) return 2;
+  if (h[6] == 0 && len == 0) return 3;
+  return oracle_unmask(read_le32(h)) == oracle_value(h + 6, 1 + len) ? 1 : 0;
+}
+
 /* ltc/stoc_file_client_impl.cpp:340-348: parity[i] = XOR over fragments of
  * backing_mem_[fragment.offset() + i] for i < parity_block_size_ (every
  * fragment contributes parity_len bytes from its start). */
@@ -274,6 +294,60 @@ int oracle_batch_strided_mt(const uint8_t *base, uint64_t stride, uint32_t len,
   }
   for (int t = 0; t < started; t++) pthread_join(tid[t], 0);
   return started;
+}
+
+/* Multi-threaded variable-length batch: the checker for full-size batches
+ * (every block of BASELINE config 3), same semantics as oracle_batch. */
+struct vshard_arg {
+  const uint8_t *base;
+  const uint64_t *offsets;
+  const uint32_t *lengths, *init;
+  uint32_t *out;
+  size_t lo, hi;
+  uint32_t flags;
+};
+
+static void *vshard_main(void *p) {
+  struct vshard_arg *a = (struct vshard_arg *)p;
+  for (size_t i = a->lo; i < a->hi; i++) {
+    uint32_t init = a->init ? a->init[i] : 0u;
+    a->out[i] = finish(oracle_extend(init, a->base + a->offsets[i], a->lengths[i]), a->flags);
+  }
+  return 0;
+}
+
+int oracle_batch_mt(const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths,
+                    const uint32_t *init_or_null, uint32_t *out, size_t n_blocks, uint32_t flags,
+                    int threads) {
+  ensure_tables();
+  if (threads < 1) threads = 1;
+  if (threads > 512) threads = 512;
+  pthread_t tid[512];
+  struct vshard_arg args[512];
+  size_t per = (n_blocks + threads - 1) / threads;
+  int started = 0;
+  for (int t = 0; t < threads; t++) {
+    size_t lo = t * per, hi = lo + per;
+    if (lo > n_blocks) lo = n_blocks;
+    if (hi > n_blocks) hi = n_blocks;
+    args[t] = (struct vshard_arg){base, offsets, lengths, init_or_null, out, lo, hi, flags};
+    if (pthread_create(&tid[t], 0, vshard_main, &args[t]) != 0) break;
+    started++;
+  }
+  /* a thread that failed to start leaves its shard to this thread */
+  for (int t = started; t < threads; t++) vshard_main(&args[t]);
+  for (int t = 0; t < started; t++) pthread_join(tid[t], 0);
+  return started;
+}
+
+/* benchmarks/db_bench.cc:635-652 Crc32c(): Value() over the same 4 KiB of 'x'
+ * until total_bytes (500 MiB there) are checksummed, on the calling thread. */
+uint32_t oracle_dbbench_crc32c(int64_t total_bytes) {
+  uint8_t data[4096];
+  memset(data, 'x', sizeof(data));
+  uint32_t crc = 0;
+  for (int64_t bytes = 0; bytes < total_bytes; bytes += 4096) crc = oracle_value(data, 4096);
+  return crc;
 }
 
 /* splitmix64 counter form: word k of the stream seeded with `seed` is

@@ -9,6 +9,7 @@
 // contiguous shards (BASELINE.md CPU plan).
 #include <cstddef>
 #include <cstdint>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -45,6 +46,16 @@ int ref_batch_strided_mt(const char* base, uint64_t stride, uint32_t len, size_t
   }
   for (auto& th : pool) th.join();
   return threads;
+}
+
+// benchmarks/db_bench.cc:635-652 Crc32c(): the reference's own throughput
+// method -- Value() over one 4 KiB string of 'x' until total_bytes, 1 thread.
+uint32_t ref_dbbench_crc32c(int64_t total_bytes) {
+  const std::string data(4096, 'x');
+  uint32_t crc = 0;
+  for (int64_t bytes = 0; bytes < total_bytes; bytes += 4096)
+    crc = leveldb::crc32c::Value(data.data(), data.size());
+  return crc;
 }
 
 }  // extern "C"

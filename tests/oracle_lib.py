@@ -57,6 +57,32 @@ class Oracle:
         lib.oracle_xor_parity.argtypes = [vp, vp, sz, sz, vp]
         lib.oracle_tables.restype = None
         lib.oracle_tables.argtypes = [vp, vp]
+        lib.oracle_batch_mt.restype = ctypes.c_int
+        lib.oracle_batch_mt.argtypes = [vp, vp, vp, vp, vp, sz, u32, ctypes.c_int]
+        lib.oracle_log_check.restype = ctypes.c_int
+        lib.oracle_log_check.argtypes = [vp, u64, u64]
+        lib.oracle_dbbench_crc32c.restype = u32
+        lib.oracle_dbbench_crc32c.argtypes = [ctypes.c_int64]
+
+    def batch_mt(self, buf: np.ndarray, offsets, lengths, init=None, flags: int = 0,
+                 threads: int = 16) -> np.ndarray:
+        """oracle_batch on `threads` host threads (full-size batches)."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        ini = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
+        out = np.empty(len(off), dtype=np.uint32)
+        self.lib.oracle_batch_mt(buf.ctypes.data, off.ctypes.data, ln.ctypes.data,
+                                 None if ini is None else ini.ctypes.data, out.ctypes.data,
+                                 len(off), flags, threads)
+        return out
+
+    def log_check(self, buf: np.ndarray, rec_offsets, buf_len=None) -> np.ndarray:
+        """db/log_reader.cc:225-262 per record: 1 ok, 0 checksum mismatch,
+        2 bad record length, 3 zero record (skipped)."""
+        n = buf.size if buf_len is None else buf_len
+        return np.array([self.lib.oracle_log_check(buf.ctypes.data, n, int(o))
+                         for o in rec_offsets], dtype=np.uint8)
 
     def extend(self, init: int, data: bytes) -> int:
         return self.lib.oracle_extend(init & 0xFFFFFFFF, data, len(data))
