@@ -77,12 +77,19 @@ uint32_t nova_crc32c_unmask(uint32_t masked_crc);
 uint32_t nova_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
 /* ---- plug-in hook: port::AcceleratedCRC32C, port/port_stdcxx.h:179-189 ---
- * Same contract: returns Extend(crc, buf, size) or 0 meaning "cannot
- * accelerate" (no device).  `buf` is HOST memory; the buffer is copied to the
- * GPU, checksummed by the HIP kernels and the result copied back, so it is
- * worth it only for large buffers.  Passes the reference's self-test
- * ("TestCRCBuffer" -> 0xdcbc59fa, util/crc32c.cc:477-485). */
+ * Same contract: returns Extend(crc, buf, size).  Passes the reference's
+ * self-test ("TestCRCBuffer" -> 0xdcbc59fa, util/crc32c.cc:477-485), after
+ * which the reference sends EVERY Extend() here (util/crc32c.cc:487-491), so
+ * the hook never returns a wrong CRC:
+ *   - buffers below NOVA_HOOK_MIN_BYTES (env, default 1 MiB) run on the host
+ *     (the library's SSE4.2 Extend; one 4 KiB block is ~1 us there);
+ *   - larger ones are copied to the GPU (one pooled stream and staging buffer
+ *     per calling thread), checksummed by the HIP kernels and folded on the
+ *     host; ANY device failure (no device, allocation beyond
+ *     NOVA_HOOK_MAX_STAGING, a HIP error) falls back to the host Extend.
+ * `buf` is HOST memory.  nova_port_stats counts the three outcomes. */
 uint32_t nova_port_accelerated_crc32c(uint32_t crc, const char* buf, size_t size);
+void nova_port_stats(uint64_t* host_calls, uint64_t* device_calls, uint64_t* fallback_calls);
 
 /* ---- device batches ------------------------------------------------------
  * Variable-length: block i is base[offsets[i] .. offsets[i]+lengths[i]).
@@ -121,16 +128,30 @@ int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const u
                                void* stream);
 
 /* ---- MANIFEST / write-ahead log records ----------
- * record_offsets[i] points at a log record header [LE32 masked crc][LE16
- * length][type] (db/log_format.h:27-30) followed by `length` payload bytes.
+ * buf holds buf_len bytes of a log file image starting at a 32 KiB log-block
+ * boundary (db/log_format.h:27, kBlockSize).  record_offsets[i] (relative to
+ * buf) points at a physical record header [LE32 masked crc][LE16 length][type]
+ * (db/log_format.h:27-30) followed by `length` payload bytes.
+ * Bounds, as log::Reader::ReadPhysicalRecord checks them (db/log_reader.cc:
+ * 228-247): a record whose header or payload runs past its 32 KiB block (or
+ * past buf_len) is never read.
  * Write: header crc = Mask(Extend(type_crc[type], payload, length)) --
  * db/log_writer.cc:99-114 (type_crc[t] = Value(&t, 1), :16-21), computed as
- * Value(header+6, 1+length).  Verify: ok_out[i] = Unmask(stored) ==
- * Value(header+6, 1+length) -- db/log_reader.cc:251-262 ("checksum mismatch"). */
-int nova_log_write_crcs(void* buf, const uint64_t* record_offsets, size_t n_records,
-                        void* stream);
-int nova_log_verify_records(const void* buf, const uint64_t* record_offsets, size_t n_records,
-                            uint8_t* ok_out, uint32_t* n_bad_out, void* stream);
+ * Value(header+6, 1+length).  Out-of-bounds records are skipped (nothing is
+ * written for them).
+ * Verify: status_out[i] is one of NOVA_LOG_*; *n_bad_out (device u32, zeroed
+ * by the caller, may be NULL) counts the records the reader reports as
+ * corruption (CHECKSUM_MISMATCH, BAD_LENGTH). */
+#define NOVA_LOG_CHECKSUM_MISMATCH 0 /* :251-262 "checksum mismatch" */
+#define NOVA_LOG_OK 1                /* Unmask(stored) == Value(header+6, 1+length) */
+#define NOVA_LOG_BAD_LENGTH 2        /* :228-235 "bad record length" (not read) */
+#define NOVA_LOG_ZERO_RECORD 3       /* :241-247 type 0, length 0: skipped, not reported */
+#define NOVA_LOG_TRUNCATED 4         /* :236-239 cut by the end of the file: EOF, not reported */
+int nova_log_write_crcs(void* buf, size_t buf_len, const uint64_t* record_offsets,
+                        size_t n_records, void* stream);
+int nova_log_verify_records(const void* buf, size_t buf_len, const uint64_t* record_offsets,
+                            size_t n_records, uint8_t* status_out, uint32_t* n_bad_out,
+                            void* stream);
 
 /* ---- XOR parity block ------------------------------
  * out[i] = XOR over fragments f of base[frag_offsets[f] + i], i < parity_len
@@ -140,16 +161,38 @@ int nova_log_verify_records(const void* buf, const uint64_t* record_offsets, siz
 int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_frags,
                     size_t parity_len, void* out, void* stream);
 
-/* ---- host-resident streamed path (BASELINE config 5) --------------------
+/* ---- host-resident streamed paths ---------------------------------------
  * Blocks live in HOST memory (pinned or pageable; the analogue of NovaLSM's
  * RDMA-registered backing_mem_, ltc/stoc_file_client_impl.cpp:43-45).  The
- * batch is cut into chunks of chunk_blocks blocks that flow H2D -> CRC -> D2H
- * over n_streams HIP streams; host_out receives n_blocks CRCs.  Synchronous.
- * If host_base is not pinned it is registered (hipHostRegister) for the
- * duration of the call. */
+ * batch is cut into chunks that flow H2D -> kernel -> D2H over n_streams
+ * pooled HIP streams (1..8); descriptors and outputs are HOST arrays.
+ * Synchronous.  Pageable memory is registered (hipHostRegister) for the
+ * duration of the call.
+ *
+ * BASELINE config 5, fixed stride: chunks of chunk_blocks blocks. */
 int nova_crc32c_stream_host(const void* host_base, uint64_t stride, uint32_t len,
                             size_t n_blocks, uint32_t* host_out, uint32_t flags,
                             size_t chunk_blocks, int n_streams);
+/* Variable-length, any order: a chunk is a run of consecutive descriptors
+ * whose blocks span <= chunk_bytes (0: 64 MiB; a larger block gets its own
+ * chunk), and copies that span -- so descriptors in address order (an
+ * SSTable's blocks) copy each byte once.  Same results as nova_crc32c_batch. */
+int nova_crc32c_batch_host(const void* host_base, const uint64_t* offsets, const uint32_t* lengths,
+                           const uint32_t* init_or_null, uint32_t* out_crc, size_t n_blocks,
+                           uint32_t flags, size_t chunk_bytes, int n_streams);
+/* Trailers into a host SSTable image (StoCWritableFileClient::Format over
+ * backing_mem_, ltc/stoc_file_client_impl.cpp:183-377): the GPU computes
+ * Mask(Extend(Value(block), type)), the host stores the 5 bytes.  Same bytes as
+ * nova_sstable_write_trailers. */
+int nova_sstable_write_trailers_host(void* host_buf, const uint64_t* offsets, const uint32_t* sizes,
+                                     size_t n_blocks, uint32_t flags, size_t chunk_bytes,
+                                     int n_streams);
+/* Read-verify of a host SSTable image (the ReadAll slab,
+ * ltc/stoc_file_client_impl.cpp:843-882): ok_out[i] and *n_bad_out are HOST
+ * outputs with nova_sstable_verify_blocks' meaning. */
+int nova_sstable_verify_blocks_host(const void* host_buf, const uint64_t* offsets,
+                                    const uint32_t* sizes, size_t n_blocks, uint8_t* ok_out,
+                                    uint32_t* n_bad_out, size_t chunk_bytes, int n_streams);
 
 /* ---- utilities ----------------------------------------------------------- */
 /* Fill nbytes of device memory with the splitmix64 counter stream
@@ -158,6 +201,12 @@ int nova_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t first
                          void* stream);
 /* Build + upload the tables for the current device (optional: done lazily). */
 int nova_device_init(void);
+/* A caller stream's claim-counter slot (16 KiB of device memory, created on the
+ * stream's first batch launch) lives until the stream is released: call this
+ * before hipStreamDestroy on a stream that ran batches.  It waits for the
+ * stream's work.  nova_stream_slots() counts live slots (diagnostics). */
+int nova_stream_release(void* stream);
+size_t nova_stream_slots(void);
 /* Lanes per block ("G") and segment bytes the dispatcher would pick for an
  * aligned fixed-stride batch; returns 1 for the streaming kernel, 0 for the
  * units kernel, 2 for the flat kernel, 3 for the rounds kernel.  nova_crc32c_describe writes a JSON object naming the kernel
@@ -166,16 +215,22 @@ int nova_device_init(void);
 int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_unit,
                      uint32_t* seg_bytes);
 int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int variable, char* buf,
-                         size_t buflen);
+                         size_t buflen); /* variable 3: a batch of log records */
 const char* nova_crc32c_kernel_name(int lanes_per_unit);
 /* Overrides for tuning/tests: lanes per unit (0 = auto) and segment size
- * (0 = auto).  Process-wide. */
+ * (0 = auto).  Per calling thread: other threads keep the automatic plan. */
 void nova_crc32c_set_tuning(int lanes_per_unit, uint32_t seg_bytes);
 const char* nova_error_string(int err);
+/* ABI version: bump on any signature change (2: log entry points take buf_len). */
+int nova_crc32c_abi_version(void);
 
-/* ---- diagnostics (profiling only; not part of the drop-in surface) ------
+/* ---- diagnostics: libnova_crc32c_diag.so ONLY ---------------------------
+ * The product library does not export anything below.  The diagnostics build
+ * (same sources, -DNOVA_DIAG) adds timing ablations, alternative schedules and
+ * read-ceiling probes for tools/ and the tuning tests.  All knobs are per
+ * calling thread.
  * variant: 0 production, 1 ablation (no table lookups -- WRONG CRCs, timing
- * only), 2 default-policy (cached) data loads instead of nt.  Process-wide. */
+ * only), 2 default-policy (cached) data loads instead of nt. */
 void nova_diag_set_variant(int variant);
 /* variant 4: the streaming kernel writes {begin, end, XCC id} per wave
  * (s_memrealtime ticks, 100 MHz) to dev_stamps[3*wave ...]. */
@@ -213,8 +268,6 @@ void nova_diag_set_chunk_blocks(int blocks);
  * ceiling for the roofline discussion. */
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream);
-/* ABI version: bump on any signature change. */
-int nova_crc32c_abi_version(void);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -1,8 +1,14 @@
-"""Build the in-tree native library libnova_crc32c.so for gfx950.
+"""Build the in-tree native libraries for gfx950.
 
 Sources: novalsm_amd/csrc/{crc32c_device.hip, crc32c_stream.cpp, crc32c_host.cpp}.
-Output:  novalsm_amd/lib/libnova_crc32c.so (git-ignored, travels to the GPU box).
-hipcc cross-compiles gfx950 code objects without a GPU.
+Outputs (git-ignored, travel to the GPU box):
+  novalsm_amd/lib/libnova_crc32c.so       the product: production kernels only
+  novalsm_amd/lib/libnova_crc32c_diag.so  the same sources with -DNOVA_DIAG: timing
+      ablations (some compute WRONG CRCs on purpose), the flat kernel, the sort
+      pre-pass, read-ceiling probes and the nova_diag_* knobs -- for tools/ and
+      the tuning-variant tests, never for callers
+hipcc cross-compiles gfx950 code objects without a GPU; the objects compile in
+parallel.
 """
 from __future__ import annotations
 
@@ -16,6 +22,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libnova_crc32c.so")
+DIAG_LIB = os.path.join(LIB_DIR, "libnova_crc32c_diag.so")
 ARCH = os.environ.get("NOVA_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["crc32c_device.hip", "crc32c_stream.cpp", "crc32c_host.cpp"]
@@ -30,36 +37,57 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP extension cannot be built")
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _stale(lib: str) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [__file__]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False, extra: list[str] | None = None) -> str:
-    if not force and not _stale():
+def _compile_cmd(cc: str, src: str, obj: str, defines: list[str], extra: list[str] | None):
+    cmd = [cc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall",
+           "-I", os.path.join(ROOT, "include")] + defines + [
+           "-c", os.path.join(CSRC, src), "-o", obj]
+    if src.endswith(".cpp"):
+        cmd[1:1] = ["-x", "hip"] if "stream" in src else ["-x", "c++"]
+    return cmd + (extra or [])
+
+
+def build(force: bool = False, verbose: bool = False, extra: list[str] | None = None,
+          diag: bool = True) -> str:
+    """Build the product library (and, with diag=True, the diagnostics one)."""
+    want = [LIB] + ([DIAG_LIB] if diag else [])
+    if not force and not any(_stale(x) for x in want):
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
-    objs = []
     cc = hipcc()
-    for src in SOURCES:
+    jobs = {}  # obj -> cmd
+    shared = []
+    for src in SOURCES[1:]:
         obj = os.path.join(LIB_DIR, os.path.splitext(src)[0] + ".o")
-        cmd = [cc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall",
-               "-I", os.path.join(ROOT, "include"), "-c", os.path.join(CSRC, src), "-o", obj]
-        if src.endswith(".cpp"):
-            cmd[1:1] = ["-x", "hip"] if "stream" in src else ["-x", "c++"]
-        cmd += extra or []
+        jobs[obj] = _compile_cmd(cc, src, obj, [], extra)
+        shared.append(obj)
+    dev_obj = os.path.join(LIB_DIR, "crc32c_device.o")
+    jobs[dev_obj] = _compile_cmd(cc, SOURCES[0], dev_obj, [], extra)
+    diag_obj = os.path.join(LIB_DIR, "crc32c_device_diag.o")
+    if diag:
+        jobs[diag_obj] = _compile_cmd(cc, SOURCES[0], diag_obj, ["-DNOVA_DIAG"], extra)
+    procs = []
+    for obj, cmd in jobs.items():
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-        objs.append(obj)
-    tmp = LIB + ".tmp"
-    subprocess.run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +
-                   ["-lpthread"], check=True)
-    os.replace(tmp, LIB)
-    for o in objs:
+        procs.append((cmd, subprocess.Popen(cmd)))
+    failed = [cmd for cmd, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    links = [(LIB, [dev_obj] + shared)] + ([(DIAG_LIB, [diag_obj] + shared)] if diag else [])
+    for lib, objs in links:
+        tmp = lib + ".tmp"
+        subprocess.run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +
+                       ["-lpthread"], check=True)
+        os.replace(tmp, lib)
+    for o in jobs:
         os.remove(o)
     return LIB
 

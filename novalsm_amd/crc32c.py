@@ -11,6 +11,7 @@ no CPU fallback on this path.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import Optional
@@ -35,14 +36,85 @@ class NovaError(RuntimeError):
 
 
 _lib: Optional[ctypes.CDLL] = None
+_diag: Optional[ctypes.CDLL] = None
+_active_diag = False  # wrappers route to the diagnostics library (diagnostics())
+
+# C signatures (include/nova_crc32c.h).  The product library exports _SIG; the
+# diagnostics build (libnova_crc32c_diag.so) exports _SIG and _DIAG_SIG.
+_u32, _u64, _sz, _vp, _i32 = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p,
+                              ctypes.c_int)
+_pu64 = ctypes.POINTER(ctypes.c_uint64)
+_SIG = {
+    "nova_crc32c_extend": (_u32, [_u32, ctypes.c_char_p, _sz]),
+    "nova_crc32c_value": (_u32, [ctypes.c_char_p, _sz]),
+    "nova_crc32c_mask": (_u32, [_u32]),
+    "nova_crc32c_unmask": (_u32, [_u32]),
+    "nova_crc32c_combine": (_u32, [_u32, _u32, _u64]),
+    "nova_port_accelerated_crc32c": (_u32, [_u32, ctypes.c_char_p, _sz]),
+    "nova_port_stats": (None, [_pu64, _pu64, _pu64]),
+    "nova_crc32c_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _vp]),
+    "nova_crc32c_batch_strided": (_i32, [_vp, _u64, _u32, _sz, _vp, _vp, _u32, _vp]),
+    "nova_sstable_write_trailers": (_i32, [_vp, _vp, _vp, _sz, _u32, _vp]),
+    "nova_sstable_verify_blocks": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "nova_crc32c_stream_host": (_i32, [_vp, _u64, _u32, _sz, _vp, _u32, _sz, _i32]),
+    "nova_crc32c_batch_host": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _sz, _i32]),
+    "nova_sstable_write_trailers_host": (_i32, [_vp, _vp, _vp, _sz, _u32, _sz, _i32]),
+    "nova_sstable_verify_blocks_host": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _sz, _i32]),
+    "nova_log_write_crcs": (_i32, [_vp, _sz, _vp, _sz, _vp]),
+    "nova_log_verify_records": (_i32, [_vp, _sz, _vp, _sz, _vp, _vp, _vp]),
+    "nova_xor_parity": (_i32, [_vp, _vp, _sz, _sz, _vp, _vp]),
+    "nova_fill_splitmix64": (_i32, [_vp, _sz, _u64, _u64, _vp]),
+    "nova_device_init": (_i32, []),
+    "nova_stream_release": (_i32, [_vp]),
+    "nova_stream_slots": (_sz, []),
+    "nova_crc32c_plan": (_i32, [_sz, _u64, ctypes.POINTER(_i32), ctypes.POINTER(_u32)]),
+    "nova_crc32c_kernel_name": (ctypes.c_char_p, [_i32]),
+    "nova_crc32c_describe": (_i32, [_sz, _u64, _u64, _i32, ctypes.c_char_p, _sz]),
+    "nova_crc32c_set_tuning": (None, [_i32, _u32]),
+    "nova_error_string": (ctypes.c_char_p, [_i32]),
+    "nova_crc32c_abi_version": (_i32, []),
+}
+_DIAG_SIG = {
+    "nova_diag_set_variant": (None, [_i32]),
+    "nova_diag_set_stamps": (None, [_vp]),
+    "nova_diag_set_static_pct": (None, [_i32]),
+    "nova_diag_set_blocks_per_group": (None, [_i32]),
+    "nova_diag_set_chunk_blocks": (None, [_i32]),
+    "nova_diag_set_stream_waves": (None, [_i32]),
+    "nova_diag_set_variable_kernel": (None, [_i32]),
+    "nova_diag_set_parity_variant": (None, [_i32]),
+    "nova_diag_set_rounds_sort": (None, [_i32]),
+    "nova_diag_set_trailer_single_pass": (None, [_i32]),
+    "nova_diag_read_stream": (_i32, [_vp, _sz, _vp, _i32, _vp]),
+    "nova_diag_read_ceiling": (_i32, [_vp, _sz, _vp, _i32, _i32, _vp]),
+}
+ABI_VERSION = 2
+
+# log verify status codes (include/nova_crc32c.h, db/log_reader.cc:228-262)
+LOG_CHECKSUM_MISMATCH = 0
+LOG_OK = 1
+LOG_BAD_LENGTH = 2
+LOG_ZERO_RECORD = 3
+LOG_TRUNCATED = 4
 
 
 def lib_path() -> str:
     return _build.LIB
 
 
+def _open(path: str, sig: dict) -> ctypes.CDLL:
+    L = ctypes.CDLL(path)
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.nova_crc32c_abi_version() != ABI_VERSION:
+        raise ImportError(f"{path}: ABI {L.nova_crc32c_abi_version()} != {ABI_VERSION} (rebuild)")
+    return L
+
+
 def load(build_if_missing: bool = False) -> ctypes.CDLL:
-    """Load the in-tree native library (never a site-packages copy)."""
+    """The in-tree product library (never a site-packages copy)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -51,53 +123,61 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
         if not build_if_missing:
             raise ImportError(f"native library missing: {path} (run __graft_entry__.build())")
         _build.build()
-    L = ctypes.CDLL(path)
-    u32, u64, sz, vp, i32 = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p,
-                             ctypes.c_int)
-    sig = {
-        "nova_crc32c_extend": (u32, [u32, ctypes.c_char_p, sz]),
-        "nova_crc32c_value": (u32, [ctypes.c_char_p, sz]),
-        "nova_crc32c_mask": (u32, [u32]),
-        "nova_crc32c_unmask": (u32, [u32]),
-        "nova_crc32c_combine": (u32, [u32, u32, u64]),
-        "nova_port_accelerated_crc32c": (u32, [u32, ctypes.c_char_p, sz]),
-        "nova_crc32c_batch": (i32, [vp, vp, vp, vp, vp, sz, u32, vp]),
-        "nova_crc32c_batch_strided": (i32, [vp, u64, u32, sz, vp, vp, u32, vp]),
-        "nova_sstable_write_trailers": (i32, [vp, vp, vp, sz, u32, vp]),
-        "nova_sstable_verify_blocks": (i32, [vp, vp, vp, sz, vp, vp, vp]),
-        "nova_crc32c_stream_host": (i32, [vp, u64, u32, sz, vp, u32, sz, i32]),
-        "nova_log_write_crcs": (i32, [vp, vp, sz, vp]),
-        "nova_log_verify_records": (i32, [vp, vp, sz, vp, vp, vp]),
-        "nova_xor_parity": (i32, [vp, vp, sz, sz, vp, vp]),
-        "nova_fill_splitmix64": (i32, [vp, sz, u64, u64, vp]),
-        "nova_device_init": (i32, []),
-        "nova_crc32c_plan": (i32, [sz, u64, ctypes.POINTER(i32), ctypes.POINTER(u32)]),
-        "nova_crc32c_kernel_name": (ctypes.c_char_p, [i32]),
-        "nova_crc32c_describe": (i32, [sz, u64, u64, i32, ctypes.c_char_p, sz]),
-        "nova_crc32c_set_tuning": (None, [i32, u32]),
-        "nova_error_string": (ctypes.c_char_p, [i32]),
-        "nova_crc32c_abi_version": (i32, []),
-        "nova_diag_set_variant": (None, [i32]),
-        "nova_diag_set_static_pct": (None, [i32]),
-        "nova_diag_set_blocks_per_group": (None, [i32]),
-        "nova_diag_set_chunk_blocks": (None, [i32]),
-        "nova_diag_set_stream_waves": (None, [i32]),
-        "nova_diag_set_variable_kernel": (None, [i32]),
-        "nova_diag_set_parity_variant": (None, [i32]),
-        "nova_diag_set_rounds_sort": (None, [i32]),
-        "nova_diag_set_trailer_single_pass": (None, [i32]),
-    }
-    for name, (res, args) in sig.items():
-        fn = getattr(L, name)
-        fn.restype = res
-        fn.argtypes = args
-    _lib = L
-    return L
+    _lib = _open(path, _SIG)
+    return _lib
+
+
+def load_diag() -> ctypes.CDLL:
+    """The diagnostics build (tools/ and tuning tests only: it can compute wrong
+    CRCs on purpose, see include/nova_crc32c.h)."""
+    global _diag
+    if _diag is None:
+        if not os.path.exists(_build.DIAG_LIB):
+            raise ImportError(f"diagnostics library missing: {_build.DIAG_LIB}")
+        _diag = _open(_build.DIAG_LIB, {**_SIG, **_DIAG_SIG})
+    return _diag
+
+
+def _L() -> ctypes.CDLL:
+    return load_diag() if _active_diag else load()
+
+
+def enable_diagnostics() -> ctypes.CDLL:
+    """For tools/: route every wrapper to the diagnostics library from now on."""
+    global _active_diag
+    D = load_diag()
+    _active_diag = True
+    return D
+
+
+@contextlib.contextmanager
+def diagnostics():
+    """Route this module's wrappers to the diagnostics library inside the block
+    (its nova_diag_* knobs are per calling thread); yields that library.  The
+    knobs and the tuning are reset on exit."""
+    global _active_diag
+    D = load_diag()
+    prev = _active_diag
+    _active_diag = True
+    try:
+        yield D
+    finally:
+        _active_diag = prev
+        D.nova_crc32c_set_tuning(0, 0)
+        D.nova_diag_set_variant(0)
+        D.nova_diag_set_static_pct(-1)
+        D.nova_diag_set_blocks_per_group(0)
+        D.nova_diag_set_chunk_blocks(0)
+        D.nova_diag_set_stream_waves(0)
+        D.nova_diag_set_variable_kernel(0)
+        D.nova_diag_set_rounds_sort(2)
+        D.nova_diag_set_trailer_single_pass(0)
+        D.nova_diag_set_parity_variant(0)
 
 
 def _check(rc: int, what: str) -> None:
     if rc != 0:
-        msg = load().nova_error_string(rc).decode()
+        msg = _L().nova_error_string(rc).decode()
         raise NovaError(f"{what} failed: {msg} ({rc})")
 
 
@@ -114,7 +194,7 @@ def _bytes(data) -> bytes:
 def Extend(init_crc: int, data, n: Optional[int] = None) -> int:
     b = _bytes(data)
     n = len(b) if n is None else n
-    return load().nova_crc32c_extend(init_crc & 0xFFFFFFFF, b, n)
+    return _L().nova_crc32c_extend(init_crc & 0xFFFFFFFF, b, n)
 
 
 def Value(data, n: Optional[int] = None) -> int:
@@ -122,24 +202,35 @@ def Value(data, n: Optional[int] = None) -> int:
 
 
 def Mask(crc: int) -> int:
-    return load().nova_crc32c_mask(crc & 0xFFFFFFFF)
+    return _L().nova_crc32c_mask(crc & 0xFFFFFFFF)
 
 
 def Unmask(masked_crc: int) -> int:
-    return load().nova_crc32c_unmask(masked_crc & 0xFFFFFFFF)
+    return _L().nova_crc32c_unmask(masked_crc & 0xFFFFFFFF)
 
 
 def Combine(crc_a: int, crc_b: int, len_b: int) -> int:
-    return load().nova_crc32c_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b)
+    return _L().nova_crc32c_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b)
 
 
 def AcceleratedCRC32C(crc: int, data) -> int:
-    """port::AcceleratedCRC32C (port/port_stdcxx.h:179-189) backed by the GPU."""
+    """port::AcceleratedCRC32C (port/port_stdcxx.h:179-189): the GPU for large
+    buffers, the host Extend below NOVA_HOOK_MIN_BYTES and on any GPU failure."""
     b = _bytes(data)
-    return load().nova_port_accelerated_crc32c(crc & 0xFFFFFFFF, b, len(b))
+    return _L().nova_port_accelerated_crc32c(crc & 0xFFFFFFFF, b, len(b))
+
+
+def port_stats() -> dict:
+    h, d, f = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    _L().nova_port_stats(ctypes.byref(h), ctypes.byref(d), ctypes.byref(f))
+    return {"host": h.value, "device": d.value, "fallback": f.value}
 
 
 # ---- device batches -------------------------------------------------------
+# Every tensor argument is checked before its pointer reaches the C-ABI: the
+# kernels read descriptors as raw u64/u32 arrays and data as bytes, so a wrong
+# dtype, a non-contiguous view or a tensor on another device would be read
+# silently as garbage.
 
 def _stream_ptr(stream=None) -> int:
     import torch
@@ -147,12 +238,36 @@ def _stream_ptr(stream=None) -> int:
     return int(s.cuda_stream)
 
 
-def _ptr(t) -> Optional[int]:
+def _u64_dtypes():
+    import torch
+    return tuple(d for d in (torch.int64, getattr(torch, "uint64", None)) if d is not None)
+
+
+def _u32_dtypes():
+    import torch
+    return tuple(d for d in (torch.int32, getattr(torch, "uint32", None)) if d is not None)
+
+
+def _arg(t, name: str, dtypes, device=None, min_numel: int = 0) -> Optional[int]:
+    """Pointer of a checked tensor argument (None passes through as NULL)."""
     if t is None:
         return None
-    if not t.is_cuda:
-        raise NovaError("device batch expects GPU tensors (no CPU fallback on this path)")
+    if not getattr(t, "is_cuda", False):
+        raise NovaError(f"{name}: device batch expects GPU tensors (no CPU fallback on this path)")
+    if t.dtype not in dtypes:
+        raise NovaError(f"{name}: dtype {t.dtype} not in {[str(d) for d in dtypes]}")
+    if not t.is_contiguous():
+        raise NovaError(f"{name}: must be contiguous")
+    if device is not None and t.device != device:
+        raise NovaError(f"{name}: on {t.device}, data is on {device}")
+    if t.numel() < min_numel:
+        raise NovaError(f"{name}: {t.numel()} elements, need {min_numel}")
     return int(t.data_ptr())
+
+
+def _data(t, name: str = "data") -> int:
+    import torch
+    return _arg(t, name, (torch.uint8,))
 
 
 def _require_gpu():
@@ -163,7 +278,7 @@ def _require_gpu():
 
 def batch(data, offsets, lengths, init=None, flags: int = 0, out=None, stream=None):
     """Variable-length batch (nova_crc32c_batch). data: uint8 GPU tensor;
-    offsets: int64/uint64 GPU tensor; lengths: int32/uint32 GPU tensor."""
+    offsets: int64/uint64; lengths, init, out: int32/uint32 (same device)."""
     import torch
     _require_gpu()
     n = int(offsets.numel())
@@ -171,8 +286,11 @@ def batch(data, offsets, lengths, init=None, flags: int = 0, out=None, stream=No
         raise NovaError("offsets/lengths size mismatch")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=data.device)
-    rc = load().nova_crc32c_batch(_ptr(data), _ptr(offsets), _ptr(lengths), _ptr(init),
-                                  _ptr(out), n, flags, _stream_ptr(stream))
+    dv, u32, u64 = data.device, _u32_dtypes(), _u64_dtypes()
+    rc = _L().nova_crc32c_batch(_data(data), _arg(offsets, "offsets", u64, dv),
+                                _arg(lengths, "lengths", u32, dv),
+                                _arg(init, "init", u32, dv, n), _arg(out, "out", u32, dv, n), n,
+                                flags, _stream_ptr(stream))
     _check(rc, "nova_crc32c_batch")
     return out
 
@@ -181,12 +299,16 @@ def batch_strided(data, stride: int, length: int, n_blocks: int, init=None, flag
                   out=None, stream=None, base_offset: int = 0):
     import torch
     _require_gpu()
+    ptr = _data(data)
     if n_blocks and base_offset + (n_blocks - 1) * stride + length > data.numel():
         raise NovaError("blocks exceed the data tensor")
     if out is None:
         out = torch.empty(n_blocks, dtype=torch.int32, device=data.device)
-    rc = load().nova_crc32c_batch_strided(_ptr(data) + base_offset, stride, length, n_blocks,
-                                          _ptr(init), _ptr(out), flags, _stream_ptr(stream))
+    dv, u32 = data.device, _u32_dtypes()
+    rc = _L().nova_crc32c_batch_strided(ptr + base_offset, stride, length, n_blocks,
+                                        _arg(init, "init", u32, dv, n_blocks),
+                                        _arg(out, "out", u32, dv, n_blocks), flags,
+                                        _stream_ptr(stream))
     _check(rc, "nova_crc32c_batch_strided")
     return out
 
@@ -194,9 +316,13 @@ def batch_strided(data, stride: int, length: int, n_blocks: int, init=None, flag
 def write_trailers(buf, offsets, sizes, type_byte: int = 0, tb_quirk: bool = False, stream=None,
                    hint_large: bool = False):
     _require_gpu()
+    if sizes.numel() != offsets.numel():
+        raise NovaError("offsets/sizes size mismatch")
     flags = TYPE(type_byte) | (TB_QUIRK if tb_quirk else 0) | (HINT_LARGE_BLOCKS if hint_large else 0)
-    rc = load().nova_sstable_write_trailers(_ptr(buf), _ptr(offsets), _ptr(sizes),
-                                            int(offsets.numel()), flags, _stream_ptr(stream))
+    dv = buf.device
+    rc = _L().nova_sstable_write_trailers(_data(buf, "buf"), _arg(offsets, "offsets", _u64_dtypes(), dv),
+                                          _arg(sizes, "sizes", _u32_dtypes(), dv),
+                                          int(offsets.numel()), flags, _stream_ptr(stream))
     _check(rc, "nova_sstable_write_trailers")
     return buf
 
@@ -207,36 +333,55 @@ def verify_blocks(buf, offsets, sizes, stream=None, ok=None, bad=None):
     import torch
     _require_gpu()
     n = int(offsets.numel())
+    if sizes.numel() != n:
+        raise NovaError("offsets/sizes size mismatch")
     if ok is None:
         ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
     if bad is None:
         bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
-    rc = load().nova_sstable_verify_blocks(_ptr(buf), _ptr(offsets), _ptr(sizes), n, _ptr(ok),
-                                           _ptr(bad), _stream_ptr(stream))
+    dv = buf.device
+    rc = _L().nova_sstable_verify_blocks(_data(buf, "buf"), _arg(offsets, "offsets", _u64_dtypes(), dv),
+                                         _arg(sizes, "sizes", _u32_dtypes(), dv), n,
+                                         _arg(ok, "ok", (torch.uint8,), dv, n),
+                                         _arg(bad, "bad", _u32_dtypes(), dv, 1), _stream_ptr(stream))
     _check(rc, "nova_sstable_verify_blocks")
     return ok, bad
 
 
-def log_write_crcs(buf, record_offsets, stream=None):
-    """db/log_writer.cc:99-114 for every record header at record_offsets (in place)."""
+def log_write_crcs(buf, record_offsets, stream=None, buf_len: Optional[int] = None):
+    """db/log_writer.cc:99-114 for every record header at record_offsets (in
+    place).  buf is a log image from a 32 KiB block boundary; buf_len defaults
+    to its size."""
     _require_gpu()
-    rc = load().nova_log_write_crcs(_ptr(buf), _ptr(record_offsets), int(record_offsets.numel()),
-                                    _stream_ptr(stream))
+    bl = int(buf.numel()) if buf_len is None else int(buf_len)
+    if bl > buf.numel():
+        raise NovaError("buf_len exceeds the buffer")
+    rc = _L().nova_log_write_crcs(_data(buf, "buf"), bl,
+                                  _arg(record_offsets, "record_offsets", _u64_dtypes(), buf.device),
+                                  int(record_offsets.numel()), _stream_ptr(stream))
     _check(rc, "nova_log_write_crcs")
     return buf
 
 
-def log_verify_records(buf, record_offsets, stream=None, ok=None, bad=None):
-    """db/log_reader.cc:251-262 per record -> (ok uint8 tensor, n_bad int32 tensor[1])."""
+def log_verify_records(buf, record_offsets, stream=None, ok=None, bad=None,
+                       buf_len: Optional[int] = None):
+    """db/log_reader.cc:228-262 per record -> (status uint8 tensor of LOG_*,
+    n_bad int32 tensor[1] counting CHECKSUM_MISMATCH and BAD_LENGTH)."""
     import torch
     _require_gpu()
     n = int(record_offsets.numel())
+    bl = int(buf.numel()) if buf_len is None else int(buf_len)
+    if bl > buf.numel():
+        raise NovaError("buf_len exceeds the buffer")
     if ok is None:
         ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
     if bad is None:
         bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
-    rc = load().nova_log_verify_records(_ptr(buf), _ptr(record_offsets), n, _ptr(ok), _ptr(bad),
-                                        _stream_ptr(stream))
+    dv = buf.device
+    rc = _L().nova_log_verify_records(_data(buf, "buf"), bl,
+                                      _arg(record_offsets, "record_offsets", _u64_dtypes(), dv), n,
+                                      _arg(ok, "ok", (torch.uint8,), dv, n),
+                                      _arg(bad, "bad", _u32_dtypes(), dv, 1), _stream_ptr(stream))
     _check(rc, "nova_log_verify_records")
     return ok, bad
 
@@ -247,55 +392,134 @@ def xor_parity(buf, frag_offsets, parity_len: int, out=None, stream=None):
     _require_gpu()
     if out is None:
         out = torch.empty(parity_len, dtype=torch.uint8, device=buf.device)
-    rc = load().nova_xor_parity(_ptr(buf), _ptr(frag_offsets), int(frag_offsets.numel()),
-                                parity_len, _ptr(out), _stream_ptr(stream))
+    dv = buf.device
+    rc = _L().nova_xor_parity(_data(buf, "buf"), _arg(frag_offsets, "frag_offsets", _u64_dtypes(), dv),
+                              int(frag_offsets.numel()), parity_len,
+                              _arg(out, "out", (torch.uint8,), dv, parity_len), _stream_ptr(stream))
     _check(rc, "nova_xor_parity")
     return out
 
 
+# ---- host-resident paths ----------------------------------------------------
+
+def _host_ptr(x, name: str) -> int:
+    """Pointer of a host buffer: a CPU torch tensor (pinned or not) or a
+    numpy array; must be contiguous."""
+    if hasattr(x, "data_ptr"):
+        if getattr(x, "is_cuda", False):
+            raise NovaError(f"{name}: host path expects host memory")
+        if not x.is_contiguous():
+            raise NovaError(f"{name}: must be contiguous")
+        return int(x.data_ptr())
+    if not x.flags["C_CONTIGUOUS"]:
+        raise NovaError(f"{name}: must be contiguous")
+    return int(x.ctypes.data)
+
+
+def _np_desc(offsets, lengths):
+    import numpy as np
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    if o.shape != ln.shape:
+        raise NovaError("offsets/lengths size mismatch")
+    return o, ln
+
+
 def stream_host(host_u8, stride: int, length: int, n_blocks: int, flags: int = 0,
                 chunk_blocks: int = 4096, n_streams: int = 3):
-    """Host-resident blocks (pinned torch CPU tensor or numpy array) -> CRCs (numpy u32)."""
+    """Host-resident fixed-stride blocks (pinned torch CPU tensor or numpy array) -> CRCs (numpy u32)."""
     import numpy as np
     _require_gpu()
     out = np.empty(n_blocks, dtype=np.uint32)
-    if hasattr(host_u8, "data_ptr"):
-        ptr = int(host_u8.data_ptr())
-    else:
-        ptr = int(host_u8.ctypes.data)
-    rc = load().nova_crc32c_stream_host(ptr, stride, length, n_blocks, int(out.ctypes.data),
-                                        flags, chunk_blocks, n_streams)
+    rc = _L().nova_crc32c_stream_host(_host_ptr(host_u8, "host"), stride, length, n_blocks,
+                                      int(out.ctypes.data), flags, chunk_blocks, n_streams)
     _check(rc, "nova_crc32c_stream_host")
     return out
 
 
+def batch_host(host_u8, offsets, lengths, init=None, flags: int = 0, chunk_bytes: int = 0,
+               n_streams: int = 3):
+    """Variable-length blocks in host memory (nova_crc32c_batch_host) -> numpy u32."""
+    import numpy as np
+    _require_gpu()
+    o, ln = _np_desc(offsets, lengths)
+    ini = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
+    out = np.empty(len(o), dtype=np.uint32)
+    rc = _L().nova_crc32c_batch_host(_host_ptr(host_u8, "host"), int(o.ctypes.data),
+                                     int(ln.ctypes.data),
+                                     None if ini is None else int(ini.ctypes.data),
+                                     int(out.ctypes.data), len(o), flags, chunk_bytes, n_streams)
+    _check(rc, "nova_crc32c_batch_host")
+    return out
+
+
+def write_trailers_host(host_u8, offsets, sizes, type_byte: int = 0, tb_quirk: bool = False,
+                        chunk_bytes: int = 0, n_streams: int = 3):
+    _require_gpu()
+    o, ln = _np_desc(offsets, sizes)
+    flags = TYPE(type_byte) | (TB_QUIRK if tb_quirk else 0)
+    rc = _L().nova_sstable_write_trailers_host(_host_ptr(host_u8, "host"), int(o.ctypes.data),
+                                               int(ln.ctypes.data), len(o), flags, chunk_bytes,
+                                               n_streams)
+    _check(rc, "nova_sstable_write_trailers_host")
+    return host_u8
+
+
+def verify_blocks_host(host_u8, offsets, sizes, chunk_bytes: int = 0, n_streams: int = 3):
+    """-> (ok numpy u8, n_bad int)."""
+    import numpy as np
+    _require_gpu()
+    o, ln = _np_desc(offsets, sizes)
+    ok = np.empty(len(o), dtype=np.uint8)
+    bad = ctypes.c_uint32(0)
+    rc = _L().nova_sstable_verify_blocks_host(_host_ptr(host_u8, "host"), int(o.ctypes.data),
+                                              int(ln.ctypes.data), len(o), int(ok.ctypes.data),
+                                              ctypes.addressof(bad), chunk_bytes, n_streams)
+    _check(rc, "nova_sstable_verify_blocks_host")
+    return ok, bad.value
+
+
 def fill_splitmix64(t, seed: int, first_word: int = 0, stream=None):
     _require_gpu()
-    rc = load().nova_fill_splitmix64(_ptr(t), t.numel() * t.element_size(), seed, first_word,
-                                     _stream_ptr(stream))
+    if not t.is_contiguous():
+        raise NovaError("fill_splitmix64: tensor must be contiguous")
+    ptr = _arg(t, "t", (t.dtype,))
+    rc = _L().nova_fill_splitmix64(ptr, t.numel() * t.element_size(), seed, first_word,
+                                   _stream_ptr(stream))
     _check(rc, "nova_fill_splitmix64")
     return t
 
 
+def stream_release(stream) -> None:
+    """nova_stream_release: drop the claim-counter slot of a torch stream that
+    ran batches (before the stream goes away)."""
+    _check(_L().nova_stream_release(int(stream.cuda_stream)), "nova_stream_release")
+
+
+def stream_slots() -> int:
+    return int(_L().nova_stream_slots())
+
+
 def set_tuning(lanes_per_unit: int = 0, seg_bytes: int = 0) -> None:
-    load().nova_crc32c_set_tuning(lanes_per_unit, seg_bytes)
+    """Per calling thread (include/nova_crc32c.h)."""
+    _L().nova_crc32c_set_tuning(lanes_per_unit, seg_bytes)
 
 
 def plan(n_blocks: int, bytes_per_block: int):
     g = ctypes.c_int(0)
     s = ctypes.c_uint32(0)
-    load().nova_crc32c_plan(n_blocks, bytes_per_block, ctypes.byref(g), ctypes.byref(s))
+    _L().nova_crc32c_plan(n_blocks, bytes_per_block, ctypes.byref(g), ctypes.byref(s))
     return g.value, s.value
 
 
 def describe(n_blocks: int, length: int, stride: int, variable: bool = False,
-             large: bool = False) -> dict:
+             large: bool = False, log: bool = False) -> dict:
     import json
     buf = ctypes.create_string_buffer(512)
-    v = (2 if large else 1) if variable else 0
-    load().nova_crc32c_describe(n_blocks, length, stride, v, buf, 512)
+    v = 3 if log else ((2 if large else 1) if variable else 0)
+    _L().nova_crc32c_describe(n_blocks, length, stride, v, buf, 512)
     return json.loads(buf.value.decode())
 
 
 def kernel_name(lanes_per_unit: int) -> str:
-    return load().nova_crc32c_kernel_name(lanes_per_unit).decode()
+    return _L().nova_crc32c_kernel_name(lanes_per_unit).decode()

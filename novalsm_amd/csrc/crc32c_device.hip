@@ -96,7 +96,38 @@ struct CrcParams {
   uint64_t omask, lmask, imask;
   const uint32_t* perm;      // rounds kernel: block index per sorted position (or null)
   uint32_t sort_local;       // rounds kernel: sort each chunk's blocks by step count
+  uint64_t buf_len;          // log modes: bytes of the log image at base (bounds of every record)
 };
+
+// ---- log records: bounds and status (db/log_reader.cc:228-262) ------------
+// A record at offset o (the image starts at a 32 KiB log-block boundary,
+// db/log_format.h:27) must fit its log block and the image; otherwise it is
+// not read and gets a status instead of a CRC check.  Inside the kernels such
+// a record is carried as an EMPTY CRC range (n = 0; real records have n >= 1,
+// the type byte) whose aux word holds the status.
+constexpr uint32_t kLogBlock = 32768;
+__device__ __forceinline__ uint64_t log_block_end(uint64_t o, uint64_t buf_len) {
+  const uint64_t e = (o / kLogBlock + 1) * kLogBlock;
+  return e < buf_len ? e : buf_len;
+}
+// Status of a record whose 7-byte header fits (o + 7 <= block end), from its
+// length and type bytes; NOVA_LOG_OK means "check the CRC".
+// A record that runs past its block: cut by the end of the file if that block
+// is the file's last, partial one (the reader's eof_, :236-239), else "bad
+// record length" (:230-235).
+__device__ __forceinline__ uint32_t log_cut_status(uint64_t o, uint64_t buf_len) {
+  const uint64_t be = log_block_end(o, buf_len);
+  return (be == buf_len && (buf_len % kLogBlock) != 0) ? NOVA_LOG_TRUNCATED : NOVA_LOG_BAD_LENGTH;
+}
+__device__ __forceinline__ uint32_t log_status(uint64_t o, uint32_t length, uint32_t type,
+                                               uint64_t buf_len) {
+  if (o + 7 + length > log_block_end(o, buf_len)) return log_cut_status(o, buf_len);
+  if (type == 0 && length == 0) return NOVA_LOG_ZERO_RECORD;  // :241-247 skipped
+  return NOVA_LOG_OK;
+}
+__device__ __forceinline__ bool log_header_fits(uint64_t o, uint64_t buf_len) {
+  return o + 7 <= log_block_end(o, buf_len);
+}
 
 // ---- device helpers --------------------------------------------------------
 
@@ -580,11 +611,19 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
     const bool valid = lane < (int)p.chunk && b < p.n_blocks;
     uint64_t a = 0;
     uint32_t n = 0, init = 0;
+    uint32_t lstat = NOVA_LOG_OK;  // log modes: record status (log_status)
     if (valid) {
       a = (uint64_t)p.base + (p.offsets ? p.offsets[b] : b * p.stride);
       if (MODE == kLogWrite || MODE == kLogVerify) {
-        const uint8_t* h = (const uint8_t*)a;  // record header
-        n = 1u + ((uint32_t)h[4] | ((uint32_t)h[5] << 8));
+        const uint64_t o = a - (uint64_t)p.base;
+        if (log_header_fits(o, p.buf_len)) {
+          const uint8_t* h = (const uint8_t*)a;  // record header
+          const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
+          lstat = log_status(o, length, MODE == kLogVerify ? h[6] : 1u, p.buf_len);
+          n = lstat == NOVA_LOG_OK ? 1u + length : 0u;
+        } else {
+          lstat = log_cut_status(o, p.buf_len);
+        }
         a += 6;  // CRC input starts at the type byte
       } else {
         n = (p.lengths ? p.lengths[b] : p.len) + extra;
@@ -720,7 +759,12 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
     // -- epilogue: lane i finalises block b
     if (valid) {
       uint32_t crc = (n >= 4) ? (raw ? wacc[lane] : ~wacc[lane]) : small_crc;
-      if (MODE == kLogWrite || MODE == kLogVerify) {
+      if ((MODE == kLogWrite || MODE == kLogVerify) && lstat != NOVA_LOG_OK) {
+        if (MODE == kLogVerify) {  // not read: the status (counted if the reader reports it)
+          p.ok_out[b] = (uint8_t)lstat;
+          if (lstat == NOVA_LOG_BAD_LENGTH && p.n_bad) atomicAdd(p.n_bad, 1u);
+        }
+      } else if (MODE == kLogWrite || MODE == kLogVerify) {
         uint8_t* h = (uint8_t*)a - 6;
         const uint32_t m = mask_crc(crc);  // db/log_writer.cc:113
         if (MODE == kLogWrite) {
@@ -1144,11 +1188,12 @@ __device__ __forceinline__ void finish_block(const uint8_t* lds, uint32_t byte_t
   }
   uint32_t crc = raw ? R : ~R;
   if constexpr (kLog) {
-    wb_a = Y.u0 - 6;
+    const bool status_only = Y.u1 == Y.u0;  // a record not read: Y.st holds its status
+    wb_a = status_only ? 0ull : Y.u0 - 6;  // log write: nothing is written for it
     wb_v = mask_crc(crc);  // db/log_writer.cc:113
     if constexpr (MODE == kLogVerify) {
       wb_a = (uint64_t)(p.ok_out + Y.rec);
-      wb_v = unmask_crc(Y.st) == crc ? 1u : 0u;  // db/log_reader.cc:254-256
+      wb_v = status_only ? Y.st : (unmask_crc(Y.st) == crc ? 1u : 0u);  // db/log_reader.cc:254-256
     }
   } else if constexpr (MODE == kVerify) {
     const uint32_t k = nb >> 2;
@@ -1177,8 +1222,12 @@ __device__ __forceinline__ void write_result(const CrcParams& p, uint64_t wb_a, 
   typedef __attribute__((address_space(1))) uint8_t gu8;
   typedef __attribute__((address_space(1))) uint32_t gu32;
   if constexpr (MODE == kLogWrite) {
-    store_u32_unaligned((uint8_t*)wb_a, wb_v);
-  } else if constexpr (MODE == kLogVerify || MODE == kVerify) {
+    if (wb_a) store_u32_unaligned((uint8_t*)wb_a, wb_v);
+  } else if constexpr (MODE == kLogVerify) {
+    *(gu8*)wb_a = (uint8_t)wb_v;
+    if ((wb_v == NOVA_LOG_CHECKSUM_MISMATCH || wb_v == NOVA_LOG_BAD_LENGTH) && p.n_bad)
+      atomicAdd(p.n_bad, 1u);
+  } else if constexpr (MODE == kVerify) {
     *(gu8*)wb_a = (uint8_t)wb_v;
     if (!wb_v && p.n_bad) atomicAdd(p.n_bad, 1u);
   } else if constexpr (MODE == kTrailer) {
@@ -1188,6 +1237,9 @@ __device__ __forceinline__ void write_result(const CrcParams& p, uint64_t wb_a, 
   }
 }
 
+#ifdef NOVA_DIAG
+// The flat kernel is measured slower than the rounds kernel on every workload
+// (DESIGN.md 3.5): diagnostics build only.
 template <int G, int MODE, int VAR = 0>
 __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1255,7 +1307,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
     return reinterpret_cast<uint4*>(lds + desc_base + (bank * C + i) * 16u);
   };
   uint32_t t_olo = 0, t_ohi = 0, t_len = 0, t_aux = 0;      // descriptor words in flight
-  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0;  // log: header bytes in flight
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0, h6 = 0;  // log: header bytes in flight
   int pend = 0;            // 1: LDS write due (log: header loads due), 2: log pack + write due
   uint32_t pend_bank = 0;
   uint64_t ch0 = kNoChunk, ch1 = kNoChunk;  // chunk held by bank 0 / 1
@@ -1282,8 +1334,9 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
   // first).
   auto step_pending = [&](bool first) {
     if constexpr (kLog) {
+      const uint64_t o = ((uint64_t)t_ohi << 32) | t_olo;
       if (pend == 1 && !first) {
-        const uint8_t* h = (const uint8_t*)(base + (((uint64_t)t_ohi << 32) | t_olo));
+        const uint8_t* h = log_header_fits(o, p.buf_len) ? (const uint8_t*)(base + o) : p.zline;
         h4 = h[4];
         h5 = h[5];
         if constexpr (MODE == kLogVerify) {
@@ -1291,13 +1344,18 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
           h1 = h[1];
           h2 = h[2];
           h3 = h[3];
+          h6 = h[6];
         }
         pend = 2;
         return;
       }
       if (pend != 2 || !first) return;
-      t_len = 1u + (h4 | (h5 << 8));  // type byte + payload (db/log_format.h:27-30)
-      t_aux = h0 | (h1 << 8) | (h2 << 16) | (h3 << 24);
+      const uint32_t length = h4 | (h5 << 8);  // type byte + payload (db/log_format.h:27-30)
+      const uint32_t ls = log_header_fits(o, p.buf_len)
+                              ? log_status(o, length, MODE == kLogVerify ? h6 : 1u, p.buf_len)
+                              : log_cut_status(o, p.buf_len);
+      t_len = ls == NOVA_LOG_OK ? 1u + length : 0u;  // 0: not read, t_aux = status
+      t_aux = ls == NOVA_LOG_OK ? (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)) : ls;
     } else {
       if (pend != 1 || first) return;
     }
@@ -1330,7 +1388,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
   auto take = [&](bool first) {
     if (first) {
       asm volatile("" ::"v"(req));
-      if constexpr (kLog) asm volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(h4), "v"(h5));
+      if constexpr (kLog)
+        asm volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(h4), "v"(h5), "v"(h6));
     } else {
       asm volatile("" ::"v"(t_olo), "v"(t_ohi), "v"(t_len), "v"(t_aux));
     }
@@ -1479,6 +1538,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
   __builtin_amdgcn_s_waitcnt(0);
   sched_release(p.sched);
 }
+#endif  // NOVA_DIAG
 
 // ---- binning pre-pass + crc32c_rounds_kernel<G, MODE> ------------------------
 // Variable-length batches in ROUNDS: the wave's lane groups take kGroups blocks
@@ -1492,6 +1552,9 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
 // sort into 256 classes: exact below 128 steps, 16 per octave above), which
 // also hands the last, smallest work to the tail of the launch.
 
+#ifdef NOVA_DIAG
+// The whole-batch sort was measured slower than sorting each claimed chunk
+// (DESIGN.md 3.5a): diagnostics build only.
 constexpr int kBins = 256;
 
 __device__ __forceinline__ uint32_t steps_class(uint64_t S) {
@@ -1572,6 +1635,7 @@ __global__ void __launch_bounds__(256) bin_scatter_kernel(CrcParams p, uint64_t 
     perm[base[r] + atomicAdd(&h[r], 1u)] = (uint32_t)b;
   }
 }
+#endif  // NOVA_DIAG
 
 template <int G, int MODE, int VAR = 0>
 __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p) {
@@ -1632,7 +1696,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   // the load side (empty steps) until it is: no stage ever runs out of order.
   constexpr uint32_t kNone = 0xffffffffu;  // no chunk (chunk ids fit 32 bits: n < 2^38)
   uint32_t t_rec = 0, t_olo = 0, t_ohi = 0, t_len = 0, t_aux = 0;
-  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0;
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0, h6 = 0;
   uint64_t n_u0 = 0, c_u0 = 0;
   uint32_t n_n = 0, n_rec = 0, n_aux = 0, c_n = 0, c_rec = 0, c_aux = 0;
   uint32_t t_ok = 0, n_ok = 0, c_ok = 0;  // slot holds a block of the batch
@@ -1692,7 +1756,9 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     } else if (st == 3) {
       const uint64_t a = base + (((uint64_t)t_ohi << 32) | t_olo) + (uint64_t)t_rec * p.stride;
       if constexpr (kLog) {
-        const uint8_t* h = (const uint8_t*)a;
+        // a header past its log block / the image is not read (bounds, status)
+        const uint64_t o = ((uint64_t)t_ohi << 32) | t_olo;
+        const uint8_t* h = log_header_fits(o, p.buf_len) ? (const uint8_t*)a : p.zline;
         h4 = h[4];
         h5 = h[5];
         if constexpr (MODE == kLogVerify) {
@@ -1700,6 +1766,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
           h1 = h[1];
           h2 = h[2];
           h3 = h[3];
+          h6 = h[6];
         }
         stage = 4;
       } else {
@@ -1713,10 +1780,15 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         stage = 0;
       }
     } else if (st == 4) {
-      n_u0 = base + (((uint64_t)t_ohi << 32) | t_olo) + 6;  // CRC input: type byte + payload
-      n_n = 1u + (h4 | (h5 << 8));                          // db/log_format.h:27-30
+      const uint64_t o = ((uint64_t)t_ohi << 32) | t_olo;
+      n_u0 = base + o + 6;  // CRC input: type byte + payload
+      const uint32_t length = h4 | (h5 << 8);  // db/log_format.h:27-30
+      const uint32_t ls = log_header_fits(o, p.buf_len)
+                              ? log_status(o, length, MODE == kLogVerify ? h6 : 1u, p.buf_len)
+                              : log_cut_status(o, p.buf_len);
+      n_n = ls == NOVA_LOG_OK ? 1u + length : 0u;  // 0: not read, n_aux = status
       n_rec = t_rec;
-      n_aux = h0 | (h1 << 8) | (h2 << 16) | (h3 << 24);
+      n_aux = ls == NOVA_LOG_OK ? (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)) : ls;
       n_chunk = t_chunk;
       sort_nxt();
       fl |= fReady;
@@ -1818,7 +1890,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       }
     } else {
       asm volatile("" ::"v"(t_rec));
-      if constexpr (kLog) asm volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(h4), "v"(h5));
+      if constexpr (kLog)
+        asm volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(h4), "v"(h5), "v"(h6));
       if (stage == 2) pipe(2);
       else if (stage == 4) pipe(4);
       if (fl & fClaim) {
@@ -2073,6 +2146,7 @@ __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t s
   }
 }
 
+#ifdef NOVA_DIAG
 // Diagnostic: plain coalesced streaming read (grid-stride, 4 x 16 B per lane
 // in flight), the chip's read ceiling for comparison with the CRC kernels.
 __global__ void __launch_bounds__(256) read_stream_kernel(const uint8_t* base, uint64_t n16,
@@ -2119,6 +2193,7 @@ __global__ void __launch_bounds__(1024) read_ceiling_kernel(const uint8_t* base,
   }
   out[tid] = acc;
 }
+#endif  // NOVA_DIAG
 
 // ---- host: per-device tables ----------------------------------------------
 
@@ -2133,32 +2208,28 @@ struct DevTables {
   int err = 0;
   // Claim counters, one 16 KiB slot per HIP stream (256 workgroups x 64 B).
   // Launches on one stream run in order, so no two running launches share a
-  // slot; each launch leaves its slot zeroed (sched_release).
+  // slot; each launch leaves its slot zeroed (sched_release).  A slot lives
+  // until nova_stream_release(stream) (or process exit); the library's own
+  // streams (port hook, host-streamed path) come from a pool and are reused.
+  // The lock covers only the map: nothing waits on the GPU while holding it.
   std::mutex sched_mu;
   std::unordered_map<uint64_t, uint32_t*> sched_by_stream;
-  // Rounds kernel: per-stream scratch for the sort (2 x kBins counters + perm).
-  struct SortScratch {
-    uint32_t* hist = nullptr;
-    uint32_t* perm = nullptr;
-    size_t cap = 0;
-    uint32_t* crc = nullptr;  // trailer writer: per-block masked CRCs between its passes
-    size_t crc_cap = 0;
-  };
-  std::unordered_map<uint64_t, SortScratch> sort_by_stream;
 };
 
 constexpr int kMaxDevices = 64;
 constexpr int kSchedWords = 256 * 16;  // per stream: up to 256 workgroups x 64 B
-std::atomic<int> g_tune_static_pct{-1};  // reused: steal probe limit (-1 = default)
+thread_local std::atomic<int> g_tune_static_pct{-1};  // reused: steal probe limit (-1 = default)
 DevTables g_dev[kMaxDevices];
 std::once_flag g_once[kMaxDevices];
 
-std::atomic<int> g_tune_g{0};
-std::atomic<int> g_tune_var{0};
-std::atomic<int> g_tune_bpg{0};
-std::atomic<int> g_tune_chunk{0};
-std::atomic<int> g_tune_waves{0};  // waves per workgroup override (0 = per-kernel default)
-std::atomic<int> g_tune_parity{0};  // XOR parity kernel variant (0 = default)
+thread_local std::atomic<int> g_tune_g{0};
+#ifdef NOVA_DIAG
+thread_local std::atomic<int> g_tune_var{0};  // kernel variant (ablations)
+#endif
+thread_local std::atomic<int> g_tune_bpg{0};
+thread_local std::atomic<int> g_tune_chunk{0};
+thread_local std::atomic<int> g_tune_waves{0};  // waves per workgroup override (0 = per-kernel default)
+thread_local std::atomic<int> g_tune_parity{0};  // XOR parity kernel variant (0 = default)
 
 // Waves per workgroup.  The tables fill the CU's LDS, so a CU runs exactly one
 // workgroup; fewer waves keep fewer HBM reads in flight per CU, which the
@@ -2169,8 +2240,10 @@ int waves_per_wg(int def) {
   const int w = g_tune_waves.load();
   return (w > 0 && w <= kWaves) ? w : def;
 }
-std::atomic<uint64_t*> g_diag_stamps{nullptr};
-std::atomic<uint32_t> g_tune_seg{0};
+#ifdef NOVA_DIAG
+thread_local std::atomic<uint64_t*> g_diag_stamps{nullptr};
+#endif
+thread_local std::atomic<uint32_t> g_tune_seg{0};
 
 void build_main_image(const nova::gf2::Lin& m, std::vector<uint32_t>& img) {
   uint32_t t[4][256];
@@ -2226,11 +2299,23 @@ constexpr size_t flat_lds() {
   return kMainBytes + (2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16)) * kTreeBytes + 1024;
 }
 
+#ifdef NOVA_DIAG
 template <int G, int MODE, int VAR = 0>
 int set_lds_attr_flat() {
   return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_flat_kernel<G, MODE, VAR>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
 }
+
+template <int MODE, int VAR = 0>
+int set_lds_attrs_flat() {
+  int e = 0;
+  if ((e = set_lds_attr_flat<1, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_flat<2, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_flat<4, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_flat<8, MODE, VAR>())) return e;
+  return set_lds_attr_flat<16, MODE, VAR>();
+}
+#endif
 
 template <int G, int MODE, int VAR = 0>
 int set_lds_attr_rounds() {
@@ -2245,16 +2330,6 @@ int set_lds_attrs_rounds() {
   if ((e = set_lds_attr_rounds<4, MODE, VAR>())) return e;
   if ((e = set_lds_attr_rounds<8, MODE, VAR>())) return e;
   return set_lds_attr_rounds<16, MODE, VAR>();
-}
-
-template <int MODE, int VAR = 0>
-int set_lds_attrs_flat() {
-  int e = 0;
-  if ((e = set_lds_attr_flat<1, MODE, VAR>())) return e;
-  if ((e = set_lds_attr_flat<2, MODE, VAR>())) return e;
-  if ((e = set_lds_attr_flat<4, MODE, VAR>())) return e;
-  if ((e = set_lds_attr_flat<8, MODE, VAR>())) return e;
-  return set_lds_attr_flat<16, MODE, VAR>();
 }
 
 template <int VAR = 0>
@@ -2311,6 +2386,19 @@ void init_device(int dev, DevTables* t) {
     for (uint32_t b = 0; b < 256; b++) b8[b] = m1(b);
     if ((t->err = upload(&t->byte8, b8))) return;
   }
+  if ((t->err = set_lds_attrs_rounds<kStore>())) return;
+  if ((t->err = set_lds_attrs_rounds<kTrailer>())) return;
+  if ((t->err = set_lds_attrs_rounds<kVerify>())) return;
+  if ((t->err = set_lds_attrs_rounds<kLogWrite>())) return;
+  if ((t->err = set_lds_attrs_rounds<kLogVerify>())) return;
+  if ((t->err = set_lds_attrs_mode<kStore>())) return;
+  if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
+  if ((t->err = set_lds_attrs_mode<kVerify>())) return;
+  if ((t->err = set_lds_attrs_mode<kLogWrite>())) return;
+  if ((t->err = set_lds_attrs_mode<kLogVerify>())) return;
+  if ((t->err = set_lds_attrs_stream<0>())) return;
+#ifdef NOVA_DIAG
+  // timing ablations and alternative schedules (diagnostics build only)
   if ((t->err = set_lds_attrs_flat<kStore>())) return;
   if ((t->err = set_lds_attrs_flat<kTrailer>())) return;
   if ((t->err = set_lds_attrs_flat<kVerify>())) return;
@@ -2318,27 +2406,17 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_flat<kLogVerify>())) return;
   if ((t->err = set_lds_attrs_flat<kStore, kVarNoLookup>())) return;
   if ((t->err = set_lds_attrs_flat<kStore, kVarCached>())) return;
-  if ((t->err = set_lds_attrs_rounds<kStore>())) return;
-  if ((t->err = set_lds_attrs_rounds<kTrailer>())) return;
-  if ((t->err = set_lds_attrs_rounds<kVerify>())) return;
-  if ((t->err = set_lds_attrs_rounds<kLogWrite>())) return;
-  if ((t->err = set_lds_attrs_rounds<kLogVerify>())) return;
   if ((t->err = set_lds_attrs_rounds<kStore, kVarNoLookup>())) return;
   if ((t->err = set_lds_attrs_rounds<kStore, kVarNarrow>())) return;
-  if ((t->err = set_lds_attrs_mode<kStore>())) return;
-  if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
-  if ((t->err = set_lds_attrs_mode<kVerify>())) return;
-  if ((t->err = set_lds_attrs_mode<kLogWrite>())) return;
-  if ((t->err = set_lds_attrs_mode<kLogVerify>())) return;
   if ((t->err = set_lds_attrs_mode<kStore, kVarNoLookup>())) return;
   if ((t->err = set_lds_attrs_mode<kStore, kVarNarrow>())) return;
   if ((t->err = set_lds_attrs_mode<kStore, kVarCached>())) return;
-  if ((t->err = set_lds_attrs_stream<0>())) return;
   if ((t->err = set_lds_attrs_stream<kVarNoLookup>())) return;
   if ((t->err = set_lds_attrs_stream<kVarCached>())) return;
   if ((t->err = set_lds_attrs_stream<kVarWide>())) return;
   if ((t->err = set_lds_attrs_stream<kVarStamps>())) return;
   if ((t->err = set_lds_attrs_stream<kVarStamps | kVarStaticClaims>())) return;
+#endif
 }
 
 DevTables* tables(int* err) {
@@ -2371,6 +2449,30 @@ uint32_t* sched_slot(DevTables* t, hipStream_t stream) {
   return static_cast<uint32_t*>(d);
 }
 
+// Drop the stream's slot (nova_stream_release): waits for the stream's work,
+// then frees the slot outside the lock.
+int sched_release_stream(DevTables* t, hipStream_t stream) {
+  uint64_t key = (uint64_t)(uintptr_t)stream;
+  if (stream == hipStreamPerThread)
+    key = (std::hash<std::thread::id>{}(std::this_thread::get_id()) << 1) | 1u;
+  const hipError_t e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) return (int)e;
+  uint32_t* slot = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(t->sched_mu);
+    auto it = t->sched_by_stream.find(key);
+    if (it == t->sched_by_stream.end()) return 0;
+    slot = it->second;
+    t->sched_by_stream.erase(it);
+  }
+  return (int)hipFree(slot);
+}
+
+size_t sched_slots(DevTables* t) {
+  std::lock_guard<std::mutex> lk(t->sched_mu);
+  return t->sched_by_stream.size();
+}
+
 int gindex(int G) { return G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : 4; }
 
 // Dispatcher policy for batches the streaming kernel does not take.
@@ -2385,7 +2487,7 @@ uint64_t flat_waves() {
   return w > kFlatMaxWaves ? kFlatMaxWaves : w;
 }
 enum VarKernel { kAuto = 0, kUnitsK = 1, kFlatK = 2, kRoundsK = 3 };
-std::atomic<int> g_tune_kernel{0};
+thread_local std::atomic<int> g_tune_kernel{0};
 struct Plan {
   int kernel;
   int G;
@@ -2446,11 +2548,11 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, b
   return pl;
 }
 
+size_t flat_lds_g(int G);
+#ifdef NOVA_DIAG
 // Blocks per claimed chunk of the flat kernel: one per lane group (the bank
 // refill is one step old when read), four per group for log records (the
 // header bytes need two more steps); at most 64 (one per lane).
-uint64_t flat_waves();
-size_t flat_lds_g(int G);
 uint32_t flat_chunk(int G, int mode) {
   const uint32_t groups = 64u / (uint32_t)G;
   const bool log = mode == kLogWrite || mode == kLogVerify;
@@ -2463,6 +2565,7 @@ uint32_t flat_chunk(int G, int mode) {
   if (c < 2 * groups) c = 2 * groups;  // the kernel relies on it (positions < 2C)
   return c;
 }
+#endif
 
 size_t flat_lds_g(int G) {
   switch (G) {
@@ -2474,6 +2577,7 @@ size_t flat_lds_g(int G) {
   }
 }
 
+#ifdef NOVA_DIAG
 template <int MODE, int VAR>
 int launch_flat_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
   switch (G) {
@@ -2535,6 +2639,7 @@ int launch_flat(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   if (MODE == kStore && var == kVarCached) return launch_flat_g<kStore, kVarCached>(G, dim3(wgs), block, lds, stream, p);
   return launch_flat_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
 }
+#endif  // NOVA_DIAG
 
 template <int MODE, int VAR>
 int launch_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
@@ -2578,10 +2683,12 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   const size_t lds = kMainBytes + levels * kTreeBytes + kWaves * kWaveScratch;
   const dim3 block(64 * nwaves);
+#ifdef NOVA_DIAG
   const int var = g_tune_var.load();
   if (MODE == kStore && var == kVarNoLookup) return launch_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
   if (MODE == kStore && var == kVarNarrow) return launch_g<kStore, kVarNarrow>(G, dim3(wgs), block, lds, stream, p);
   if (MODE == kStore && var == kVarCached) return launch_g<kStore, kVarCached>(G, dim3(wgs), block, lds, stream, p);
+#endif
   return launch_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
 }
 
@@ -2622,75 +2729,47 @@ uint32_t stream_bpg(int G, uint32_t len) {
   return b < 1 ? 1u : (b > 64 ? 64u : (uint32_t)b);
 }
 
-// Per-stream sort scratch (grown on demand; launches on one stream run in order).
-DevTables::SortScratch* sort_scratch(DevTables* t, hipStream_t stream, size_t n) {
-  uint64_t key = (uint64_t)(uintptr_t)stream;
-  if (stream == hipStreamPerThread)
-    key = (std::hash<std::thread::id>{}(std::this_thread::get_id()) << 1) | 1u;
-  std::lock_guard<std::mutex> lk(t->sched_mu);
-  DevTables::SortScratch& sc = t->sort_by_stream[key];
-  if (!sc.hist) {
-    void* d = nullptr;
-    if (hipMalloc(&d, 2 * kBins * sizeof(uint32_t)) != hipSuccess) return nullptr;
-    sc.hist = static_cast<uint32_t*>(d);
+// Scratch that lives between launches of ONE call is allocated and freed in
+// stream order (hipMallocAsync / hipFreeAsync from the device's default
+// pool): every call owns its own array, so calls from several host threads
+// on one stream cannot see each other's scratch, and nothing is freed while
+// a kernel still reads it.
+struct StreamScratch {
+  void* p = nullptr;
+  hipStream_t s = nullptr;
+  int alloc(size_t bytes, hipStream_t stream) {
+    s = stream;
+    return hipMallocAsync(&p, bytes, stream) == hipSuccess ? 0 : NOVA_E_NOMEM;
   }
-  if (sc.cap < n) {
-    if (sc.perm) {
-      (void)hipStreamSynchronize(stream);  // the old array may still be read
-      (void)hipFree(sc.perm);
-      sc.perm = nullptr;
-      sc.cap = 0;
-    }
-    void* d = nullptr;
-    if (hipMalloc(&d, n * sizeof(uint32_t)) != hipSuccess) return nullptr;
-    sc.perm = static_cast<uint32_t*>(d);
-    sc.cap = n;
+  ~StreamScratch() {
+    if (p) (void)hipFreeAsync(p, s);
   }
-  return &sc;
-}
+};
 
-// Per-stream u32 array for the trailer writer's two passes (grown on demand).
-uint32_t* crc_scratch(DevTables* t, hipStream_t stream, size_t n) {
-  uint64_t key = (uint64_t)(uintptr_t)stream;
-  if (stream == hipStreamPerThread)
-    key = (std::hash<std::thread::id>{}(std::this_thread::get_id()) << 1) | 1u;
-  std::lock_guard<std::mutex> lk(t->sched_mu);
-  DevTables::SortScratch& sc = t->sort_by_stream[key];
-  if (sc.crc_cap < n) {
-    if (sc.crc) {
-      (void)hipStreamSynchronize(stream);  // the old array may still be in use
-      (void)hipFree(sc.crc);
-      sc.crc = nullptr;
-      sc.crc_cap = 0;
-    }
-    void* d = nullptr;
-    if (hipMalloc(&d, n * sizeof(uint32_t)) != hipSuccess) return nullptr;
-    sc.crc = static_cast<uint32_t*>(d);
-    sc.crc_cap = n;
-  }
-  return sc.crc;
-}
-
+#ifdef NOVA_DIAG
 template <int MODE>
-int launch_sort(CrcParams& p, DevTables* t, hipStream_t stream, uint64_t kStep) {
-  DevTables::SortScratch* sc = sort_scratch(t, stream, p.n_blocks);
-  if (!sc) return NOVA_E_NOMEM;
-  hipError_t e = hipMemsetAsync(sc->hist, 0, kBins * sizeof(uint32_t), stream);
+int launch_sort(CrcParams& p, DevTables* t, hipStream_t stream, uint64_t kStep, StreamScratch& sc) {
+  const size_t hist_bytes = 2 * kBins * sizeof(uint32_t);
+  if (sc.alloc(hist_bytes + p.n_blocks * sizeof(uint32_t), stream)) return NOVA_E_NOMEM;
+  uint32_t* hist = static_cast<uint32_t*>(sc.p);
+  uint32_t* perm = hist + 2 * kBins;
+  hipError_t e = hipMemsetAsync(hist, 0, kBins * sizeof(uint32_t), stream);
   if (e != hipSuccess) return (int)e;
   uint64_t wgs = (p.n_blocks + 255) / 256;
   const uint64_t cap = (uint64_t)t->cus * 4;
   if (wgs > cap) wgs = cap;
-  hipLaunchKernelGGL(bin_count_kernel<MODE>, dim3(wgs), dim3(256), 0, stream, p, kStep, sc->hist);
-  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(kBins), 0, stream, sc->hist, sc->hist + kBins);
+  hipLaunchKernelGGL(bin_count_kernel<MODE>, dim3(wgs), dim3(256), 0, stream, p, kStep, hist);
+  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(kBins), 0, stream, hist, hist + kBins);
   hipLaunchKernelGGL(bin_scatter_kernel<MODE>, dim3(wgs), dim3(256), 0, stream, p, kStep,
-                     sc->hist + kBins, sc->perm);
+                     hist + kBins, perm);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-  p.perm = sc->perm;
+  p.perm = perm;
   return 0;
 }
+#endif
 
-std::atomic<int> g_tune_sort{2};  // rounds kernel: 0 in order, 1 whole-batch sort, 2 per chunk
-std::atomic<int> g_tune_trailer_1pass{0};  // trailer writer: 1 = single pass in the rounds kernel
+thread_local std::atomic<int> g_tune_sort{2};  // rounds kernel: 0 in order, 1 whole-batch sort, 2 per chunk
+thread_local std::atomic<int> g_tune_trailer_1pass{0};  // trailer writer: 1 = single pass in the rounds kernel
 
 template <int MODE, int VAR>
 int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
@@ -2730,14 +2809,18 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_
   p.perm = nullptr;
   const int sort = g_tune_sort.load();  // 0 none, 1 whole batch (pre-pass), 2 per chunk
   p.sort_local = sort == 2 ? 1u : 0u;
+#ifdef NOVA_DIAG
+  StreamScratch sort_sc;  // freed in stream order after the launch below
   if (sort == 1 && p.n_blocks >= 1024) {
-    const int e = launch_sort<MODE>(p, t, stream, 64ull * G);
+    const int e = launch_sort<MODE>(p, t, stream, 64ull * G, sort_sc);
     if (e) return e;
   }
+#endif
   {
-    // chunk = R rounds of 64/G blocks.  Log records: 64 (the header stage
-    // needs 4 steps of pipeline).  SSTable blocks: 4 rounds, since a chunk is
-    // also the unit of the tail balance and big blocks make big chunks.
+    // chunk = R rounds of 64/G blocks.  Default (plan() passes 0 only when
+    // tuning forces G): log records 64, SSTable blocks 4 rounds, since a chunk
+    // is also the unit of the tail balance and big blocks make big chunks.
+    // plan() sizes both to the batch (latency-bound small batches).
     const uint32_t groups = 64u / (uint32_t)G;
     const bool log = MODE == kLogWrite || MODE == kLogVerify;
     uint32_t c = chunk ? chunk : (log ? 64u : 4u * groups);
@@ -2766,10 +2849,12 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_
   if (!p.sched) return NOVA_E_NOMEM;
   const dim3 block(64 * nwaves);
   const size_t lds = flat_lds_g(G) + nwaves * 64 * 4;  // + per-wave sort scratch
+#ifdef NOVA_DIAG
   if (MODE == kStore && g_tune_var.load() == kVarNoLookup)
     return launch_rounds_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
   if (MODE == kStore && g_tune_var.load() == kVarNarrow)
     return launch_rounds_g<kStore, kVarNarrow>(G, dim3(wgs), block, lds, stream, p);
+#endif
   return launch_rounds_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
 }
 
@@ -2797,6 +2882,7 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   if (!p.sched) return NOVA_E_NOMEM;
   const int levels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   const size_t lds = kMainBytes + levels * kTreeBytes;
+#ifdef NOVA_DIAG
   if (g_tune_var.load() == kVarNoLookup) return launch_stream_g<kVarNoLookup>(G, dim3(wgs), lds, stream, p);
   if (g_tune_var.load() == kVarCached) return launch_stream_g<kVarCached>(G, dim3(wgs), lds, stream, p);
   if (g_tune_var.load() == kVarWide) return launch_stream_g<kVarWide>(G, dim3(wgs), lds, stream, p);
@@ -2808,6 +2894,7 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
     p.stamps = g_diag_stamps.load();
     return launch_stream_g<kVarStamps | kVarStaticClaims>(G, dim3(wgs), lds, stream, p);
   }
+#endif
   return launch_stream_g<0>(G, dim3(wgs), lds, stream, p);
 }
 
@@ -2829,10 +2916,11 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // whole fixed cost to the call.
   const bool small = p.n_blocks <= 2ull * t->cus * flat_waves();
   if (pl.kernel == kRoundsK && mode == kTrailer && !g_tune_trailer_1pass.load() && !small) {
-    // Two passes: CRCs (type byte appended, masked) into a per-stream array,
-    // then the trailer bytes (trailer_scatter_kernel).
-    uint32_t* tmp = crc_scratch(t, stream, p.n_blocks);
-    if (!tmp) return NOVA_E_NOMEM;
+    // Two passes: CRCs (type byte appended, masked) into this call's own
+    // stream-ordered array, then the trailer bytes (trailer_scatter_kernel).
+    StreamScratch sc;  // freed in stream order after the scatter
+    if (sc.alloc(p.n_blocks * sizeof(uint32_t), stream)) return NOVA_E_NOMEM;
+    uint32_t* tmp = static_cast<uint32_t*>(sc.p);
     CrcParams q = p;
     q.out = tmp;
     q.flags = (p.flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT;
@@ -2854,6 +2942,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
       default: return launch_rounds<kVerify>(G, p, t, stream, pl.chunk);
     }
   }
+#ifdef NOVA_DIAG
   if (pl.kernel == kFlatK) {
     switch (mode) {
       case kStore: return launch_flat<kStore>(G, p, t, stream);
@@ -2863,6 +2952,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
       default: return launch_flat<kVerify>(G, p, t, stream);
     }
   }
+#endif
   switch (mode) {
     case kStore: return launch_mode<kStore>(G, p, t, stream);
     case kTrailer: return launch_mode<kTrailer>(G, p, t, stream);
@@ -2872,15 +2962,40 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   }
 }
 
+// The device's CU count for plan reports (the same value run() uses), without
+// initialising the device: 256 (MI355X) when no table set exists yet.
+uint32_t cus_hint() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  if (dev < 0 || dev >= kMaxDevices || g_dev[dev].cus <= 0) return 256;
+  return (uint32_t)g_dev[dev].cus;
+}
+
 }  // namespace
 
 extern "C" {
 
-int nova_crc32c_abi_version(void) { return 1; }
+int nova_crc32c_abi_version(void) { return 2; }
 
 int nova_device_init(void) {
   int err = 0;
   return tables(&err) ? 0 : err;
+}
+
+int nova_stream_release(void* stream) {
+  int err = 0;
+  DevTables* t = tables(&err);
+  if (!t) return err;
+  return sched_release_stream(t, (hipStream_t)stream);
+}
+
+size_t nova_stream_slots(void) {
+  int err = 0;
+  DevTables* t = tables(&err);
+  return t ? sched_slots(t) : 0;
 }
 
 int nova_crc32c_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
@@ -2940,21 +3055,23 @@ int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const u
   return run(kVerify, p, false, 0, (hipStream_t)stream);
 }
 
-int nova_log_write_crcs(void* buf, const uint64_t* record_offsets, size_t n_records,
-                        void* stream) {
+int nova_log_write_crcs(void* buf, size_t buf_len, const uint64_t* record_offsets,
+                        size_t n_records, void* stream) {
   if (n_records && (!buf || !record_offsets)) return NOVA_E_INVAL;
   CrcParams p{};
   p.base = (const uint8_t*)buf;
+  p.buf_len = buf_len;
   p.offsets = record_offsets;
   p.n_blocks = n_records;
   return run(kLogWrite, p, false, 0, (hipStream_t)stream);
 }
 
-int nova_log_verify_records(const void* buf, const uint64_t* record_offsets, size_t n_records,
-                            uint8_t* ok_out, uint32_t* n_bad_out, void* stream) {
+int nova_log_verify_records(const void* buf, size_t buf_len, const uint64_t* record_offsets,
+                            size_t n_records, uint8_t* ok_out, uint32_t* n_bad_out, void* stream) {
   if (n_records && (!buf || !record_offsets || !ok_out)) return NOVA_E_INVAL;
   CrcParams p{};
   p.base = (const uint8_t*)buf;
+  p.buf_len = buf_len;
   p.offsets = record_offsets;
   p.ok_out = ok_out;
   p.n_bad = n_bad_out;
@@ -3021,7 +3138,7 @@ int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_u
     if (seg_bytes) *seg_bytes = 0;
     return 1;  // streaming kernel
   }
-  const Plan pl = plan(n_blocks, bytes_per_block, true, kStore, false);
+  const Plan pl = plan(n_blocks, bytes_per_block, true, kStore, false, cus_hint());
   if (lanes_per_unit) *lanes_per_unit = pl.G;
   if (seg_bytes) *seg_bytes = pl.seg;
   return pl.kernel == kFlatK ? 2 : pl.kernel == kRoundsK ? 3 : 0;  // flat : rounds : units
@@ -3044,24 +3161,29 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
                  sg, sg, stream_bpg(sg, (uint32_t)len),
                  g_tune_static_pct.load() < 0 ? 8 : g_tune_static_pct.load());
   } else {
-    const Plan pl = plan(n_blocks, len, !variable, kStore, variable == 2);
-    const int g = pl.G;
+    const bool log = variable == 3;
+    const int mode = log ? kLogWrite : kStore;
+    const Plan pl = plan(n_blocks, len, !variable, mode, variable == 2, cus_hint());
+    const int g = pl.G < 2 ? 2 : pl.G;
+    // the chunk launch_rounds() runs when plan() leaves it to the default
+    const uint32_t def_chunk = log ? 64u : 4u * (64u / (uint32_t)g);
     if (pl.kernel == kRoundsK)
       n = snprintf(buf, buflen,
-                   "{\"kernel\": \"crc32c_rounds_kernel<%d, 0>\", \"lanes_per_block\": %d, "
-                   "\"sort\": %d, \"waves_per_wg\": %d, \"chunk_blocks\": %u}", g < 2 ? 2 : g,
-                   g < 2 ? 2 : g, g_tune_sort.load(), (int)flat_waves(),
-                   pl.chunk ? pl.chunk : 4u * (64u / (uint32_t)(g < 2 ? 2 : g)));
-    else if (pl.kernel != kFlatK)
+                   "{\"kernel\": \"crc32c_rounds_kernel<%d, %d>\", \"lanes_per_block\": %d, "
+                   "\"sort\": %d, \"waves_per_wg\": %d, \"chunk_blocks\": %u}", g, mode,
+                   g, g_tune_sort.load(), (int)flat_waves(), pl.chunk ? pl.chunk : def_chunk);
+#ifdef NOVA_DIAG
+    else if (pl.kernel == kFlatK)
       n = snprintf(buf, buflen,
-                   "{\"kernel\": \"crc32c_units_kernel<%d, 0>\", \"lanes_per_unit\": %d, "
-                   "\"segment_bytes\": %u, \"waves_per_wg\": %d}", g, g, pl.seg,
-                   waves_per_wg(kUnitsWaves));
+                   "{\"kernel\": \"crc32c_flat_kernel<%d, %d>\", \"lanes_per_block\": %d, "
+                   "\"chunk_blocks\": %u, \"waves_per_wg\": %d}", pl.G, mode, pl.G,
+                   flat_chunk(pl.G, mode), (int)flat_waves());
+#endif
     else
       n = snprintf(buf, buflen,
-                   "{\"kernel\": \"crc32c_flat_kernel<%d, 0>\", \"lanes_per_block\": %d, "
-                   "\"chunk_blocks\": %u, \"waves_per_wg\": %d}", g, g, flat_chunk(g, kStore),
-                   (int)flat_waves());
+                   "{\"kernel\": \"crc32c_units_kernel<%d, %d>\", \"lanes_per_unit\": %d, "
+                   "\"segment_bytes\": %u, \"waves_per_wg\": %d}", pl.G, mode, pl.G, pl.seg,
+                   waves_per_wg(kUnitsWaves));
   }
   return n;
 }
@@ -3082,6 +3204,7 @@ void nova_crc32c_set_tuning(int lanes_per_unit, uint32_t seg_bytes) {
   g_tune_seg.store(seg_bytes);
 }
 
+#ifdef NOVA_DIAG
 void nova_diag_set_variant(int variant) { g_tune_var.store(variant); }
 
 void nova_diag_set_stamps(uint64_t* dev_stamps) { g_diag_stamps.store(dev_stamps); }
@@ -3129,6 +3252,8 @@ int nova_diag_read_ceiling(const void* base, size_t bytes, uint32_t* out_dev, in
 #undef NOVA_RC
   return NOVA_E_INVAL;
 }
+
+#endif  // NOVA_DIAG
 
 const char* nova_error_string(int err) {
   switch (err) {

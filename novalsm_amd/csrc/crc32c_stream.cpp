@@ -1,16 +1,30 @@
 // Host-resident paths of the engine:
-//   * nova_crc32c_stream_host -- BASELINE config 5: blocks in host memory (the
-//     analogue of NovaLSM's RDMA-registered SSTable buffer, backing_mem_ in
-//     ltc/stoc_file_client_impl.cpp:43-45 over nova_buf registered in
-//     rdma/nova_rdma_rc_broker.cpp:31-35) stream H2D -> CRC kernel -> D2H in
-//     chunks over several HIP streams so copies overlap the kernels.
+//   * nova_crc32c_stream_host -- BASELINE config 5: fixed-stride blocks in host
+//     memory (the analogue of NovaLSM's RDMA-registered SSTable buffer,
+//     backing_mem_ in ltc/stoc_file_client_impl.cpp:43-45 over nova_buf
+//     registered in rdma/nova_rdma_rc_broker.cpp:31-35) stream H2D -> CRC
+//     kernel -> D2H in chunks over several HIP streams so copies overlap the
+//     kernels.
+//   * nova_crc32c_batch_host / nova_sstable_write_trailers_host /
+//     nova_sstable_verify_blocks_host -- the same for a real SSTable image:
+//     variable-length blocks with 5-byte trailers, e.g. the Format() buffer
+//     (ltc/stoc_file_client_impl.cpp:183-377) or the ReadAll() slab (:843-882).
+//     Chunks are contiguous runs of blocks; each copies the byte span its
+//     blocks cover.
 //   * nova_port_accelerated_crc32c -- the reference's plug-in hook
-//     port::AcceleratedCRC32C (port/port_stdcxx.h:179-189) backed by the GPU:
-//     the buffer is cut into 4 KiB sub-blocks whose linear ("raw") CRCs are
-//     computed by the HIP kernels and folded on the host with the GF(2) shift.
+//     port::AcceleratedCRC32C (port/port_stdcxx.h:179-189) backed by the GPU
+//     for large buffers, by the host Extend otherwise and on any GPU error.
+//
+// The library's own HIP streams come from a per-device pool (created once,
+// reused): a stream per call would also leave one claim-counter slot per
+// stream address behind (crc32c_device.hip, sched_slot).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "../../include/nova_crc32c.h"
@@ -21,15 +35,25 @@ namespace {
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
-  ~DevBuf() {
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  ~DevBuf() { reset(); }
+  void reset() {
     if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
   }
   int ensure(size_t bytes) {
     if (bytes <= n) return 0;
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
-    if (hipMalloc(&p, bytes) != hipSuccess) return NOVA_E_NOMEM;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+      (void)hipGetLastError();
+      return NOVA_E_NOMEM;
+    }
     n = bytes;
     return 0;
   }
@@ -38,6 +62,10 @@ struct DevBuf {
 struct PinBuf {
   void* p = nullptr;
   size_t n = 0;
+  PinBuf() = default;
+  PinBuf(const PinBuf&) = delete;
+  PinBuf& operator=(const PinBuf&) = delete;
+  PinBuf(PinBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
   ~PinBuf() {
     if (p) (void)hipHostFree(p);
   }
@@ -46,7 +74,10 @@ struct PinBuf {
     if (p) (void)hipHostFree(p);
     p = nullptr;
     n = 0;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return NOVA_E_NOMEM;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return NOVA_E_NOMEM;
+    }
     n = bytes;
     return 0;
   }
@@ -62,6 +93,304 @@ bool is_pinned(const void* p) {
          attr.type == hipMemoryTypeManaged;
 }
 
+// ---- library-owned stream pool ----------------------------------------------
+constexpr int kMaxDevices = 64;
+struct StreamPool {
+  std::mutex mu;
+  std::vector<hipStream_t> idle[kMaxDevices];
+};
+StreamPool& pool() {
+  static StreamPool* p = new StreamPool;  // never destroyed: streams outlive exit order
+  return *p;
+}
+
+// A pooled stream of the current device, or nullptr.
+hipStream_t acquire_stream(int* dev_out) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  *dev_out = dev;
+  {
+    std::lock_guard<std::mutex> lk(pool().mu);
+    auto& v = pool().idle[dev];
+    if (!v.empty()) {
+      hipStream_t s = v.back();
+      v.pop_back();
+      return s;
+    }
+  }
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return s;
+}
+
+void release_stream(int dev, hipStream_t s) {
+  if (!s) return;
+  std::lock_guard<std::mutex> lk(pool().mu);
+  pool().idle[dev].push_back(s);
+}
+
+// RAII set of pooled streams for one call.
+struct Streams {
+  std::vector<hipStream_t> s;
+  int dev = 0;
+  int get(int n) {
+    for (int i = 0; i < n; i++) {
+      hipStream_t x = acquire_stream(&dev);
+      if (!x) return NOVA_E_NODEV;
+      s.push_back(x);
+    }
+    return 0;
+  }
+  int sync() {
+    int rc = 0;
+    for (hipStream_t x : s) {
+      const hipError_t e = hipStreamSynchronize(x);
+      if (!rc && e != hipSuccess) rc = (int)e;
+    }
+    return rc;
+  }
+  ~Streams() {
+    (void)sync();  // never hand back a stream with work in flight
+    for (hipStream_t x : s) release_stream(dev, x);
+  }
+};
+
+// Registers pageable host memory for the duration of a call (no-op if pinned).
+struct HostReg {
+  void* p = nullptr;
+  int reg(const void* base, size_t len) {
+    if (!len || is_pinned(base)) return 0;
+    if (hipHostRegister(const_cast<void*>(base), len, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return NOVA_E_NOMEM;
+    }
+    p = const_cast<void*>(base);
+    return 0;
+  }
+  ~HostReg() {
+    if (p) (void)hipHostUnregister(p);
+  }
+};
+
+// ---- variable-length host images --------------------------------------------
+enum HostOp { kHostCrc = 0, kHostTrailers = 1, kHostVerify = 2 };
+
+// Per-stream staging of one chunk: its byte span and rebased descriptors.
+struct Stage {
+  DevBuf data, offs, lens, init, out;
+  PinBuf hoffs, hlens;  // rebased descriptors (pinned: async H2D)
+};
+
+// Runs a batch over blocks that live in host memory.  Blocks [b0, b1) form a
+// chunk when their spanned bytes fit chunk_bytes (a single larger block gets a
+// chunk of its own); the span [lo, hi) is copied H2D, the chunk's offsets are
+// rebased to it, the kernel runs on the device copy and the per-block results
+// (CRCs or verify flags) come back D2H into pinned memory.
+int host_batch(HostOp op, const void* host_base, const uint64_t* offsets, const uint32_t* lengths,
+               const uint32_t* init, size_t n_blocks, uint32_t flags, uint32_t* crc_out,
+               uint8_t* ok_out, size_t chunk_bytes, int n_streams) {
+  if (n_blocks == 0) return 0;
+  if (!host_base || !offsets || !lengths) return NOVA_E_INVAL;
+  if (chunk_bytes == 0) chunk_bytes = 64ull << 20;
+  n_streams = std::max(1, std::min(n_streams, 8));
+  int err = nova_device_init();
+  if (err) return err;
+  const uint64_t tail = op == kHostVerify ? 5 : 0;  // verify reads the trailer too
+  // chunk boundaries and spans
+  struct Chunk { size_t b0, b1; uint64_t lo, hi; };
+  std::vector<Chunk> chunks;
+  uint64_t span_max = 0;
+  size_t blocks_max = 0;
+  uint64_t glo = ~0ull, ghi = 0;
+  for (size_t b = 0; b < n_blocks;) {
+    Chunk c{b, b, offsets[b], offsets[b] + lengths[b] + tail};
+    while (c.b1 < n_blocks) {
+      const uint64_t lo = std::min(c.lo, offsets[c.b1]);
+      const uint64_t hi = std::max(c.hi, offsets[c.b1] + lengths[c.b1] + tail);
+      if (c.b1 > c.b0 && hi - lo > chunk_bytes) break;
+      c.lo = lo;
+      c.hi = hi;
+      c.b1++;
+    }
+    span_max = std::max(span_max, c.hi - c.lo);
+    blocks_max = std::max(blocks_max, c.b1 - c.b0);
+    glo = std::min(glo, c.lo);
+    ghi = std::max(ghi, c.hi);
+    chunks.push_back(c);
+    b = c.b1;
+  }
+  HostReg hr;
+  if ((err = hr.reg(static_cast<const uint8_t*>(host_base) + glo, ghi - glo))) return err;
+  Streams st;
+  if ((err = st.get(n_streams))) return err;
+  std::vector<Stage> stage(n_streams);
+  PinBuf pres;  // results for the whole batch
+  const size_t res_bytes = op == kHostVerify ? n_blocks : n_blocks * 4;
+  if ((err = pres.ensure(res_bytes))) return err;
+  for (auto& s : stage) {
+    if ((err = s.data.ensure(span_max + 16))) return err;
+    if ((err = s.offs.ensure(blocks_max * 8)) || (err = s.lens.ensure(blocks_max * 4)) ||
+        (err = s.out.ensure(op == kHostVerify ? blocks_max + 4 : blocks_max * 4)) ||
+        (err = s.hoffs.ensure(blocks_max * 8)) || (err = s.hlens.ensure(blocks_max * 4)))
+      return err;
+    if (init && (err = s.init.ensure(blocks_max * 4))) return err;
+  }
+  const uint8_t* hb = static_cast<const uint8_t*>(host_base);
+  int rc = 0;
+  for (size_t k = 0; k < chunks.size() && !rc; k++) {
+    const Chunk& c = chunks[k];
+    const int si = (int)(k % n_streams);
+    Stage& s = stage[si];
+    hipStream_t hs = st.s[si];
+    const size_t m = c.b1 - c.b0;
+    // the stream's previous chunk must be done with the pinned descriptors
+    if (k >= (size_t)n_streams && (rc = (int)hipStreamSynchronize(hs))) break;
+    uint64_t* ho = static_cast<uint64_t*>(s.hoffs.p);
+    for (size_t i = 0; i < m; i++) ho[i] = offsets[c.b0 + i] - c.lo;
+    std::memcpy(s.hlens.p, lengths + c.b0, m * 4);
+    hipError_t e = hipMemcpyAsync(s.data.p, hb + c.lo, c.hi - c.lo, hipMemcpyHostToDevice, hs);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.offs.p, ho, m * 8, hipMemcpyHostToDevice, hs);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.lens.p, s.hlens.p, m * 4, hipMemcpyHostToDevice, hs);
+    if (e == hipSuccess && init)
+      e = hipMemcpyAsync(s.init.p, init + c.b0, m * 4, hipMemcpyHostToDevice, hs);
+    if (e != hipSuccess) { rc = (int)e; break; }
+    const uint64_t* doffs = static_cast<const uint64_t*>(s.offs.p);
+    const uint32_t* dlens = static_cast<const uint32_t*>(s.lens.p);
+    if (op == kHostVerify) {
+      rc = nova_sstable_verify_blocks(s.data.p, doffs, dlens, m, static_cast<uint8_t*>(s.out.p),
+                                      nullptr, hs);
+      if (!rc) rc = (int)hipMemcpyAsync(static_cast<uint8_t*>(pres.p) + c.b0, s.out.p, m,
+                                        hipMemcpyDeviceToHost, hs);
+    } else {
+      // trailers: CRCs (type byte appended, masked) come back; the host writes
+      // the 5 trailer bytes into its own image
+      const uint32_t f = op == kHostTrailers
+                             ? ((flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT |
+                                (flags & NOVA_CRC32C_HINT_LARGE_BLOCKS))
+                             : flags;
+      rc = nova_crc32c_batch(s.data.p, doffs, dlens,
+                             init ? static_cast<const uint32_t*>(s.init.p) : nullptr,
+                             static_cast<uint32_t*>(s.out.p), m, f, hs);
+      if (!rc) rc = (int)hipMemcpyAsync(static_cast<uint32_t*>(pres.p) + c.b0, s.out.p, m * 4,
+                                        hipMemcpyDeviceToHost, hs);
+    }
+  }
+  const int rs = st.sync();
+  if (!rc) rc = rs;
+  if (rc) return rc;
+  if (op == kHostVerify) {
+    std::memcpy(ok_out, pres.p, n_blocks);
+  } else if (op == kHostCrc) {
+    std::memcpy(crc_out, pres.p, n_blocks * 4);
+  } else {  // table/table_builder.cc:200-206, ltc/stoc_file_client_impl.cpp:713-719
+    uint8_t* img = static_cast<uint8_t*>(const_cast<void*>(host_base));
+    const uint32_t* m = static_cast<const uint32_t*>(pres.p);
+    const uint8_t type = (uint8_t)((flags >> 8) & 0xffu);
+    const bool quirk = (flags & NOVA_TRAILER_TB_QUIRK) != 0;
+    for (size_t i = 0; i < n_blocks; i++) {
+      uint8_t* t = img + offsets[i] + lengths[i];
+      t[0] = type;
+      t[1] = (uint8_t)m[i];
+      t[2] = (uint8_t)(m[i] >> 8);
+      t[3] = (uint8_t)(m[i] >> 16);
+      t[4] = quirk ? (uint8_t)'!' : (uint8_t)(m[i] >> 24);
+    }
+  }
+  return 0;
+}
+
+// ---- port hook ----------------------------------------------------------------
+std::atomic<uint64_t> g_hook_host{0}, g_hook_device{0}, g_hook_fallback{0};
+
+size_t env_size(const char* name, size_t def) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return def;
+  char* end = nullptr;
+  const unsigned long long x = std::strtoull(v, &end, 0);
+  return end && *end == 0 ? (size_t)x : def;
+}
+
+// Below this size Extend stays on the host: a 1 MiB buffer is ~40 us on one
+// core (SSE4.2), about the cost of H2D + a launch + D2H + a sync.
+size_t hook_min_bytes() {
+  static const size_t v = env_size("NOVA_HOOK_MIN_BYTES", 1u << 20);
+  return v;
+}
+// Largest device staging buffer the hook allocates (a larger call runs on the host).
+size_t hook_max_staging() {
+  static const size_t v = env_size("NOVA_HOOK_MAX_STAGING", 1ull << 30);
+  return v;
+}
+
+// Per-thread device state of the hook: one pooled stream, staging buffers.
+struct HookState {
+  hipStream_t s = nullptr;
+  int dev = -1;
+  DevBuf dbuf, dout;
+  ~HookState() {
+    if (s) {
+      (void)hipStreamSynchronize(s);
+      release_stream(dev, s);
+    }
+  }
+};
+
+// Extend(crc, buf, size) on the GPU: the buffer is cut into 4 KiB sub-blocks
+// whose linear ("raw") CRCs the kernels compute; the host folds them with the
+// GF(2) shift.  Returns nonzero on any failure (the caller falls back).
+int device_extend(uint32_t crc, const char* buf, size_t size, uint32_t* out) {
+  if (size > hook_max_staging()) return NOVA_E_NOMEM;
+  if (nova_device_init() != 0) return NOVA_E_NODEV;
+  thread_local HookState hs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return NOVA_E_NODEV;
+  }
+  if (!hs.s || hs.dev != dev) {
+    if (hs.s) release_stream(hs.dev, hs.s);
+    hs.s = acquire_stream(&hs.dev);
+    if (!hs.s) return NOVA_E_NODEV;
+    hs.dbuf.reset();
+    hs.dout.reset();
+  }
+  constexpr uint32_t kSub = 4096;
+  const size_t nsub = (size + kSub - 1) / kSub;
+  const size_t full = size / kSub;
+  if (hs.dbuf.ensure(size) || hs.dout.ensure(nsub * 4)) return NOVA_E_NOMEM;
+  std::vector<uint32_t> raw(nsub);
+  int rc = (int)hipMemcpyAsync(hs.dbuf.p, buf, size, hipMemcpyHostToDevice, hs.s);
+  if (!rc && full)
+    rc = nova_crc32c_batch_strided(hs.dbuf.p, kSub, kSub, full, nullptr,
+                                   static_cast<uint32_t*>(hs.dout.p), NOVA_CRC32C_RAW, hs.s);
+  const uint32_t tail = (uint32_t)(size - full * kSub);
+  if (!rc && tail)
+    rc = nova_crc32c_batch_strided(static_cast<uint8_t*>(hs.dbuf.p) + full * kSub, tail, tail, 1,
+                                   nullptr, static_cast<uint32_t*>(hs.dout.p) + full,
+                                   NOVA_CRC32C_RAW, hs.s);
+  if (!rc) rc = (int)hipMemcpyAsync(raw.data(), hs.dout.p, nsub * 4, hipMemcpyDeviceToHost, hs.s);
+  const hipError_t se = hipStreamSynchronize(hs.s);
+  if (!rc && se != hipSuccess) rc = (int)se;
+  if (rc) {
+    (void)hipGetLastError();
+    return rc;
+  }
+  // raw(D) = fold of sub-block raws; Extend(crc, D) = ~(M_size(~crc) ^ raw(D)).
+  using namespace nova::gf2;
+  const Lin m_sub = shift_bytes(kSub);
+  uint32_t acc = 0;
+  for (size_t i = 0; i < full; i++) acc = m_sub(acc) ^ raw[i];
+  if (tail) acc = shift_bytes(tail)(acc) ^ raw[full];
+  *out = ~(shift_bytes(size)(~crc) ^ acc);
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -72,26 +401,21 @@ int nova_crc32c_stream_host(const void* host_base, uint64_t stride, uint32_t len
   if (n_blocks == 0) return 0;
   if (!host_base || !host_out || stride < len) return NOVA_E_INVAL;
   if (chunk_blocks == 0) chunk_blocks = 4096;
-  if (n_streams < 1) n_streams = 1;
-  if (n_streams > 8) n_streams = 8;
+  n_streams = std::max(1, std::min(n_streams, 8));
   int err = nova_device_init();
   if (err) return err;
 
   const size_t span = (n_blocks - 1) * stride + len;
-  bool registered = false;
-  if (!is_pinned(host_base)) {
-    if (hipHostRegister(const_cast<void*>(host_base), span, hipHostRegisterDefault) != hipSuccess)
-      return NOVA_E_NOMEM;
-    registered = true;
-  }
+  HostReg hr;
+  if ((err = hr.reg(host_base, span))) return err;
   const size_t chunk_span = (chunk_blocks - 1) * stride + len;
-  std::vector<hipStream_t> streams(n_streams, nullptr);
+  Streams st;
+  if ((err = st.get(n_streams))) return err;
   std::vector<DevBuf> dbuf(n_streams), dout(n_streams);
   PinBuf pout;
   int rc = pout.ensure(n_blocks * 4);
   for (int s = 0; s < n_streams && !rc; s++) {
-    if (hipStreamCreateWithFlags(&streams[s], hipStreamNonBlocking) != hipSuccess) rc = NOVA_E_NODEV;
-    if (!rc) rc = dbuf[s].ensure(chunk_span);
+    rc = dbuf[s].ensure(chunk_span);
     if (!rc) rc = dout[s].ensure(chunk_blocks * 4);
   }
   const uint8_t* hb = static_cast<const uint8_t*>(host_base);
@@ -101,59 +425,73 @@ int nova_crc32c_stream_host(const void* host_base, uint64_t stride, uint32_t len
     const int s = (int)(k % n_streams);
     const size_t bytes = (m - 1) * stride + len;
     hipError_t e = hipMemcpyAsync(dbuf[s].p, hb + b0 * stride, bytes, hipMemcpyHostToDevice,
-                                  streams[s]);
+                                  st.s[s]);
     if (e != hipSuccess) { rc = (int)e; break; }
     rc = nova_crc32c_batch_strided(dbuf[s].p, stride, len, m, nullptr,
-                                   static_cast<uint32_t*>(dout[s].p), flags, streams[s]);
+                                   static_cast<uint32_t*>(dout[s].p), flags, st.s[s]);
     if (rc) break;
     e = hipMemcpyAsync(static_cast<uint32_t*>(pout.p) + b0, dout[s].p, m * 4,
-                       hipMemcpyDeviceToHost, streams[s]);
+                       hipMemcpyDeviceToHost, st.s[s]);
     if (e != hipSuccess) rc = (int)e;
   }
-  for (int s = 0; s < n_streams; s++) {
-    if (streams[s]) {
-      hipError_t e = hipStreamSynchronize(streams[s]);
-      if (!rc && e != hipSuccess) rc = (int)e;
-      (void)hipStreamDestroy(streams[s]);
-    }
-  }
+  const int rs = st.sync();
+  if (!rc) rc = rs;
   if (!rc) std::memcpy(host_out, pout.p, n_blocks * 4);
-  if (registered) (void)hipHostUnregister(const_cast<void*>(host_base));
+  return rc;
+}
+
+int nova_crc32c_batch_host(const void* host_base, const uint64_t* offsets, const uint32_t* lengths,
+                           const uint32_t* init_or_null, uint32_t* out_crc, size_t n_blocks,
+                           uint32_t flags, size_t chunk_bytes, int n_streams) {
+  if (n_blocks && !out_crc) return NOVA_E_INVAL;
+  return host_batch(kHostCrc, host_base, offsets, lengths, init_or_null, n_blocks, flags, out_crc,
+                    nullptr, chunk_bytes, n_streams);
+}
+
+int nova_sstable_write_trailers_host(void* host_buf, const uint64_t* offsets, const uint32_t* sizes,
+                                     size_t n_blocks, uint32_t flags, size_t chunk_bytes,
+                                     int n_streams) {
+  return host_batch(kHostTrailers, host_buf, offsets, sizes, nullptr, n_blocks, flags, nullptr,
+                    nullptr, chunk_bytes, n_streams);
+}
+
+int nova_sstable_verify_blocks_host(const void* host_buf, const uint64_t* offsets,
+                                    const uint32_t* sizes, size_t n_blocks, uint8_t* ok_out,
+                                    uint32_t* n_bad_out, size_t chunk_bytes, int n_streams) {
+  if (n_blocks && !ok_out) return NOVA_E_INVAL;
+  const int rc = host_batch(kHostVerify, host_buf, offsets, sizes, nullptr, n_blocks, 0, nullptr,
+                            ok_out, chunk_bytes, n_streams);
+  if (!rc && n_bad_out) {
+    uint32_t bad = 0;
+    for (size_t i = 0; i < n_blocks; i++) bad += ok_out[i] ? 0u : 1u;
+    *n_bad_out = bad;
+  }
   return rc;
 }
 
 uint32_t nova_port_accelerated_crc32c(uint32_t crc, const char* buf, size_t size) {
-  // Contract of port::AcceleratedCRC32C: the extended CRC, or 0 = cannot accelerate.
+  // Contract of port::AcceleratedCRC32C: the extended CRC.  Once the reference
+  // adopts the hook (util/crc32c.cc:487-491) every Extend() comes here, so the
+  // hook never answers "cannot accelerate" (0) with a wrong CRC: small buffers
+  // and any GPU failure take the host Extend.
   if (size == 0) return crc;
-  if (!buf || nova_device_init() != 0) return 0;
-  constexpr uint32_t kSub = 4096;
-  const size_t nsub = (size + kSub - 1) / kSub;
-  const size_t full = size / kSub;
-  thread_local DevBuf dbuf, dout;
-  if (dbuf.ensure(size) || dout.ensure(nsub * 4)) return 0;
-  hipStream_t s = nullptr;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return 0;
-  std::vector<uint32_t> raw(nsub);
-  int rc = (int)hipMemcpyAsync(dbuf.p, buf, size, hipMemcpyHostToDevice, s);
-  if (!rc && full)
-    rc = nova_crc32c_batch_strided(dbuf.p, kSub, kSub, full, nullptr,
-                                   static_cast<uint32_t*>(dout.p), NOVA_CRC32C_RAW, s);
-  const uint32_t tail = (uint32_t)(size - full * kSub);
-  if (!rc && tail)
-    rc = nova_crc32c_batch_strided(static_cast<uint8_t*>(dbuf.p) + full * kSub, tail, tail, 1,
-                                   nullptr, static_cast<uint32_t*>(dout.p) + full,
-                                   NOVA_CRC32C_RAW, s);
-  if (!rc) rc = (int)hipMemcpyAsync(raw.data(), dout.p, nsub * 4, hipMemcpyDeviceToHost, s);
-  if (!rc) rc = (int)hipStreamSynchronize(s);
-  (void)hipStreamDestroy(s);
-  if (rc) return 0;
-  // raw(D) = fold of sub-block raws; Extend(crc, D) = ~(M_size(~crc) ^ raw(D)).
-  using namespace nova::gf2;
-  const Lin m_sub = shift_bytes(kSub);
-  uint32_t acc = 0;
-  for (size_t i = 0; i < full; i++) acc = m_sub(acc) ^ raw[i];
-  if (tail) acc = shift_bytes(tail)(acc) ^ raw[full];
-  return ~(shift_bytes(size)(~crc) ^ acc);
+  if (buf && size >= hook_min_bytes()) {
+    uint32_t out = 0;
+    if (device_extend(crc, buf, size, &out) == 0) {
+      g_hook_device.fetch_add(1, std::memory_order_relaxed);
+      return out;
+    }
+    g_hook_fallback.fetch_add(1, std::memory_order_relaxed);
+  } else {
+    g_hook_host.fetch_add(1, std::memory_order_relaxed);
+  }
+  return nova_crc32c_extend(crc, buf, size);
+}
+
+void nova_port_stats(uint64_t* host_calls, uint64_t* device_calls, uint64_t* fallback_calls) {
+  if (host_calls) *host_calls = g_hook_host.load();
+  if (device_calls) *device_calls = g_hook_device.load();
+  if (fallback_calls) *fallback_calls = g_hook_fallback.load();
 }
 
 }  // extern "C"

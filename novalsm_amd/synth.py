@@ -36,3 +36,61 @@ def splitmix64_bytes(seed: int, nbytes: int, first_byte: int = 0) -> np.ndarray:
     raw = words.view(np.uint8)
     s = first_byte - 8 * w0
     return raw[s:s + nbytes].copy()
+
+
+# ---- log images -------------------------------------------------------------
+LOG_BLOCK = 32768   # db/log_format.h:27 kBlockSize
+LOG_HEADER = 7      # db/log_format.h:30 kHeaderSize
+FULL, FIRST, MIDDLE, LAST = 1, 2, 3, 4  # db/log_format.h:14-24
+
+
+def log_layout(payload_lens, block_offset: int = 0):
+    """Physical layout of a log file written by log::Writer::AddRecord
+    (db/log_writer.cc:53-97): logical records of the given payload sizes are
+    cut into physical records [crc 4][len 2][type 1][payload] that never cross
+    a 32 KiB block; a block remainder shorter than a header becomes a zero
+    trailer.  Returns (offsets u64, lengths u32, types u8, trailer ranges
+    [(start, end)], total bytes); offsets are from the file start, which sits
+    block_offset bytes into its first block (Writer(dest, dest_length))."""
+    offs, lens, types, pads = [], [], [], []
+    pos = 0
+    bo = block_offset % LOG_BLOCK
+    for left in (int(x) for x in payload_lens):
+        begin = True
+        while True:
+            leftover = LOG_BLOCK - bo
+            if leftover < LOG_HEADER:  # :64-73 switch to a new block
+                if leftover > 0:
+                    pads.append((pos, pos + leftover))
+                    pos += leftover
+                bo = 0
+            avail = LOG_BLOCK - bo - LOG_HEADER
+            frag = min(left, avail)
+            end = frag == left
+            t = FULL if (begin and end) else FIRST if begin else LAST if end else MIDDLE
+            offs.append(pos)
+            lens.append(frag)
+            types.append(t)
+            pos += LOG_HEADER + frag
+            bo += LOG_HEADER + frag
+            left -= frag
+            begin = False
+            if left <= 0:  # an empty record still emits one zero-length fragment
+                break
+    return (np.array(offs, np.uint64), np.array(lens, np.uint32), np.array(types, np.uint8),
+            pads, pos)
+
+
+def log_image(seed: int, payload_lens, block_offset: int = 0):
+    """A host log image over the layout above: splitmix64(seed) payload bytes,
+    header length/type fields set, trailers zero, CRC fields NOT yet written.
+    Returns (image u8, offsets, lengths, types)."""
+    offs, lens, types, pads, total = log_layout(payload_lens, block_offset)
+    img = splitmix64_bytes(seed, total)
+    o = offs.astype(np.int64)
+    img[o + 4] = (lens & 0xFF).astype(np.uint8)
+    img[o + 5] = (lens >> 8).astype(np.uint8)
+    img[o + 6] = types
+    for a, b in pads:
+        img[a:b] = 0
+    return img, offs, lens, types

@@ -224,22 +224,26 @@ int oracle_log_verify(const uint8_t *rec) {
   return oracle_unmask(read_le32(rec)) == oracle_value(rec + 6, 1 + len);
 }
 
-/* db/log_reader.cc:225-262 ReadPhysicalRecord's per-record checks, in order,
+/* db/log_reader.cc:196-262 ReadPhysicalRecord's per-record checks, in order,
  * for the record whose header starts at buf+off in a log image of buf_len
  * bytes that begins on a 32 KiB log-block boundary (db/log_format.h:27,
- * kBlockSize): the record must end inside its log block and the image
- * ("bad record length", :230-240), a kZeroType record of length 0 is skipped
- * unreported (:243-249), else the CRC is checked ("checksum mismatch",
- * :251-262).  Returns 1 ok, 0 checksum mismatch, 2 bad record length,
- * 3 zero record. */
+ * kBlockSize).  The reader holds the rest of the current block in buffer_
+ * (a short read, i.e. the file's last partial block, sets eof_):
+ *   - header or payload past the block (:197-221, :228-239): with eof_ the
+ *     record was cut by the end of the file -> 4, reported as EOF, not as a
+ *     corruption; otherwise "bad record length" -> 2;
+ *   - a kZeroType record of length 0 is skipped unreported (:241-247) -> 3;
+ *   - else the CRC is checked (:249-262): 1 ok, 0 "checksum mismatch".
+ * (The NOVA_LOG_* codes of include/nova_crc32c.h.) */
 int oracle_log_check(const uint8_t *buf, uint64_t buf_len, uint64_t off) {
   const uint64_t kBlock = 32768, kHeader = 7;
   uint64_t end = (off / kBlock + 1) * kBlock;
   if (end > buf_len) end = buf_len;
-  if (off + kHeader > end) return 2;
+  const int cut = (end == buf_len && buf_len % kBlock != 0) ? 4 : 2;  /* eof_ : bad length */
+  if (off + kHeader > end) return cut;
   const uint8_t *h = buf + off;
   uint32_t len = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
-  if (off + kHeader + len > end) return 2;
+  if (off + kHeader + len > end) return cut;
   if (h[6] == 0 && len == 0) return 3;
   return oracle_unmask(read_le32(h)) == oracle_value(h + 6, 1 + len) ? 1 : 0;
 }

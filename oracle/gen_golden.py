@@ -21,7 +21,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
-from novalsm_amd.synth import splitmix64_bytes  # noqa: E402
+from novalsm_amd.synth import log_image, splitmix64_bytes  # noqa: E402
 
 REF_SO = os.path.join(HERE, "_ref", "libref_crc32c.so")
 
@@ -133,26 +133,29 @@ def main() -> None:
     out["packed"] = {"seed": seed, "total": total, "offsets": offs, "sizes": sizes,
                      "crc": crcs, "tb_trailer_hex": tb, "stoc_trailer_hex": stoc}
 
-    # 7. a write-ahead/MANIFEST log image: records [LE32 masked crc][LE16 len]
-    # [type][payload] whose crc is db/log_writer.cc:112-114:
-    # Mask(Extend(type_crc[t], payload, len)), type_crc[t] = Value(&t, 1) (:16-21).
+    # 7. a write-ahead/MANIFEST log image as log::Writer::AddRecord lays it out
+    # (db/log_writer.cc:53-97, novalsm_amd/synth.log_layout): 300 logical
+    # records (a few longer than a 32 KiB block, so FIRST/MIDDLE/LAST
+    # fragments and zero block trailers occur), each physical record's crc is
+    # db/log_writer.cc:105-111: Mask(Extend(type_crc[t], payload, len)),
+    # type_crc[t] = Value(&t, 1) (:16-21).
     r = np.random.default_rng(4)
-    recs, pos = [], 0
+    plens = []
     for i in range(300):
-        ln = int(r.integers(0, 3000)) if i % 11 else int(r.integers(0, 4))
-        t = int(r.integers(1, 5))
-        recs.append((pos, ln, t))
-        pos += 7 + ln
-    logbuf = bytearray(splitmix64_bytes(6, pos).tobytes())
+        if i % 11 == 0:
+            plens.append(int(r.integers(0, 4)))
+        elif i % 97 == 5:
+            plens.append(int(r.integers(33000, 70000)))
+        else:
+            plens.append(int(r.integers(0, 3000)))
+    logbuf, loffs, llens, ltypes = log_image(6, plens)
     log_crc = []
-    for o, ln, t in recs:
-        logbuf[o + 4] = ln & 0xff
-        logbuf[o + 5] = ln >> 8
-        logbuf[o + 6] = t
-        c = ref.ref_mask(ext(ext(0, bytes([t])), bytes(logbuf[o + 7:o + 7 + ln])))
+    for o, ln, t in zip(loffs.tolist(), llens.tolist(), ltypes.tolist()):
+        c = ref.ref_mask(ext(ext(0, bytes([t])), logbuf[o + 7:o + 7 + ln].tobytes()))
         log_crc.append(c)
-        logbuf[o:o + 4] = c.to_bytes(4, "little")
-    out["log"] = {"seed": 6, "total": pos, "records": [[o, ln, t] for o, ln, t in recs],
+    out["log"] = {"seed": 6, "payload_lens": plens, "total": int(logbuf.size),
+                  "records": [[o, ln, t] for o, ln, t in zip(loffs.tolist(), llens.tolist(),
+                                                             ltypes.tolist())],
                   "header_crc": log_crc}
 
     # 8. BASELINE config 1 sample: 1024 x 4 KiB blocks, splitmix64 seed 1

@@ -78,8 +78,8 @@ class Oracle:
         return out
 
     def log_check(self, buf: np.ndarray, rec_offsets, buf_len=None) -> np.ndarray:
-        """db/log_reader.cc:225-262 per record: 1 ok, 0 checksum mismatch,
-        2 bad record length, 3 zero record (skipped)."""
+        """db/log_reader.cc:196-262 per record: 1 ok, 0 checksum mismatch,
+        2 bad record length, 3 zero record (skipped), 4 cut by end of file."""
         n = buf.size if buf_len is None else buf_len
         return np.array([self.lib.oracle_log_check(buf.ctypes.data, n, int(o))
                          for o in rec_offsets], dtype=np.uint8)

@@ -24,17 +24,10 @@ def torch_gpu():
 
 @pytest.fixture(autouse=True)
 def _reset_tuning():
+    # product-library tuning (per thread); the diagnostics library's knobs are
+    # reset when a test's C.diagnostics() block exits
     yield
     C.set_tuning(0, 0)
-    L = C.load()
-    L.nova_diag_set_chunk_blocks(0)
-    L.nova_diag_set_static_pct(-1)
-    L.nova_diag_set_blocks_per_group(0)
-    L.nova_diag_set_stream_waves(0)
-    L.nova_diag_set_variant(0)
-    L.nova_diag_set_variable_kernel(0)
-    L.nova_diag_set_rounds_sort(2)
-    L.nova_diag_set_trailer_single_pass(0)
 
 
 def dev(torch, arr, dtype=None):
@@ -166,12 +159,16 @@ def test_variable_batch_vs_oracle(torch_gpu, oracle, lanes, seg, chunk, steal, w
     """Variable-length batch through the units kernel, across unit sizes and
     the claim scheduler's chunk size / steal bound."""
     torch = torch_gpu
-    C.set_tuning(lanes, seg)
-    L = C.load()
-    L.nova_diag_set_chunk_blocks(chunk)
-    L.nova_diag_set_static_pct(steal)
-    L.nova_diag_set_stream_waves(waves)
-    L.nova_diag_set_variant(var)
+    with C.diagnostics() as L:
+        C.set_tuning(lanes, seg)
+        L.nova_diag_set_chunk_blocks(chunk)
+        L.nova_diag_set_static_pct(steal)
+        L.nova_diag_set_stream_waves(waves)
+        L.nova_diag_set_variant(var)
+        _variable_batch_checks(torch, oracle, lanes, seg)
+
+
+def _variable_batch_checks(torch, oracle, lanes, seg):
     rng = np.random.default_rng(lanes * 1000 + seg)
     n = 1500
     cls = rng.choice([1, 3, 4, 17, 600, 4096, 16384, 65536], n, p=[.03, .03, .04, .1, .1, .4,
@@ -259,11 +256,196 @@ def test_stream_host_matches_device(torch_gpu, oracle):
 
 
 def test_accelerated_hook(torch_gpu, oracle):
-    # port::AcceleratedCRC32C self-test: util/crc32c.cc:477-485
+    """port::AcceleratedCRC32C self-test (util/crc32c.cc:477-485), then sizes on
+    both sides of NOVA_HOOK_MIN_BYTES (1 MiB): the 1-byte type-byte Extend of
+    table/table_builder.cc:203 and a 4 KiB block never launch a kernel; large
+    buffers run on the GPU."""
     assert C.AcceleratedCRC32C(0, b"TestCRCBuffer") == 0xDCBC59FA
-    for n, init in [(1, 0), (4096, 5), (4097, 0xFFFFFFFF), (1 << 20, 0x1234), (3 << 20 | 77, 9)]:
+    s0 = C.port_stats()
+    for n, init in [(1, 0), (4096, 5), (4097, 0xFFFFFFFF)]:
         d = splitmix64_bytes(n, n).tobytes()
         assert C.AcceleratedCRC32C(init, d) == oracle.extend(init, d)
+    s1 = C.port_stats()
+    assert s1["device"] == s0["device"] and s1["host"] - s0["host"] == 3
+    for n, init in [(1 << 20, 0x1234), (3 << 20 | 77, 9)]:
+        d = splitmix64_bytes(n, n).tobytes()
+        assert C.AcceleratedCRC32C(init, d) == oracle.extend(init, d)
+    s2 = C.port_stats()
+    assert s2["device"] - s1["device"] == 2 and s2["fallback"] == s1["fallback"]
+
+
+def test_accelerated_hook_device_failure_falls_back(torch_gpu, oracle, tmp_path):
+    """A device-side failure (here: a staging cap below the buffer size, set
+    before the process's first hook call) gives Extend's value, not 0."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from novalsm_amd import crc32c as C\n"
+            "from novalsm_amd.synth import splitmix64_bytes\n"
+            "d = splitmix64_bytes(3, 2 << 20).tobytes()\n"
+            "print(C.AcceleratedCRC32C(7, d), C.port_stats()['fallback'], C.port_stats()['device'])\n"
+            ) % (str(__import__('pathlib').Path(__file__).resolve().parents[1]),)
+    env = dict(__import__('os').environ, NOVA_HOOK_MAX_STAGING=str(1 << 20))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    crc, fb, devc = (int(x) for x in r.stdout.split()[-3:])
+    d = splitmix64_bytes(3, 2 << 20).tobytes()
+    assert crc == oracle.extend(7, d) and fb == 1 and devc == 0
+
+
+@pytest.mark.timeout(300)
+def test_no_device_memory_growth(torch_gpu, oracle):
+    """the hook and the host-streamed paths reuse pooled streams,
+    so thousands of calls from several threads leave the claim-counter slot
+    count and free device memory flat; nova_stream_release frees a caller
+    stream's slot."""
+    torch = torch_gpu
+    import threading
+    d = splitmix64_bytes(4, (1 << 20) + 5).tobytes()
+    want = oracle.extend(0, d)
+    host = torch.from_numpy(splitmix64_bytes(6, 64 * 4096)).pin_memory()
+    C.AcceleratedCRC32C(0, d)
+    C.stream_host(host, 4096, 4096, 64, chunk_blocks=16, n_streams=3)
+    torch.cuda.synchronize()
+    slots0, free0 = C.stream_slots(), torch.cuda.mem_get_info()[0]
+    errors = []
+
+    def work():
+        try:
+            for _ in range(150):
+                assert C.AcceleratedCRC32C(0, d) == want
+            for _ in range(20):
+                C.stream_host(host, 4096, 4096, 64, chunk_blocks=16, n_streams=3)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+    th = [threading.Thread(target=work) for _ in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    torch.cuda.synchronize()
+    # 4 threads: at most 4 hook streams + 3 x 4 stream_host streams in the pool
+    assert C.stream_slots() <= slots0 + 16
+    s = torch.cuda.Stream()
+    C.batch_strided(dev(torch, splitmix64_bytes(1, 4096 * 8)), 4096, 4096, 8, stream=s)
+    n1 = C.stream_slots()
+    C.stream_release(s)
+    assert C.stream_slots() == n1 - 1
+    for _ in range(300):  # more hook calls on the warm pool: no growth at all
+        C.AcceleratedCRC32C(0, d)
+    torch.cuda.synchronize()
+    assert C.stream_slots() == n1 - 1
+    assert torch.cuda.mem_get_info()[0] >= free0 - (64 << 20)
+
+
+def test_shared_stream_trailer_threads(torch_gpu, oracle):
+    """several host threads writing trailers of large batches (the
+    two-pass path, > 6144 blocks) on the SAME stream (the default one) each get
+    their own CRC scratch: every trailer matches the oracle."""
+    torch = torch_gpu
+    import threading
+    n = 9000
+    imgs, descs = [], []
+    for t in range(4):
+        rng = np.random.default_rng(300 + t)
+        lens = rng.integers(1, 600, n).astype(np.uint32)
+        offs = np.zeros(n, np.uint64)
+        offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5))
+        host = splitmix64_bytes(40 + t, int(offs[-1]) + int(lens[-1]) + 5 + 16)
+        imgs.append((host, dev(torch, host)))
+        descs.append((offs, lens, dev(torch, offs, torch.int64), dev(torch, lens, torch.int32)))
+    torch.cuda.synchronize()
+    errors = []
+
+    def work(t):
+        try:
+            for _ in range(5):
+                C.write_trailers(imgs[t][1], descs[t][2], descs[t][3], 0, True,
+                                 stream=torch.cuda.default_stream())
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for t in range(4):
+        host, dbuf = imgs[t]
+        offs, lens = descs[t][0], descs[t][1]
+        got = dbuf.cpu().numpy()
+        for i in range(0, n, 7):
+            o, ln = int(offs[i]), int(lens[i])
+            assert oracle.trailer(host[o:o + ln].tobytes(), 0, True) == got[o + ln:o + ln + 5].tobytes()
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_resident_sstable_paths(torch_gpu, oracle, pinned):
+    """an SSTable image in host memory (the Format() buffer /
+    ReadAll() slab, ltc/stoc_file_client_impl.cpp:183-377, :843-882) -- CRCs,
+    trailers and verify through H2D -> kernel -> D2H chunks, equal to the
+    device paths and the oracle; descriptors partly out of address order."""
+    torch = torch_gpu
+    rng = np.random.default_rng(11)
+    n = 5000
+    lens = (4096 + rng.integers(0, 256, n)).astype(np.uint32)
+    lens[rng.integers(0, n, 50)] = rng.integers(0, 40, 50)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5))
+    total = int(offs[-1]) + int(lens[-1]) + 5
+    img0 = splitmix64_bytes(12, total)
+    perm = np.arange(n)
+    perm[100:200] = perm[100:200][::-1]  # a reversed run: spans still bounded
+    po, pl = offs[perm], lens[perm]
+    img = torch.from_numpy(img0.copy())
+    if pinned:
+        img = img.pin_memory()
+    got = C.batch_host(img, po, pl, chunk_bytes=3 << 20, n_streams=3)
+    assert np.array_equal(got, oracle.batch(img0, po, pl, None))
+    C.write_trailers_host(img, po, pl, 0, True, chunk_bytes=3 << 20)
+    want = img0.copy()
+    for i in range(n):
+        o, ln = int(offs[i]), int(lens[i])
+        want[o + ln:o + ln + 5] = np.frombuffer(oracle.trailer(img0[o:o + ln].tobytes(), 0, True),
+                                                np.uint8)
+    assert np.array_equal(img.numpy(), want)
+    C.write_trailers_host(img, po, pl, 0, False, chunk_bytes=1 << 20, n_streams=2)
+    ok, nbad = C.verify_blocks_host(img, po, pl, chunk_bytes=2 << 20)
+    assert ok.all() and nbad == 0
+    victims = [3, 150, 4999]
+    for v in victims:
+        img[int(offs[perm[v]])] ^= 1 if lens[perm[v]] else 0
+        if not lens[perm[v]]:
+            img[int(offs[perm[v]]) + 1] ^= 1
+    ok, nbad = C.verify_blocks_host(img, po, pl)
+    assert sorted(np.nonzero(ok == 0)[0].tolist()) == victims and nbad == 3
+    dok, _ = C.verify_blocks(img.cuda(), dev(torch, po, torch.int64), dev(torch, pl, torch.int32))
+    assert np.array_equal(dok.cpu().numpy(), ok)
+
+
+def test_device_batches_validate_arguments(torch_gpu):
+    """wrong descriptor dtypes, non-contiguous views and CPU tensors
+    are refused before the C-ABI (the kernels would read them as raw u64/u32)."""
+    torch = torch_gpu
+    data = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    offs = torch.zeros(4, dtype=torch.int64, device="cuda")
+    lens = torch.full((4,), 16, dtype=torch.int32, device="cuda")
+    C.batch(data, offs, lens)  # the good case
+    for args in [(data, offs.to(torch.int32), lens), (data, offs, lens.to(torch.int64)),
+                 (data.view(torch.int32), offs, lens),
+                 (data, torch.zeros(8, dtype=torch.int64, device="cuda")[::2], lens),
+                 (data, offs.cpu(), lens)]:
+        with pytest.raises(C.NovaError):
+            C.batch(*args)
+    with pytest.raises(C.NovaError):
+        C.batch(data, offs, lens, out=torch.empty(4, dtype=torch.int64, device="cuda"))
+    with pytest.raises(C.NovaError):
+        C.verify_blocks(data, offs, lens, ok=torch.empty(4, dtype=torch.int32, device="cuda"))
+    with pytest.raises(C.NovaError):
+        C.log_write_crcs(data, offs.to(torch.int32))
 
 
 def test_determinism(torch_gpu):
@@ -364,11 +546,7 @@ def test_stream_kernel_shapes(torch_gpu, oracle, length, n):
     (8, 2, 8, 16, 2)])
 def test_stream_kernel_tuning_variants(torch_gpu, oracle, lanes, bpg, steal, waves, var):
     torch = torch_gpu
-    import ctypes
-    L = C.load()
-    L.nova_diag_set_static_pct.argtypes = [ctypes.c_int]
-    L.nova_diag_set_blocks_per_group.argtypes = [ctypes.c_int]
-    try:
+    with C.diagnostics() as L:
         C.set_tuning(lanes, 0)
         L.nova_diag_set_blocks_per_group(bpg)
         L.nova_diag_set_static_pct(steal)
@@ -380,9 +558,6 @@ def test_stream_kernel_tuning_variants(torch_gpu, oracle, lanes, bpg, steal, wav
         out = u32(C.batch_strided(buf, length, length, n))
         want = oracle.batch_strided_mt(buf.cpu().numpy(), length, length, n, threads=8)
         assert np.array_equal(out, want)
-    finally:
-        L.nova_diag_set_blocks_per_group(0)
-        L.nova_diag_set_static_pct(-1)
 
 
 def test_pinned_host_zero_copy(torch_gpu, oracle, golden):
@@ -455,21 +630,14 @@ def test_concurrent_host_threads(torch_gpu, oracle):
             assert np.array_equal(r, want)
 
 
-def _log_image(golden):
-    lg = golden["log"]
-    buf = splitmix64_bytes(lg["seed"], lg["total"]).copy()
-    for (o, ln, t) in lg["records"]:
-        buf[o + 4] = ln & 0xFF
-        buf[o + 5] = ln >> 8
-        buf[o + 6] = t
-    return buf, np.array([r[0] for r in lg["records"]], np.uint64)
-
-
 def test_log_records_write_verify(torch_gpu, golden, oracle):
     """MANIFEST/WAL record CRCs (db/log_writer.cc:99-114,
-    db/log_reader.cc:251-262) against the reference-generated log fixture."""
+    db/log_reader.cc:196-262) against the reference-generated log fixture (a
+    log::Writer layout with FULL/FIRST/MIDDLE/LAST fragments over ~20 blocks),
+    then the reader's per-record statuses against the oracle."""
+    from tests.test_oracle_golden import golden_log_image
     torch = torch_gpu
-    host, offs = _log_image(golden)
+    host, offs = golden_log_image(golden)
     buf = dev(torch, host)
     doffs = dev(torch, offs, torch.int64)
     C.log_write_crcs(buf, doffs)
@@ -477,15 +645,70 @@ def test_log_records_write_verify(torch_gpu, golden, oracle):
     for o, c in zip(offs, golden["log"]["header_crc"]):
         assert int.from_bytes(h[int(o):int(o) + 4].tobytes(), "little") == c
     ok, bad = C.log_verify_records(buf, doffs)
-    assert ok.cpu().numpy().all() and int(bad.item()) == 0
+    assert (ok.cpu().numpy() == C.LOG_OK).all() and int(bad.item()) == 0
     victims = [3, 50, 299]
     for v in victims:
         o = int(offs[v]) + 6  # corrupt the type byte (covered by the crc)
         buf[o] ^= 0x01
     ok, bad = C.log_verify_records(buf, doffs)
-    assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == victims
+    assert sorted(np.nonzero(ok.cpu().numpy() == C.LOG_CHECKSUM_MISMATCH)[0].tolist()) == victims
     assert int(bad.item()) == 3
-    assert np.array_equal(ok.cpu().numpy(), oracle.log_verify(buf.cpu().numpy(), offs))
+    assert np.array_equal(ok.cpu().numpy(), oracle.log_check(buf.cpu().numpy(), offs))
+
+
+@pytest.mark.parametrize("kernel", ["default", "units"])
+def test_log_record_bounds(torch_gpu, golden, oracle, kernel):
+    """ADVICE r01 / db/log_reader.cc:196-247: a record whose length field runs
+    past its 32 KiB block or the image is never read (bad length, counted; or
+    EOF if the image ends inside that block), a type-0 length-0 record is
+    skipped, a header past buf_len is not read; write skips them all.  Status
+    per record equals the oracle's ReadPhysicalRecord restatement."""
+    from tests.test_oracle_golden import golden_log_image
+    torch = torch_gpu
+    host, offs = golden_log_image(golden)
+    oracle.log_write(host, offs)
+    n = len(offs)
+    rng = np.random.default_rng(9)
+    vic = rng.choice(n - 1, 30, replace=False)
+    for k, v in enumerate(vic):
+        o = int(offs[v])
+        if k % 3 == 0:
+            host[o + 5] = 0xFF  # length >= 65280: past any block
+        elif k % 3 == 1:
+            host[o + 4:o + 7] = 0  # zero record
+        else:
+            host[o + 8] ^= 0x80  # payload / CRC mismatch (or a 1-byte record's crc field)
+    want_img = host.copy()
+    cut = host.size - 3  # the image ends inside the last record: EOF for it
+    # plus descriptors past the image: header not read
+    offs_x = np.concatenate([offs, np.array([cut - 2, cut + 100], np.uint64)])
+    buf = dev(torch, np.concatenate([host, np.zeros(256, np.uint8)]))
+    doffs = dev(torch, offs_x, torch.int64)
+    ctx = C.diagnostics() if kernel == "units" else None
+    if ctx:
+        ctx.__enter__()
+        C.set_tuning(16, 4096)  # forced segments: the units kernel's log path
+    try:
+        st, bad = C.log_verify_records(buf, doffs, buf_len=cut)
+        want = oracle.log_check(host, offs_x, buf_len=cut)
+        assert np.array_equal(st.cpu().numpy(), want)
+        assert int(bad.item()) == int(((want == 0) | (want == 2)).sum())
+        assert {0, 1, 2, 3, 4} <= set(want.tolist())
+        # write: recompute every readable record; the rest are left untouched
+        before = buf.cpu().numpy().copy()
+        C.log_write_crcs(buf, doffs, buf_len=cut)
+        got = buf.cpu().numpy()
+        for i, o in enumerate(offs_x.tolist()):
+            o = int(o)
+            if want[i] in (0, 1, 3):  # readable: crc field = Mask(Value(type + payload))
+                ln = int(host[o + 4]) | (int(host[o + 5]) << 8)
+                c = oracle.mask(oracle.value(want_img[o + 6:o + 7 + ln].tobytes()))
+                assert int.from_bytes(got[o:o + 4].tobytes(), "little") == c, i
+            elif o + 4 <= got.size:
+                assert np.array_equal(got[o:o + 4], before[o:o + 4]), i
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
 
 
 @pytest.mark.parametrize("align", [True, False])
@@ -545,15 +768,19 @@ def test_flat_many_blocks(torch_gpu, oracle, kernel, lanes, chunk, waves):
     not in address order), random inits, for every lane count, chunk size,
     wave count, sorted and unsorted rounds."""
     torch = torch_gpu
-    C.set_tuning(lanes, 0)
-    L = C.load()
-    L.nova_diag_set_variable_kernel(kernel)
-    if kernel == 3:  # rounds kernel: "chunk" = chunk blocks * 4 + sort mode (3: per chunk)
-        L.nova_diag_set_rounds_sort(2 if (chunk & 3) == 3 else (chunk & 3))
-        L.nova_diag_set_chunk_blocks(chunk >> 2)
-    else:
-        L.nova_diag_set_chunk_blocks(chunk)
-    L.nova_diag_set_stream_waves(waves)
+    with C.diagnostics() as L:
+        C.set_tuning(lanes, 0)
+        L.nova_diag_set_variable_kernel(kernel)
+        if kernel == 3:  # rounds kernel: "chunk" = chunk blocks * 4 + sort mode (3: per chunk)
+            L.nova_diag_set_rounds_sort(2 if (chunk & 3) == 3 else (chunk & 3))
+            L.nova_diag_set_chunk_blocks(chunk >> 2)
+        else:
+            L.nova_diag_set_chunk_blocks(chunk)
+        L.nova_diag_set_stream_waves(waves)
+        _many_blocks_checks(torch, oracle, lanes, chunk, waves)
+
+
+def _many_blocks_checks(torch, oracle, lanes, chunk, waves):
     rng = np.random.default_rng(1000 + lanes * 7 + chunk + waves)
     n = 120000
     lens = rng.choice([0, 1, 2, 3, 4, 5, 17, 100, 600, 1500, 4096, 9000], n,
@@ -581,24 +808,29 @@ def test_flat_many_blocks(torch_gpu, oracle, kernel, lanes, chunk, waves):
     (2, 8, 16), (2, 4, 17), (2, 16, 64), (3, 0, 0), (3, 2, 0), (3, 4, 0), (3, 16, 0),
     (3, 8, 16), (3, 8, 32), (3, 16, 16), (3, 8, 8)])
 def test_log_many_records(torch_gpu, oracle, kernel, lanes, chunk):
-    """Log record CRC write + verify over a log image with enough records to
-    exercise the header pipeline of the flat kernel's descriptor banks
-    (db/log_writer.cc:99-114, db/log_reader.cc:251-262), every lane count."""
+    """Log record CRC write + verify over a log::Writer image (db/log_writer.cc:
+    53-114) with enough records to exercise every kernel's header pipeline
+    (db/log_reader.cc:249-262), every lane count and chunk size; kernel 0 is
+    the product dispatch, 1-3 force units / flat / rounds (diagnostics build)."""
     torch = torch_gpu
-    C.set_tuning(lanes, 0)
-    C.load().nova_diag_set_chunk_blocks(chunk)
-    C.load().nova_diag_set_variable_kernel(kernel)
+    if kernel == 0:
+        _log_many_checks(torch, oracle, lanes, chunk)
+        return
+    with C.diagnostics() as L:
+        C.set_tuning(lanes, 0)
+        L.nova_diag_set_chunk_blocks(chunk)
+        L.nova_diag_set_variable_kernel(kernel)
+        _log_many_checks(torch, oracle, lanes, chunk)
+
+
+def _log_many_checks(torch, oracle, lanes, chunk):
+    from novalsm_amd.synth import log_image
     rng = np.random.default_rng(77 + lanes + chunk)
     n = 60000
-    plen = rng.integers(0, 700, n).astype(np.uint64)
+    plen = rng.integers(0, 700, n)
     plen[rng.integers(0, n, 200)] = rng.integers(0, 3, 200)  # empty / tiny payloads
-    offs = np.zeros(n, np.uint64)
-    offs[1:] = np.cumsum(plen[:-1] + np.uint64(7))
-    total = int(offs[-1] + plen[-1] + np.uint64(7))
-    host = splitmix64_bytes(lanes + 11, total + 16).copy()
-    host[offs.astype(np.int64) + 4] = (plen & np.uint64(0xFF)).astype(np.uint8)
-    host[offs.astype(np.int64) + 5] = (plen >> np.uint64(8)).astype(np.uint8)
-    host[offs.astype(np.int64) + 6] = rng.integers(1, 5, n).astype(np.uint8)
+    plen[rng.integers(0, n, 20)] = rng.integers(30000, 70000, 20)  # fragmented records
+    host, offs, _, _ = log_image(lanes + 11, plen)
     buf = dev(torch, host)
     doffs = dev(torch, offs, torch.int64)
     C.log_write_crcs(buf, doffs)
@@ -607,12 +839,13 @@ def test_log_many_records(torch_gpu, oracle, kernel, lanes, chunk):
     got = buf.cpu().numpy()
     assert np.array_equal(got, want)
     ok, bad = C.log_verify_records(buf, doffs)
-    assert ok.cpu().numpy().all() and int(bad.item()) == 0
-    victims = rng.choice(n, 25, replace=False)
+    assert (ok.cpu().numpy() == C.LOG_OK).all() and int(bad.item()) == 0
+    victims = rng.choice(len(offs), 25, replace=False)
     for v in victims:
-        buf[int(offs[v]) + 6] ^= 0x02
+        buf[int(offs[v]) + 6] ^= 0x02  # type byte: a FULL/FIRST... record stays readable
     ok, bad = C.log_verify_records(buf, doffs)
-    assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
+    okh = ok.cpu().numpy()
+    assert sorted(np.nonzero(okh == C.LOG_CHECKSUM_MISMATCH)[0].tolist()) == sorted(victims.tolist())
     assert int(bad.item()) == len(victims)
 
 
@@ -638,12 +871,15 @@ def test_large_blocks_hint_same_results(torch_gpu, oracle, mode):
             assert np.array_equal(u32(out), want), hint
     elif mode == "trailers":
         bufs = []
-        for hint, one_pass in ((False, 0), (True, 0), (False, 1)):
-            C.load().nova_diag_set_trailer_single_pass(one_pass)
+        for hint in (False, True):
             buf = dev(torch, host)
             C.write_trailers(buf, do, dl, 0, True, hint_large=hint)
             bufs.append(buf.cpu().numpy())
-        C.load().nova_diag_set_trailer_single_pass(0)
+        with C.diagnostics() as L:  # the single-pass A/B (trailer bytes from the CRC kernel)
+            L.nova_diag_set_trailer_single_pass(1)
+            buf = dev(torch, host)
+            C.write_trailers(buf, do, dl, 0, True)
+            bufs.append(buf.cpu().numpy())
         assert np.array_equal(bufs[0], bufs[1]) and np.array_equal(bufs[0], bufs[2])
         for i in np.linspace(0, n - 1, 40).astype(np.int64):
             o, ln = int(offs[i]), int(lens[i])

@@ -3,7 +3,9 @@
 * leveldb::crc32c::{Extend,Value,Mask,Unmask} mirror (util/crc32c.h) on the
   host scalar path, against the reference-generated golden fixture.
 * libnova_crc32c.so loads and exports every symbol include/nova_crc32c.h
-  declares.
+  declares for the product, and none of the diagnostics-only ones (timing
+  ablations that compute wrong CRCs live in libnova_crc32c_diag.so).
+* The port hook's host fallback, argument validation and dispatch plans.
 """
 import ctypes
 import os
@@ -23,22 +25,39 @@ def lib():
     return C.load(build_if_missing=True)
 
 
-def declared_symbols():
+DIAG_MARK = "---- diagnostics: libnova_crc32c_diag.so ONLY"
+
+
+def declared_symbols(diag: bool = False):
     with open(os.path.join(ROOT, "include", "nova_crc32c.h")) as f:
         src = f.read()
+    i = src.index(DIAG_MARK)
+    src = src[i:] if diag else src[:i]
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(nova_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_every_declared_symbol_is_exported(lib):
     syms = declared_symbols()
-    assert len(syms) >= 18
+    assert len(syms) >= 24
     for s in syms:
         assert hasattr(lib, s), s
 
 
+def test_product_exports_no_diagnostics(lib):
+    """The product .so cannot be switched to a wrong-CRC ablation: no
+    nova_diag_* symbol, and the diagnostics build has all of them."""
+    diag = declared_symbols(diag=True)
+    assert len(diag) >= 10 and all(s.startswith("nova_diag_") for s in diag)
+    for s in diag:
+        assert not hasattr(lib, s), s
+    D = C.load_diag()
+    for s in declared_symbols() + diag:
+        assert hasattr(D, s), s
+
+
 def test_abi_version(lib):
-    assert lib.nova_crc32c_abi_version() == 1
+    assert lib.nova_crc32c_abi_version() == C.ABI_VERSION == 2
 
 
 def test_standard_results():
@@ -81,12 +100,61 @@ def test_combine(golden, oracle):
         assert C.Combine(C.Value(a), C.Value(b), nb) == oracle.value(a + b)
 
 
-def test_hook_without_gpu_reports_cannot_accelerate():
-    # port::AcceleratedCRC32C contract: 0 means "cannot accelerate"
+def test_hook_never_returns_a_wrong_crc_without_gpu(oracle):
+    """port::AcceleratedCRC32C once adopted (util/crc32c.cc:487-491) sees every
+    Extend(): with the device path failing (no GPU here) it must still return
+    Extend's value -- small buffers on the host by design, large ones through
+    the fallback."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present: covered by the gpu suite")
-    assert C.AcceleratedCRC32C(0, b"TestCRCBuffer") == 0
+    before = C.port_stats()
+    assert C.AcceleratedCRC32C(0, b"TestCRCBuffer") == 0xDCBC59FA  # util/crc32c.cc:479-481
+    for n, init in [(1, 0), (4096, 5), ((1 << 20) + 77, 0x1234), (3 << 20, 0xFFFFFFFF)]:
+        d = splitmix64_bytes(n, n).tobytes()
+        assert C.AcceleratedCRC32C(init, d) == oracle.extend(init, d), n
+    after = C.port_stats()
+    assert after["host"] - before["host"] == 3
+    assert after["fallback"] - before["fallback"] == 2
+    assert after["device"] == before["device"]
+
+
+class _FakeTensor:
+    """Stands in for a GPU tensor to exercise the argument checks on the CPU."""
+
+    def __init__(self, dtype, n=8, contiguous=True, device="cuda:0", cuda=True):
+        self.dtype, self._n, self._c, self.device, self.is_cuda = dtype, n, contiguous, device, cuda
+
+    def is_contiguous(self):
+        return self._c
+
+    def numel(self):
+        return self._n
+
+    def data_ptr(self):
+        return 4096
+
+
+def test_argument_validation_rejects_bad_tensors():
+    """Descriptors are read as raw u64 / u32 arrays by the kernels: a wrong
+    dtype, a strided view, another device or a short output is refused before
+    any pointer reaches the C-ABI."""
+    import torch
+    u64, u32 = C._u64_dtypes(), C._u32_dtypes()
+    ok = C._arg(_FakeTensor(torch.int64), "offsets", u64, "cuda:0", 8)
+    assert ok == 4096
+    bad = [
+        (_FakeTensor(torch.int32), u64, None, 0),                     # int32 offsets
+        (_FakeTensor(torch.int64), u32, None, 0),                     # int64 lengths
+        (_FakeTensor(torch.int64, contiguous=False), u64, None, 0),   # strided view
+        (_FakeTensor(torch.int64, device="cuda:1"), u64, "cuda:0", 0),  # other device
+        (_FakeTensor(torch.int32, n=3), u32, None, 4),                # output too short
+        (_FakeTensor(torch.int64, cuda=False), u64, None, 0),         # host tensor
+        (_FakeTensor(torch.float32), (torch.uint8,), None, 0),        # data not bytes
+    ]
+    for t, dt, dev, mn in bad:
+        with pytest.raises(C.NovaError):
+            C._arg(t, "x", dt, dev, mn)
 
 
 def test_batch_refuses_cpu_tensors():
@@ -119,3 +187,14 @@ def test_rounds_plan_sized_to_the_batch(n, lanes, chunk):
     assert d["kernel"].startswith("crc32c_rounds_kernel")
     assert (d["lanes_per_block"], d["chunk_blocks"]) == (lanes, chunk)
     assert C.describe(n, 0, 0, variable=True, large=True)["kernel"].startswith("crc32c_units_kernel")
+
+
+@pytest.mark.parametrize("n,chunk", [(1, 16), (196607, 16), (196608, 32), (393215, 32),
+                                     (393216, 64), (1 << 21, 64)])
+def test_log_plan_sized_to_the_batch(n, chunk):
+    """Log records (~2 KiB): 16-record chunks below 32 chunks per wave slot,
+    32 below 64, the throughput default 64 above; describe()
+    reports the chunk the log launch uses."""
+    d = C.describe(n, 0, 0, log=True)
+    assert d["kernel"].startswith("crc32c_rounds_kernel<8, 3>"), d
+    assert d["chunk_blocks"] == chunk

@@ -136,19 +136,57 @@ def test_alignment_independence(oracle, n):
         assert int(got[0]) == want, off
 
 
-def test_log_fixture(oracle, golden):
-    # db/log_writer.cc:99-114 / db/log_reader.cc:251-262 through the oracle
+def golden_log_image(golden):
+    """The fixture's log file: log::Writer's layout (db/log_writer.cc:53-97) of
+    the recorded payload sizes, CRC fields not yet written."""
+    from novalsm_amd.synth import log_image
     lg = golden["log"]
-    buf = splitmix64_bytes(lg["seed"], lg["total"]).copy()
-    for (o, ln, t) in lg["records"]:
-        buf[o + 4] = ln & 0xFF
-        buf[o + 5] = ln >> 8
-        buf[o + 6] = t
-    offs = [r[0] for r in lg["records"]]
+    img, offs, lens, types = log_image(lg["seed"], lg["payload_lens"])
+    assert img.size == lg["total"]
+    assert [[int(o), int(n), int(t)] for o, n, t in zip(offs, lens, types)] == lg["records"]
+    return img, offs
+
+
+def test_log_fixture(oracle, golden):
+    # db/log_writer.cc:99-114 / db/log_reader.cc:249-262 through the oracle
+    lg = golden["log"]
+    buf, offs = golden_log_image(golden)
+    assert {r[2] for r in lg["records"]} == {1, 2, 3, 4}  # FULL, FIRST, MIDDLE, LAST fragments
     oracle.log_write(buf, offs)
     for (o, _, _), c in zip(lg["records"], lg["header_crc"]):
         assert int.from_bytes(buf[o:o + 4].tobytes(), "little") == c
     assert oracle.log_verify(buf, offs).all()
+    assert (oracle.log_check(buf, offs) == 1).all()
+
+
+def test_log_check_statuses(oracle, golden):
+    """ReadPhysicalRecord's checks in the oracle (db/log_reader.cc:196-262):
+    a length that runs past its 32 KiB block is a bad record length, a zero
+    record is skipped, a record cut by the end of a partial last block is EOF,
+    a flipped payload byte is a checksum mismatch."""
+    from novalsm_amd.synth import LOG_BLOCK
+    buf, offs = golden_log_image(golden)
+    oracle.log_write(buf, offs)
+    i_len, i_crc, i_zero = 7, 20, 40
+    o = int(offs[i_len])
+    buf[o + 5] = 0xFF  # length ~65 KiB: past its block
+    buf[int(offs[i_crc]) + 9] ^= 0x04
+    oz = int(offs[i_zero])
+    buf[oz + 4:oz + 7] = 0  # type 0, length 0
+    st = oracle.log_check(buf, offs)
+    want = np.ones(len(offs), np.uint8)
+    want[[i_len, i_crc, i_zero]] = [2, 0, 3]
+    assert np.array_equal(st, want)
+    # the file ends inside its last block: the last record cut short -> EOF (4)
+    assert buf.size % LOG_BLOCK != 0
+    st = oracle.log_check(buf, offs, buf_len=buf.size - 1)
+    assert st[-1] == 4 and (st[:-1] == want[:-1]).all()
+    # a record that runs into the next block (its block is full) -> bad length (2)
+    j = int(np.searchsorted(offs, LOG_BLOCK, side="left")) - 1  # last record of block 0
+    oj = int(offs[j])
+    room = LOG_BLOCK - oj - 7
+    buf[oj + 4], buf[oj + 5] = (room + 1) & 0xFF, (room + 1) >> 8
+    assert oracle.log_check(buf, offs[j:j + 1])[0] == 2
 
 
 def test_xor_parity_oracle():

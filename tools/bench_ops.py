@@ -47,17 +47,16 @@ def timed(torch, fn, steps, warmup, stream):
 
 
 def log_layout(total_target: int, seed: int):
-    """Records [crc 4][len 2][type 1][payload len], len ~ U[1,4096] from
-    splitmix64(seed), packed back to back up to ~total_target bytes."""
-    from novalsm_amd.synth import splitmix64_words
+    """A log file of ~total_target bytes as log::Writer lays it out
+    (db/log_writer.cc:53-97, novalsm_amd/synth.log_layout): logical records of
+    U[1,4096] B payload from splitmix64(seed), fragmented at 32 KiB blocks.
+    Returns the physical records' (offsets, payload lengths, types, total)."""
+    from novalsm_amd.synth import splitmix64_words, log_layout as writer_layout
     n = total_target // (7 + 2048)
     r = splitmix64_words(seed, 0, n)
-    lens = ((r % np.uint64(4096)) + np.uint64(1)).astype(np.uint64)
-    types = ((r >> np.uint64(20)) % np.uint64(4) + np.uint64(1)).astype(np.uint8)
-    offs = np.zeros(n, np.uint64)
-    offs[1:] = np.cumsum(lens[:-1] + np.uint64(7))
-    total = int(offs[-1] + lens[-1] + np.uint64(7))
-    return offs, lens, types, total
+    plens = ((r % np.uint64(4096)) + np.uint64(1)).astype(np.int64)
+    offs, lens, types, _, total = writer_layout(plens)
+    return offs, lens.astype(np.uint64), types, total
 
 
 def main() -> int:
@@ -138,9 +137,9 @@ def main() -> int:
                 blk = buf[o:o + ln + 5].cpu().numpy().tobytes()
                 ok &= orc.trailer(blk[:ln], 0, True) == blk[ln:]
             emit("trailers", wl, sum_len + 5 * n, sec, ok, {"image": image})
-            C.load().nova_diag_set_trailer_single_pass(1)  # A/B: trailer bytes stored by the CRC kernel
-            sec1 = timed(torch, tw, args.steps, args.warmup, stream)
-            C.load().nova_diag_set_trailer_single_pass(0)
+            with C.diagnostics() as D:  # A/B: trailer bytes stored by the CRC kernel
+                D.nova_diag_set_trailer_single_pass(1)
+                sec1 = timed(torch, tw, args.steps, args.warmup, stream)
             gbs1 = (sum_len + 5 * n) / sec1 / 1e9
             print(json.dumps({"sweep": "trailers_single_pass", "image": image, "GBps": round(gbs1, 1),
                               "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
@@ -180,7 +179,7 @@ def main() -> int:
             ok = True
             for i in sample:
                 a, L = int(offs_np[i]), int(lens_np[i])
-                rec = buf[a:a + 7 + L].cpu().numpy()
+                rec = buf[a:a + 7 + L].cpu().numpy()  # (the type byte is the header's last)
                 want = orc.mask(orc.extend(orc.value(rec[6:7].tobytes()), rec[7:].tobytes()))
                 ok &= int.from_bytes(rec[:4].tobytes(), "little") == want
             emit("log_write", wl, sum_rec, sec, ok)
@@ -194,7 +193,7 @@ def main() -> int:
                 bad.zero_()
                 C.log_verify_records(buf, o, stream=stream, ok=okb, bad=bad)
             sec = timed(torch, lv, args.steps, args.warmup, stream)
-            ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
+            ok = int(bad.item()) == 0 and bool((okb.cpu().numpy() == C.LOG_OK).all())
             emit("log_verify", wl, sum_rec + n, sec, ok)
             sweep("log_verify", lv, sum_rec + n)
         del buf
@@ -217,15 +216,14 @@ def main() -> int:
             ok &= np.array_equal(out[i:i + 4096].cpu().numpy(), want)
         emit("parity", f"{k} fragments x {plen >> 20} MiB", (k + 1) * plen, sec, ok)
         if args.parity_sweep:
-            L = C.load()
-            for v in args.parity_sweep.split(","):
-                L.nova_diag_set_parity_variant(int(v, 0))
-                sec = timed(torch, lambda: C.xor_parity(buf, fo, plen, out=out, stream=stream),
-                            args.steps, args.warmup, stream)
-                gbs = (k + 1) * plen / sec / 1e9
-                print(json.dumps({"sweep": "parity", "variant": v, "GBps": round(gbs, 1),
-                                  "frac": round(gbs / HBM_PEAK_GBS, 4)}), flush=True)
-            L.nova_diag_set_parity_variant(0)
+            with C.diagnostics() as L:
+                for v in args.parity_sweep.split(","):
+                    L.nova_diag_set_parity_variant(int(v, 0))
+                    sec = timed(torch, lambda: C.xor_parity(buf, fo, plen, out=out, stream=stream),
+                                args.steps, args.warmup, stream)
+                    gbs = (k + 1) * plen / sec / 1e9
+                    print(json.dumps({"sweep": "parity", "variant": v, "GBps": round(gbs, 1),
+                                      "frac": round(gbs / HBM_PEAK_GBS, 4)}), flush=True)
 
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "bench_ops.json"), "w") as f:

@@ -29,7 +29,7 @@ def main():
     import torch
     from novalsm_amd import crc32c as C
 
-    L = C.load()
+    L = C.enable_diagnostics()
     L.nova_diag_read_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     L.nova_diag_read_ceiling.restype = ctypes.c_int

@@ -23,7 +23,7 @@ def main() -> int:
     kernel = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     sort = int(sys.argv[5]) if len(sys.argv) > 5 else 2
     orc = load_oracle()
-    L = C.load()
+    L = C.enable_diagnostics()
     assert L.nova_device_init() == 0
     C.set_tuning(lanes, 0)
     L.nova_diag_set_chunk_blocks(chunk)

@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     from novalsm_amd import crc32c as C
-    L = C.load()
+    L = C.enable_diagnostics()
     L.nova_diag_read_stream.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_void_p]
     assert L.nova_device_init() == 0

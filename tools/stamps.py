@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     from novalsm_amd import crc32c as C
-    L = C.load()
+    L = C.enable_diagnostics()
     L.nova_diag_set_variant.argtypes = [ctypes.c_int]
     L.nova_diag_set_stamps.argtypes = [ctypes.c_void_p]
     L.nova_diag_set_static_pct.argtypes = [ctypes.c_int]

@@ -33,7 +33,7 @@ def main():
     from novalsm_amd import crc32c as C
     import bench
 
-    L = C.load()
+    L = C.enable_diagnostics()
     L.nova_diag_set_variant.argtypes = [ctypes.c_int]
     L.nova_diag_read_stream.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                         ctypes.c_int, ctypes.c_void_p]

@@ -34,6 +34,9 @@ def make_workload(wl: str, stream):
     import bench
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from bench_ops import log_layout
+    mode = ""
+    if wl.endswith("_tw") or wl.endswith("_vf"):  # sst4k_tw / sst4k_vf: trailer writer / verify
+        wl, mode = wl[:-3], wl[-2:]
     if wl == "cfg2":
         n, ln = 1 << 20, 4096
         buf = torch.empty(n * ln, dtype=torch.uint8, device="cuda")
@@ -78,12 +81,21 @@ def make_workload(wl: str, stream):
     ls = torch.from_numpy(lens.view(np.int32)).cuda()
     out = torch.empty(len(offs), dtype=torch.int32, device="cuda")
     alg = int(lens.astype(np.uint64).sum())
+    if mode == "tw":  # trailer writer (TableBuilder ordering): reads sum(len), writes 5 B/block
+        return (lambda: C.write_trailers(buf, o, ls, 0, True, stream=stream)), alg + 5 * len(offs), \
+            (buf, o, ls)
+    if mode == "vf":  # read-verify over the same image: reads sum(len + 5)
+        C.write_trailers(buf, o, ls, 0, False, stream=stream)
+        okb = torch.empty(len(offs), dtype=torch.uint8, device="cuda")
+        bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+        return (lambda: C.verify_blocks(buf, o, ls, stream=stream, ok=okb, bad=bad)), \
+            alg + 5 * len(offs), (buf, o, ls, okb, bad)
     return (lambda: C.batch(buf, o, ls, out=out, stream=stream)), alg, (buf, o, ls, out)
 
 
 def set_variant(C, v: str) -> None:
     """"flat:G:chunk:waves:var" | "units:G:seg:waves:var" | "auto"."""
-    L = C.load()
+    L = C.enable_diagnostics()
     if v == "auto":
         v = "auto:0:0:0:0"
     kind, g, x, w, var = v.split(":")
@@ -115,7 +127,7 @@ def main() -> int:
     import torch
     from novalsm_amd import crc32c as C
 
-    L = C.load()
+    L = C.enable_diagnostics()
     assert L.nova_device_init() == 0
     stream = torch.cuda.current_stream()
 
