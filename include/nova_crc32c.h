@@ -193,6 +193,10 @@ int nova_sstable_write_trailers_host(void* host_buf, const uint64_t* offsets, co
 int nova_sstable_verify_blocks_host(const void* host_buf, const uint64_t* offsets,
                                     const uint32_t* sizes, size_t n_blocks, uint8_t* ok_out,
                                     uint32_t* n_bad_out, size_t chunk_bytes, int n_streams);
+/* The three calls above keep the calling thread's device staging (n_streams x
+ * the largest chunk) and pinned result buffer between calls; this frees them.
+ * chunk_bytes 0 sizes chunks to the image (about two per stream, 4-64 MiB). */
+void nova_host_staging_release(void);
 
 /* ---- utilities ----------------------------------------------------------- */
 /* Fill nbytes of device memory with the splitmix64 counter stream
@@ -209,7 +213,8 @@ int nova_stream_release(void* stream);
 size_t nova_stream_slots(void);
 /* Lanes per block ("G") and segment bytes the dispatcher would pick for an
  * aligned fixed-stride batch; returns 1 for the streaming kernel, 0 for the
- * units kernel, 2 for the flat kernel, 3 for the rounds kernel.  nova_crc32c_describe writes a JSON object naming the kernel
+ * units kernel, 2 for the flat kernel, 3 for the rounds kernel, 4 for the
+ * burst (one-SSTable latency) kernel.  nova_crc32c_describe writes a JSON object naming the kernel
  * and its launch parameters (for reports and profiles); variable: 0 fixed-stride,
  * 1 variable-length, 2 variable-length with NOVA_CRC32C_HINT_LARGE_BLOCKS. */
 int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_unit,
@@ -258,6 +263,9 @@ void nova_diag_set_rounds_sort(int on);
 /* Trailer writer on the rounds kernel: 1 = one pass (trailer bytes stored by
  * the CRC kernel), 0 = two passes (default). */
 void nova_diag_set_trailer_single_pass(int on);
+/* Burst (one-SSTable) kernel: 0 automatic, 16 or 64 lanes per block forced for
+ * any batch size of store / trailer / verify, -1 never. */
+void nova_diag_set_burst_lanes(int lanes);
 /* XOR parity kernel variant: chunks per thread (bits 0-3), fragments loaded
  * together (bits 4-7), workgroups per CU (bits 8-15); 0 fields = default. */
 void nova_diag_set_parity_variant(int variant);

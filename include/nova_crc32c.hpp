@@ -71,6 +71,31 @@ inline int VerifyBlocks(const void* buf, const uint64_t* offsets, const uint32_t
   return nova_sstable_verify_blocks(buf, offsets, sizes, n, ok, n_bad, stream);
 }
 
+// The same on an SSTable image in HOST memory (backing_mem_ / the ReadAll
+// slab): chunks are copied H2D over pooled streams, results come back; the
+// trailer bytes are stored by the host.  Synchronous.
+inline int WriteTrailersHost(void* host_buf, const uint64_t* offsets, const uint32_t* sizes,
+                             size_t n, uint8_t type, bool table_builder_quirk) {
+  return nova_sstable_write_trailers_host(
+      host_buf, offsets, sizes, n,
+      NOVA_CRC32C_TYPE(type) | (table_builder_quirk ? NOVA_TRAILER_TB_QUIRK : 0u), 0, 3);
+}
+inline int VerifyBlocksHost(const void* host_buf, const uint64_t* offsets, const uint32_t* sizes,
+                            size_t n, uint8_t* ok, uint32_t* n_bad) {
+  return nova_sstable_verify_blocks_host(host_buf, offsets, sizes, n, ok, n_bad, 0, 3);
+}
+
+// Log / MANIFEST physical records of a log image.
+// status[i] is one of NOVA_LOG_* (db/log_reader.cc:196-262).
+inline int LogWriteCrcs(void* log, size_t log_len, const uint64_t* record_offsets, size_t n,
+                        void* stream = nullptr) {
+  return nova_log_write_crcs(log, log_len, record_offsets, n, stream);
+}
+inline int LogVerifyRecords(const void* log, size_t log_len, const uint64_t* record_offsets,
+                            size_t n, uint8_t* status, uint32_t* n_bad, void* stream = nullptr) {
+  return nova_log_verify_records(log, log_len, record_offsets, n, status, n_bad, stream);
+}
+
 inline uint32_t Combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
   return nova_crc32c_combine(crc_a, crc_b, len_b);
 }

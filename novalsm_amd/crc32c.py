@@ -52,6 +52,7 @@ _SIG = {
     "nova_crc32c_combine": (_u32, [_u32, _u32, _u64]),
     "nova_port_accelerated_crc32c": (_u32, [_u32, ctypes.c_char_p, _sz]),
     "nova_port_stats": (None, [_pu64, _pu64, _pu64]),
+    "nova_host_staging_release": (None, []),
     "nova_crc32c_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _vp]),
     "nova_crc32c_batch_strided": (_i32, [_vp, _u64, _u32, _sz, _vp, _vp, _u32, _vp]),
     "nova_sstable_write_trailers": (_i32, [_vp, _vp, _vp, _sz, _u32, _vp]),
@@ -85,6 +86,7 @@ _DIAG_SIG = {
     "nova_diag_set_parity_variant": (None, [_i32]),
     "nova_diag_set_rounds_sort": (None, [_i32]),
     "nova_diag_set_trailer_single_pass": (None, [_i32]),
+    "nova_diag_set_burst_lanes": (None, [_i32]),
     "nova_diag_read_stream": (_i32, [_vp, _sz, _vp, _i32, _vp]),
     "nova_diag_read_ceiling": (_i32, [_vp, _sz, _vp, _i32, _i32, _vp]),
 }
@@ -173,6 +175,7 @@ def diagnostics():
         D.nova_diag_set_rounds_sort(2)
         D.nova_diag_set_trailer_single_pass(0)
         D.nova_diag_set_parity_variant(0)
+        D.nova_diag_set_burst_lanes(0)
 
 
 def _check(rc: int, what: str) -> None:

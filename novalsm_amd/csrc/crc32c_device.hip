@@ -54,7 +54,7 @@ namespace {
 constexpr int kWaves = 16;                 // waves per workgroup
 constexpr int kThreads = kWaves * 64;
 constexpr uint32_t kMainBytes = 131072;    // 4 tables x 256 x 32 replicas x 4 B
-constexpr int kTreeLevels = 6;             // M4, M8, M16, M32, M64, M128
+constexpr int kTreeLevels = 8;             // M4, M8, M16, ..., M512 (M256/M512: burst kernel)
 constexpr uint32_t kTreeBytes = 4096;      // per level
 constexpr uint32_t kWaveScratch = 512;     // per wave: 2x16 prefixes (+pad) + accumulators
 constexpr int kNumG = 5;                   // G = 1, 2, 4, 8, 16
@@ -534,8 +534,8 @@ __device__ __forceinline__ void sched_release(uint32_t* sched) {
 // L2 round trips per workgroup, a fixed cost that dominated small batches.
 __device__ __forceinline__ void lds_fill_tables(uint8_t* lds, const void* tab_main,
                                                 const void* tab_tree, uint32_t tree16,
-                                                const void* tab_byte, uint32_t byte16) {
-  constexpr uint32_t kMain16 = kMainBytes / 16;
+                                                const void* tab_byte, uint32_t byte16,
+                                                uint32_t kMain16 = kMainBytes / 16) {
   const uint32_t n16 = kMain16 + tree16 + byte16;
   // per-source base addresses, rebased so that LDS index j reads base + 16 j
   const uint64_t am = (uint64_t)tab_main;
@@ -1141,14 +1141,21 @@ __device__ __forceinline__ void fold_step(const uint8_t* lds, const FlatSet& Y, 
 // E = u1 & ~15): finish the register with the tail bytes [E,u1), add M_n(~init)
 // for blocks shorter than 4 bytes, apply the mode's epilogue.  The memory
 // write is returned (wb_*) and issued later (write_result).
-template <int MODE>
+// kTree: LDS byte offset of the tree's level 0 (M4).
+__device__ __forceinline__ uint32_t lapply(const uint8_t* t, uint32_t x) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(t);
+  return w[x & 255] ^ w[256 + ((x >> 8) & 255)] ^ w[512 + ((x >> 16) & 255)] ^ w[768 + (x >> 24)];
+}
+
+template <int MODE, uint32_t kTree = kMainBytes>
 __device__ __forceinline__ void finish_block(const uint8_t* lds, uint32_t byte_tab, const CrcParams& p,
                                              bool raw, uint32_t v, const FlatSet& Y, uint64_t& wb_a,
                                              uint32_t& wb_v) {
   constexpr bool kLog = MODE == kLogWrite || MODE == kLogVerify;
   const uint64_t E = Y.u1 & ~15ull;
   const uint32_t nb = (uint32_t)(Y.u1 - E);
-  uint32_t R = tapply(lds, 0, v);  // register at E
+  const uint8_t* m4 = lds + kTree;
+  uint32_t R = lapply(m4, v);  // register at E
   {
     // The tail line's bytes from u1 on are never consumed below (whole words
     // only below nb, then nb & 3 single bytes), so only the head edge (a block
@@ -1159,11 +1166,11 @@ __device__ __forceinline__ void finish_block(const uint8_t* lds, uint32_t byte_t
     const uint32_t w2 = head_word(Y.t.z, ht - 8, Y.ninit);
     const uint32_t w3 = head_word(Y.t.w, ht - 12, Y.ninit);
     uint32_t r;
-    r = tapply(lds, 0, R ^ w0);
+    r = lapply(m4, R ^ w0);
     R = nb >= 4 ? r : R;
-    r = tapply(lds, 0, R ^ w1);
+    r = lapply(m4, R ^ w1);
     R = nb >= 8 ? r : R;
-    r = tapply(lds, 0, R ^ w2);
+    r = lapply(m4, R ^ w2);
     R = nb >= 12 ? r : R;
     const uint32_t wl = sel5(nb >> 2, w0, w1, w2, w3, 0u);
     const uint32_t nr = nb & 3u;
@@ -2002,6 +2009,235 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   sched_release(p.sched);
 }
 
+// ---- crc32c_burst_kernel<G, MODE>: one SSTable per call (latency path) -------
+// NovaLSM checksums one SSTable (~4K blocks of ~4 KiB) per call and waits for
+// it.  The throughput kernels keep ONE step of loads in
+// flight per wave, so a small batch pays a full HBM round trip per step.
+// Here a lane group takes one block and issues ALL of its loads at once:
+//   * the block's region [E - K*S, E) (E = u1 & ~15, S = 16G) is K swaths;
+//     lane q holds the 16-B piece q of every swath, so its four registers are
+//     word streams with an S-byte stride (c = w ^ M_S(c)); pieces before the
+//     block read the zero line (leading zeros leave a zero register alone), the
+//     piece(s) holding [u0, u0+4) take ~init.  The wave's groups run the
+//     wave's largest K, each group's region end-aligned (shorter blocks start
+//     on zero pieces);
+//   * up to kK swaths per pass are loaded together; a longer block loads its
+//     next pass before folding the current one;
+//   * the stream words fold in-lane (M4, M8) and across the group, then the
+//     0..15 tail bytes [E, u1) and the mode's epilogue run as in the rounds
+//     kernel (finish_block);
+//   * the first block's descriptor and data loads are issued before the LDS
+//     tables are filled, and the fill is LDS-DMA (global_load_lds_dwordx4: no
+//     VGPRs, the whole image in flight at once), so the three round trips
+//     (descriptors, data, tables) overlap instead of adding up.
+// Two table sets:
+//   G = 64 (one block per wave): the M_1024 operator NOT bank-replicated plus
+//     8 tree levels and the byte table, 37 KiB -- for a few blocks per call,
+//     where the fill and the dependency chain are the cost;
+//   G = 16 (four blocks per wave): the rounds kernel's bank-replicated M_256
+//     image (128 KiB) + 6 tree levels + byte table -- conflict-free lookups for
+//     thousands of blocks, where LDS lookups are the cost (random 8-bit
+//     indices into one 1 KiB table collide ~4-way per wave-instruction).
+// V: the table set.  64: one wave per block, compact M_1024; 65: the same with
+// the M_1024 operator 16-way bank-replicated (64 KiB; lane l reads replica
+// l & 15); 16: four blocks per wave on the replicated M_256 image.
+template <int V>
+struct BurstCfg;
+template <>
+struct BurstCfg<64> {
+  static constexpr int kG = 64;
+  static constexpr int kWaves = 16;                           // launch bound
+  static constexpr int kDefWaves = 8;                         // per workgroup by default
+  static constexpr int kK = 8;                                // swaths per pass
+  static constexpr uint32_t kTree = 4096;                     // after the M_1024 op
+  static constexpr int kLevels = 8;                           // M4 .. M512
+};
+#ifdef NOVA_DIAG
+template <>
+struct BurstCfg<65> {
+  static constexpr int kG = 64;
+  static constexpr int kWaves = 16;
+  static constexpr int kDefWaves = 16;
+  static constexpr int kK = 8;
+  static constexpr uint32_t kTree = 65536;                    // after the replicated M_1024 op
+  static constexpr int kLevels = 8;
+};
+template <>
+struct BurstCfg<16> {
+  static constexpr int kG = 16;
+  static constexpr int kWaves = 16;
+  static constexpr int kDefWaves = 16;
+  static constexpr int kK = 16;
+  static constexpr uint32_t kTree = kMainBytes;               // after the replicated image
+  static constexpr int kLevels = 6;                           // M4 .. M128
+};
+#endif
+template <int V>
+constexpr uint32_t burst_byte_tab() { return BurstCfg<V>::kTree + BurstCfg<V>::kLevels * kTreeBytes; }
+template <int V>
+constexpr uint32_t burst_lds() { return burst_byte_tab<V>() + 1024; }
+constexpr uint64_t kBurstSw = 1024;  // G = 64 swath (the M_1024 operator)
+
+// LDS-DMA copy of `bytes` (a multiple of 1 KiB) from `src` to LDS byte `dst`:
+// each wave-instruction moves 1 KiB (lane l: 16 B at +16 l).  Not waited for.
+__device__ __forceinline__ void glds_copy(uint32_t dst, const void* src, uint32_t bytes) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = blockDim.x >> 6, wave = threadIdx.x >> 6;
+  for (uint32_t c = wave; c < bytes / 1024; c += nw)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)((const uint8_t*)src + 1024u * c + 16u * lane),
+        (__attribute__((address_space(3))) void*)(uintptr_t)(dst + 1024u * c), 16, 0, 0);
+}
+
+// The 16-way replicated M_1024 operator: table k, entry idx, replica c at LDS
+// byte k*16384 + idx*64 + c*4 (c4 = 4c).
+[[maybe_unused]] __device__ __forceinline__ uint32_t rapply(uint32_t c4, uint32_t x) {
+  const uint32_t a0 = ((x & 255u) << 6) | c4;
+  const uint32_t a1 = (((x >> 8) & 255u) << 6) | c4 | 16384u;
+  const uint32_t a2 = (((x >> 16) & 255u) << 6) | c4 | 32768u;
+  const uint32_t a3 = ((x >> 24) << 6) | c4 | 49152u;
+  return xor3(lds_u32(nullptr, a0), lds_u32(nullptr, a1), lds_u32(nullptr, a2)) ^ lds_u32(nullptr, a3);
+}
+
+// Stream step of one swath piece for the group's four registers.
+template <int V>
+__device__ __forceinline__ void burst_step(const uint8_t* lds, uint32_t& c0, uint32_t& c1,
+                                           uint32_t& c2, uint32_t& c3, const uint4& w,
+                                           uint32_t lo0, uint32_t lo1, uint32_t lo2, uint32_t lo3) {
+  if constexpr (V == 64) {
+    c0 = lapply(lds, c0) ^ w.x;
+    c1 = lapply(lds, c1) ^ w.y;
+    c2 = lapply(lds, c2) ^ w.z;
+    c3 = lapply(lds, c3) ^ w.w;
+  } else if constexpr (V == 65) {
+    const uint32_t c4 = (threadIdx.x & 15u) << 2;
+    c0 = rapply(c4, c0) ^ w.x;
+    c1 = rapply(c4, c1) ^ w.y;
+    c2 = rapply(c4, c2) ^ w.z;
+    c3 = rapply(c4, c3) ^ w.w;
+  } else {
+    swath4<0>(lds, c0, c1, c2, c3, w, lo0, lo1, lo2, lo3);
+  }
+}
+
+template <int V, int MODE>
+__global__ void __launch_bounds__(BurstCfg<V>::kWaves * 64) crc32c_burst_kernel(CrcParams p) {
+  using Cfg = BurstCfg<V>;
+  constexpr int G = Cfg::kG;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr bool kTail2 = MODE == kVerify;  // the stored CRC follows the CRC input
+  constexpr int kK = Cfg::kK;
+  constexpr uint64_t kS = 16ull * G;
+  constexpr uint32_t kGroups = 64 / G;
+  const int lane = threadIdx.x & 63;
+  const int q = lane & (G - 1);
+  const int grp = lane / G;
+  const uint32_t rep = (uint32_t)(lane & 31) << 2;
+  const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
+  const uint8_t* tree = lds + Cfg::kTree;  // level l: M_{4 * 2^l}
+  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
+  const uint32_t extra = (MODE == kVerify) ? 1u : 0u;  // verify covers block + type byte
+  const uint64_t zl = (uint64_t)p.zline;
+  const uint64_t base = (uint64_t)p.base;
+  const uint64_t n_all = p.n_blocks;
+  const uint64_t step_blocks = (uint64_t)gridDim.x * (blockDim.x >> 6) * kGroups;
+
+  // per-group block state (the group's lanes hold identical values)
+  uint64_t bw = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kGroups;
+  FlatSet Y;
+  uint64_t A0 = 0, first = 0, Kw = 0;
+  bool valid = false;
+  uint4 d[kK], e[kK];
+  auto load_pass = [&](uint4 (&x)[kK], uint64_t k0) {
+#pragma unroll
+    for (int i = 0; i < kK; i++) {
+      const uint64_t a = first + (k0 + i) * kS;
+      x[i] = gload16((valid && k0 + i < Kw && a >= A0) ? a : zl);
+    }
+  };
+  // descriptors of the wave's next blocks, tail lines and the first pass
+  auto start_blocks = [&]() {
+    const uint64_t b = bw + grp;
+    valid = b < n_all;
+    const uint64_t bb = valid ? b : n_all - 1;  // clamped: valid memory, result unused
+    const uint64_t u0 = base + p.offsets[bb & p.omask] + bb * p.stride;
+    const uint32_t n = p.lengths[bb & p.lmask] + p.len + extra;
+    const uint32_t init = p.init[bb & p.imask];
+    const uint64_t u1 = u0 + n;
+    const uint64_t E = u1 & ~15ull;
+    A0 = u0 & ~15ull;
+    const uint64_t K = E > A0 ? (E - A0 + kS - 1) / kS : 0;
+    uint64_t km = valid ? K : 0;  // the wave's largest block (groups end-aligned)
+#pragma unroll
+    for (int k = G; k < 64; k <<= 1) {
+      const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(km >> 32), k) << 32) |
+                         (uint32_t)__shfl_xor((int)(uint32_t)km, k);
+      km = o > km ? o : km;
+    }
+    Kw = km;
+    first = E - Kw * kS + 16ull * q;
+    Y.u0 = u0;
+    Y.u1 = u1;
+    Y.rec = b;
+    Y.ninit = (raw || n < 4) ? 0u : ~init;
+    Y.st = init;
+    Y.valid = valid;
+    // tail line(s): [E, E+16) holds the tail bytes (verify: the start of the
+    // stored CRC), [E+16, E+32) the rest of a stored CRC
+    const bool need_t = valid && (kTail2 || (u1 & 15) != 0);
+    Y.t = gload16(need_t ? E : zl);
+    if constexpr (kTail2) Y.t2 = gload16(valid && u1 + 4 > E + 16 ? E + 16 : zl);
+    if (Kw) load_pass(d, 0);
+  };
+  const bool live0 = bw < n_all;
+  if (live0) start_blocks();
+  // tables by LDS-DMA while the first block's loads are in flight
+  glds_copy(0, p.tab_main, Cfg::kTree);
+  glds_copy(Cfg::kTree, p.tab_tree, Cfg::kLevels * kTreeBytes);
+  glds_copy(burst_byte_tab<V>(), p.tab_byte, 1024);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (!live0) return;
+
+  for (;;) {
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    auto fold_pass = [&](const uint4 (&x)[kK], uint64_t k0) {
+#pragma unroll
+      for (int i = 0; i < kK; i++) {
+        if (k0 + i < Kw) {  // wave-uniform
+          const uint64_t a = first + (k0 + i) * kS;
+          const int32_t h = rel32(Y.u0, a, 32);
+          const uint4 w = is_head(h) ? head_piece(x[i], h, Y.ninit) : x[i];
+          burst_step<V>(lds, c0, c1, c2, c3, w, lo0, lo1, lo2, lo3);
+        }
+      }
+    };
+    for (uint64_t k0 = 0; k0 < Kw; k0 += 2 * kK) {
+      if (k0 + kK < Kw) load_pass(e, k0 + kK);
+      fold_pass(d, k0);
+      if (k0 + kK < Kw) {
+        if (k0 + 2 * kK < Kw) load_pass(d, k0 + 2 * kK);
+        fold_pass(e, k0 + kK);
+      }
+    }
+    // fold the group's stream words: in-lane M4/M8, then M16 .. across the group
+    uint32_t v = lapply(tree + kTreeBytes, lapply(tree, c0) ^ c1) ^ (lapply(tree, c2) ^ c3);
+#pragma unroll
+    for (int k = 0; (1 << k) < G; ++k) {
+      const uint32_t o = __shfl_xor(v, 1 << k);
+      const bool right = (q >> k) & 1;
+      v = lapply(tree + (2 + k) * kTreeBytes, right ? o : v) ^ (right ? v : o);
+    }
+    uint64_t wb_a = 0;
+    uint32_t wb_v = 0;
+    finish_block<MODE, Cfg::kTree>(lds, burst_byte_tab<V>(), p, raw, v, Y, wb_a, wb_v);
+    if (q == 0 && Y.valid) write_result<MODE>(p, wb_a, wb_v);
+    bw += step_blocks;
+    if (bw >= n_all) break;
+    start_blocks();
+  }
+}
+
 // XOR parity block over k data fragments (ltc/stoc_file_client_impl.cpp:334-349):
 // parity[i] = XOR_f mem[frag_off[f] + i] for i < parity_len.  Like the
 // reference, every fragment contributes parity_len bytes from its start (the
@@ -2204,6 +2440,8 @@ struct DevTables {
   uint32_t* sh16 = nullptr;
   uint32_t* zero_word = nullptr;  // 16 zero bytes: the NULL-init stand-in
   uint32_t* byte8 = nullptr;      // M_1 byte table (flat kernel tail steps)
+  uint32_t* op1024 = nullptr;     // M_1024 byte tables (burst kernel stream step)
+  uint32_t* op1024r = nullptr;    // the same, 16-way bank-replicated
   int cus = 0;
   int err = 0;
   // Claim counters, one 16 KiB slot per HIP stream (256 workgroups x 64 B).
@@ -2332,6 +2570,21 @@ int set_lds_attrs_rounds() {
   return set_lds_attr_rounds<16, MODE, VAR>();
 }
 
+template <int MODE>
+int set_lds_attr_burst() {
+  int e = (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_burst_kernel<64, MODE>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)burst_lds<64>());
+  if (e) return e;
+#ifdef NOVA_DIAG
+  e = (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_burst_kernel<65, MODE>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)burst_lds<65>());
+  if (e) return e;
+  e = (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_burst_kernel<16, MODE>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)burst_lds<16>());
+#endif
+  return e;
+}
+
 template <int VAR = 0>
 int set_lds_attrs_stream() {
   int e = 0;
@@ -2386,6 +2639,18 @@ void init_device(int dev, DevTables* t) {
     for (uint32_t b = 0; b < 256; b++) b8[b] = m1(b);
     if ((t->err = upload(&t->byte8, b8))) return;
   }
+  {
+    std::vector<uint32_t> op;
+    append_op(power(m1, (uint32_t)kBurstSw), op);
+    if ((t->err = upload(&t->op1024, op))) return;
+#ifdef NOVA_DIAG
+    std::vector<uint32_t> rep(16384);  // 4 tables x 256 entries x 16 replicas
+    for (int k = 0; k < 4; k++)
+      for (int idx = 0; idx < 256; idx++)
+        for (int c = 0; c < 16; c++) rep[(k * 256 + idx) * 16 + c] = op[k * 256 + idx];
+    if ((t->err = upload(&t->op1024r, rep))) return;
+#endif
+  }
   if ((t->err = set_lds_attrs_rounds<kStore>())) return;
   if ((t->err = set_lds_attrs_rounds<kTrailer>())) return;
   if ((t->err = set_lds_attrs_rounds<kVerify>())) return;
@@ -2397,6 +2662,9 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_mode<kLogWrite>())) return;
   if ((t->err = set_lds_attrs_mode<kLogVerify>())) return;
   if ((t->err = set_lds_attrs_stream<0>())) return;
+  if ((t->err = set_lds_attr_burst<kStore>())) return;
+  if ((t->err = set_lds_attr_burst<kTrailer>())) return;
+  if ((t->err = set_lds_attr_burst<kVerify>())) return;
 #ifdef NOVA_DIAG
   // timing ablations and alternative schedules (diagnostics build only)
   if ((t->err = set_lds_attrs_flat<kStore>())) return;
@@ -2898,11 +3166,88 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   return launch_stream_g<0>(G, dim3(wgs), lds, stream, p);
 }
 
+// One SSTable per call: batches up to burst_max() blocks (two per wave slot of
+// the rounds kernel, 6144 on 256 CUs) go to the burst kernel, one wave per
+// block on the compact tables, unless tuning forces a kernel.
+thread_local std::atomic<int> g_tune_burst{0};  // diagnostics: 0 auto, 16/64/65 force, -1 off
+uint64_t burst_max(uint32_t cus) { return 2ull * cus * flat_waves(); }
+int burst_lanes(int mode, uint64_t n_blocks, uint32_t cus) {
+  if (mode != kStore && mode != kTrailer && mode != kVerify) return 0;
+  const int tb = g_tune_burst.load();
+  if (tb < 0) return 0;
+  if (tb == 16 || tb == 64 || tb == 65) return tb;
+  if (g_tune_g.load() || g_tune_seg.load() || g_tune_kernel.load()) return 0;
+  return n_blocks <= burst_max(cus) ? 64 : 0;
+}
+
+template <int V, int MODE>
+int launch_burst(CrcParams& p, DevTables* t, hipStream_t stream) {
+  constexpr int G = BurstCfg<V>::kG;
+  p.tab_main = V == 64 ? t->op1024 : V == 65 ? t->op1024r : t->main[gindex(16)];
+  p.tab_tree = t->tree;
+  p.tab_byte = t->byte8;
+  p.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
+  p.omask = p.lmask = p.imask = ~0ull;
+  if (p.offsets) {
+    p.stride = 0;
+  } else {
+    p.offsets = reinterpret_cast<const uint64_t*>(t->zero_word);
+    p.omask = 0;
+  }
+  if (p.lengths) {
+    p.len = 0;
+  } else {
+    p.lengths = t->zero_word;
+    p.lmask = 0;
+  }
+  if (!p.init) {
+    p.init = t->zero_word;
+    p.imask = 0;
+  }
+  // one block per lane group; G = 16: at most one workgroup per CU (LDS), so
+  // the waves per workgroup follow the batch to spread it over the CUs
+  constexpr uint64_t per_wave = 64 / G;
+  const uint64_t waves_needed = (p.n_blocks + per_wave - 1) / per_wave;
+  // 4 waves per workgroup up to 2K blocks, 8 above (tools/latency_burst.py)
+  uint64_t nw = (uint64_t)waves_per_wg(V == 64 && p.n_blocks <= 2048 ? 4 : BurstCfg<V>::kDefWaves);
+  if (nw > (uint64_t)BurstCfg<V>::kWaves) nw = BurstCfg<V>::kWaves;
+  uint64_t wgs = (waves_needed + nw - 1) / nw;
+  if (V != 64) {
+    const uint64_t cus = (uint64_t)t->cus;
+    if (wgs < cus) {  // fewer waves per workgroup, more workgroups
+      nw = (waves_needed + cus - 1) / cus;
+      if (nw < 4) nw = 4;
+      wgs = (waves_needed + nw - 1) / nw;
+    }
+    if (wgs > cus) wgs = cus;  // the rest by the grid-stride loop
+  }
+  hipLaunchKernelGGL((crc32c_burst_kernel<V, MODE>), dim3(wgs), dim3(64 * nw), burst_lds<V>(),
+                     stream, p);
+  return (int)hipGetLastError();
+}
+
+template <int MODE>
+int launch_burst_g(int V, CrcParams& p, DevTables* t, hipStream_t stream) {
+#ifdef NOVA_DIAG
+  // measured slower at every batch size (profiles/r02_latency_burst_variants.log)
+  if (V == 65) return launch_burst<65, MODE>(p, t, stream);
+  if (V == 16) return launch_burst<16, MODE>(p, t, stream);
+#endif
+  return launch_burst<64, MODE>(p, t, stream);
+}
+
 int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStream_t stream) {
   int err = 0;
   DevTables* t = tables(&err);
   if (!t) return err;
   if (p.n_blocks == 0) return 0;
+  if (const int bg = burst_lanes(mode, p.n_blocks, (uint32_t)t->cus)) {
+    switch (mode) {
+      case kStore: return launch_burst_g<kStore>(bg, p, t, stream);
+      case kTrailer: return launch_burst_g<kTrailer>(bg, p, t, stream);
+      default: return launch_burst_g<kVerify>(bg, p, t, stream);
+    }
+  }
   if (mode == kStore && uniform && !g_tune_seg.load()) {
     const int sg = stream_lanes(p);
     if (sg) return launch_stream(sg, p, t, stream);
@@ -3132,6 +3477,11 @@ int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_u
   p.len = (uint32_t)bytes_per_block;
   p.stride = bytes_per_block;
   p.n_blocks = n_blocks;
+  if (const int bg = burst_lanes(kStore, n_blocks, cus_hint())) {
+    if (lanes_per_unit) *lanes_per_unit = bg;
+    if (seg_bytes) *seg_bytes = 0;
+    return 4;  // burst kernel
+  }
   const int sg = g_tune_seg.load() ? 0 : stream_lanes(p);
   if (sg) {
     if (lanes_per_unit) *lanes_per_unit = sg;
@@ -3154,7 +3504,13 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
   int sg = 0;
   if (!variable && !g_tune_seg.load()) sg = stream_lanes(p);
   int n;
-  if (sg) {
+  const int bg = variable == 3 ? 0 : burst_lanes(kStore, n_blocks, cus_hint());
+  if (bg) {
+    n = snprintf(buf, buflen,
+                 "{\"kernel\": \"crc32c_burst_kernel<%d, 0>\", \"lanes_per_block\": %d, "
+                 "\"swaths_per_pass\": %d}", bg, bg,
+                 bg == 16 ? 16 : BurstCfg<64>::kK);
+  } else if (sg) {
     n = snprintf(buf, buflen,
                  "{\"kernel\": \"crc32c_stream_kernel<%d, 0>\", \"lanes_per_block\": %d, "
                  "\"blocks_per_group\": %u, \"steal_probes\": %d}",
@@ -3224,6 +3580,8 @@ void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
 void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
 
 void nova_diag_set_trailer_single_pass(int on) { g_tune_trailer_1pass.store(on); }
+
+void nova_diag_set_burst_lanes(int lanes) { g_tune_burst.store(lanes); }
 
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {

@@ -66,8 +66,11 @@ struct PinBuf {
   PinBuf(const PinBuf&) = delete;
   PinBuf& operator=(const PinBuf&) = delete;
   PinBuf(PinBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
-  ~PinBuf() {
+  ~PinBuf() { reset(); }
+  void reset() {
     if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
   }
   int ensure(size_t bytes) {
     if (bytes <= n) return 0;
@@ -187,6 +190,18 @@ struct Stage {
   PinBuf hoffs, hlens;  // rebased descriptors (pinned: async H2D)
 };
 
+// The calling thread's staging, kept between calls (hipMalloc / hipHostMalloc
+// cost milliseconds: per call they were most of a one-SSTable call's time).
+// Grows to the largest chunk seen; nova_host_staging_release() frees it.
+struct HostStaging {
+  std::vector<Stage> stage;
+  PinBuf pres;
+};
+HostStaging& host_staging() {
+  thread_local HostStaging h;
+  return h;
+}
+
 // Runs a batch over blocks that live in host memory.  Blocks [b0, b1) form a
 // chunk when their spanned bytes fit chunk_bytes (a single larger block gets a
 // chunk of its own); the span [lo, hi) is copied H2D, the chunk's offsets are
@@ -197,11 +212,20 @@ int host_batch(HostOp op, const void* host_base, const uint64_t* offsets, const 
                uint8_t* ok_out, size_t chunk_bytes, int n_streams) {
   if (n_blocks == 0) return 0;
   if (!host_base || !offsets || !lengths) return NOVA_E_INVAL;
-  if (chunk_bytes == 0) chunk_bytes = 64ull << 20;
   n_streams = std::max(1, std::min(n_streams, 8));
   int err = nova_device_init();
   if (err) return err;
   const uint64_t tail = op == kHostVerify ? 5 : 0;  // verify reads the trailer too
+  if (chunk_bytes == 0) {
+    // about two chunks per stream so copies and kernels overlap, 4..64 MiB
+    uint64_t lo = ~0ull, hi = 0;
+    for (size_t b = 0; b < n_blocks; b++) {
+      lo = std::min(lo, offsets[b]);
+      hi = std::max(hi, offsets[b] + lengths[b] + tail);
+    }
+    chunk_bytes = std::max<uint64_t>(4ull << 20, std::min<uint64_t>(64ull << 20,
+                                                                     (hi - lo) / (2 * n_streams)));
+  }
   // chunk boundaries and spans
   struct Chunk { size_t b0, b1; uint64_t lo, hi; };
   std::vector<Chunk> chunks;
@@ -229,11 +253,14 @@ int host_batch(HostOp op, const void* host_base, const uint64_t* offsets, const 
   if ((err = hr.reg(static_cast<const uint8_t*>(host_base) + glo, ghi - glo))) return err;
   Streams st;
   if ((err = st.get(n_streams))) return err;
-  std::vector<Stage> stage(n_streams);
-  PinBuf pres;  // results for the whole batch
+  HostStaging& hsg = host_staging();
+  if (hsg.stage.size() < (size_t)n_streams) hsg.stage.resize(n_streams);
+  std::vector<Stage>& stage = hsg.stage;
+  PinBuf& pres = hsg.pres;  // results for the whole batch
   const size_t res_bytes = op == kHostVerify ? n_blocks : n_blocks * 4;
   if ((err = pres.ensure(res_bytes))) return err;
-  for (auto& s : stage) {
+  for (int si = 0; si < n_streams; si++) {
+    Stage& s = stage[si];
     if ((err = s.data.ensure(span_max + 16))) return err;
     if ((err = s.offs.ensure(blocks_max * 8)) || (err = s.lens.ensure(blocks_max * 4)) ||
         (err = s.out.ensure(op == kHostVerify ? blocks_max + 4 : blocks_max * 4)) ||
@@ -486,6 +513,12 @@ uint32_t nova_port_accelerated_crc32c(uint32_t crc, const char* buf, size_t size
     g_hook_host.fetch_add(1, std::memory_order_relaxed);
   }
   return nova_crc32c_extend(crc, buf, size);
+}
+
+void nova_host_staging_release(void) {
+  HostStaging& h = host_staging();
+  h.stage.clear();
+  h.pres.reset();
 }
 
 void nova_port_stats(uint64_t* host_calls, uint64_t* device_calls, uint64_t* fallback_calls) {

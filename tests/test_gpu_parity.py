@@ -328,8 +328,9 @@ def test_no_device_memory_growth(torch_gpu, oracle):
     torch.cuda.synchronize()
     # 4 threads: at most 4 hook streams + 3 x 4 stream_host streams in the pool
     assert C.stream_slots() <= slots0 + 16
-    s = torch.cuda.Stream()
-    C.batch_strided(dev(torch, splitmix64_bytes(1, 4096 * 8)), 4096, 4096, 8, stream=s)
+    s = torch.cuda.Stream()  # a batch above the burst size: the stream kernel takes a slot
+    C.batch_strided(dev(torch, splitmix64_bytes(1, 4096 * 8192)), 4096, 4096, 8192, stream=s)
+    s.synchronize()
     n1 = C.stream_slots()
     C.stream_release(s)
     assert C.stream_slots() == n1 - 1
@@ -517,12 +518,18 @@ def test_baseline_config4_shard_full(torch_gpu, oracle):
 
 @pytest.mark.parametrize("length", [256, 1024, 2048, 4096, 8192, 16384, 65536])
 @pytest.mark.parametrize("n", [1, 7, 100, 4099])
-def test_stream_kernel_shapes(torch_gpu, oracle, length, n):
-    """Aligned uniform batches go through crc32c_stream_kernel: ragged tail rounds,
-    batches smaller than one round, init arrays and flags."""
+@pytest.mark.parametrize("kernel", ["auto", "stream"])
+def test_stream_kernel_shapes(torch_gpu, oracle, length, n, kernel):
+    """Aligned uniform batches: crc32c_stream_kernel (forced by a lane count;
+    ragged tail rounds, batches smaller than one round) and the dispatcher's
+    choice for these SSTable-sized batches (the burst kernel); init arrays and
+    flags."""
     torch = torch_gpu
+    if kernel == "stream":
+        C.set_tuning(16 if length >= 16384 else 8, 0)
     d = C.describe(n, length, length)
-    assert d["kernel"].startswith("crc32c_stream_kernel"), d
+    assert d["kernel"].startswith("crc32c_stream_kernel" if kernel == "stream"
+                                  else "crc32c_burst_kernel"), d
     host = splitmix64_bytes(length + n, n * length)
     buf = dev(torch, host)
     rng = np.random.default_rng(n)
@@ -538,6 +545,71 @@ def test_stream_kernel_shapes(torch_gpu, oracle, length, n):
         else:
             want = oracle.batch_strided(host, length, length, n, init=ini, flags=flags)
         assert np.array_equal(u32(out), want), (flags, length, n)
+
+
+@pytest.mark.parametrize("mode", ["store", "trailers", "verify"])
+@pytest.mark.parametrize("lanes", [0, 16, 65])
+def test_burst_kernel(torch_gpu, oracle, mode, lanes):
+    """The one-SSTable latency path (crc32c_burst_kernel): one
+    wave per block on the compact tables (the dispatcher's choice), and the
+    measured-slower variants of the diagnostics build (16 lanes per block on
+    the replicated M_256 image; a 16-way replicated M_1024); every alignment
+    and length from 0 B to 300 KiB (many passes), per-block inits and all
+    flags, every mode, against the oracle."""
+    torch = torch_gpu
+    if lanes == 0:
+        assert C.describe(3000, 0, 0, variable=True)["kernel"].startswith("crc32c_burst_kernel<64")
+        _burst_checks(torch, oracle, mode)
+        return
+    with C.diagnostics() as L:
+        L.nova_diag_set_burst_lanes(lanes)
+        _burst_checks(torch, oracle, mode)
+
+
+def _burst_checks(torch, oracle, mode):
+    rng = np.random.default_rng(61)
+    n = 3000
+    lens = rng.choice([0, 1, 2, 3, 4, 5, 15, 16, 17, 1000, 1023, 1024, 1025, 4096, 4200, 8191,
+                       8192, 8193, 16384, 65599, 300000], n).astype(np.uint32)
+    lens += (rng.integers(0, 16, n) * (lens > 20)).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5) +
+                         rng.integers(0, 3, n - 1).astype(np.uint64))
+    offs += np.uint64(3)
+    perm = rng.permutation(n)
+    offs, lens = offs[perm], lens[perm]
+    total = int((offs + lens).max()) + 5 + 64
+    host = splitmix64_bytes(62, total).copy()
+    do, dl = dev(torch, offs, torch.int64), dev(torch, lens, torch.int32)
+    assert C.describe(n, 0, 0, variable=True)["kernel"].startswith("crc32c_burst_kernel")
+    if mode == "store":
+        init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        buf = dev(torch, host)
+        for flags, ini in [(0, None), (0, init), (C.APPEND_TYPE | C.TYPE(1) | C.MASK_OUTPUT, init)]:
+            out = C.batch(buf, do, dl, flags=flags,
+                          init=None if ini is None else dev(torch, ini.view(np.int32)))
+            want = oracle.batch(host, offs, lens, ini, flags=flags)
+            bad = np.flatnonzero(u32(out) != want)
+            assert bad.size == 0, (flags, [(int(offs[i]), int(lens[i])) for i in bad[:5]])
+        out = C.batch(buf, do, dl, flags=C.RAW)
+        want = oracle.batch(host, offs, lens, np.full(n, 0xFFFFFFFF, np.uint32)) ^ np.uint32(0xFFFFFFFF)
+        assert np.array_equal(u32(out), want)
+    elif mode == "trailers":
+        buf = dev(torch, host)
+        C.write_trailers(buf, do, dl, 3, True)
+        got = buf.cpu().numpy()
+        for i in range(n):
+            o, ln = int(offs[i]), int(lens[i])
+            assert oracle.trailer(host[o:o + ln].tobytes(), 3, True) == got[o + ln:o + ln + 5].tobytes(), i
+    else:
+        buf = dev(torch, host)
+        C.write_trailers(buf, do, dl, 0, False)
+        victims = rng.choice(n, 11, replace=False)
+        for v in victims:
+            buf[int(offs[v]) + int(lens[v]) // 2] ^= 0x20
+        ok, bad = C.verify_blocks(buf, do, dl)
+        assert sorted(np.flatnonzero(ok.cpu().numpy() == 0).tolist()) == sorted(victims.tolist())
+        assert int(bad.item()) == len(victims)
 
 
 @pytest.mark.parametrize("lanes,bpg,steal,waves,var", [
@@ -930,5 +1002,8 @@ def test_batch_size_dispatch_thresholds(torch_gpu, oracle, n):
     assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
     assert int(bad.item()) == len(victims)
     d = C.describe(n, 0, 0, variable=True)
-    want_chunk = 4 if n <= 6144 else (32 if n >= 196608 else 16 if n >= 98304 else 8)
-    assert d["chunk_blocks"] == want_chunk and d["lanes_per_block"] == (16 if n <= 6144 else 8)
+    if n <= 6144:
+        assert d["kernel"].startswith("crc32c_burst_kernel"), d
+    else:
+        want_chunk = 32 if n >= 196608 else 16 if n >= 98304 else 8
+        assert d["chunk_blocks"] == want_chunk and d["lanes_per_block"] == 8
