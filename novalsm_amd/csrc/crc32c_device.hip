@@ -97,6 +97,13 @@ struct CrcParams {
   const uint32_t* perm;      // rounds kernel: block index per sorted position (or null)
   uint32_t sort_local;       // rounds kernel: sort each chunk's blocks by step count
   uint64_t buf_len;          // log modes: bytes of the log image at base (bounds of every record)
+  // log-stream kernel (crc32c_logstream_kernel) and its gated fallback
+  const uint32_t* first;     // first record of each 32 KiB log block (n_lblocks + 1 entries)
+  uint64_t n_lblocks;        // log blocks in the image
+  uint32_t* ls_flag;         // bit 0: offsets unsorted (pre-pass), bit 1: records overlap
+  uint32_t* ls_bad;          // log-stream mismatch count (added to n_bad unless it falls back)
+  uint32_t* ls_left;         // records the log-stream kernel leaves to the rounds follow-up
+  const uint32_t* gate;      // rounds kernel: run only if *gate != 0 (else fold ls_bad in)
 };
 
 // ---- log records: bounds and status (db/log_reader.cc:228-262) ------------
@@ -145,6 +152,7 @@ constexpr int kVarStamps = 4;    // record per-wave s_memrealtime stamps (diagno
 constexpr int kVarStaticClaims = 8;  // stream kernel: claims without atomics (diagnostics)
 constexpr int kVarNarrow = 16;  // flat/rounds/units: one word's lookups in flight (fold4, A/B)
 constexpr int kVarWide = 32;    // stream kernel: a swath's 16 lookups in flight (fold4w, A/B)
+constexpr int kVarLsFast = 64;  // log-stream kernel: every swath on the fast path (ablation: WRONG CRCs)
 
 // 16-byte load through the global (not flat) address space.  Block bytes are
 // read exactly once, so production loads carry the nt policy: on gfx950 it
@@ -1645,7 +1653,8 @@ __global__ void __launch_bounds__(256) bin_scatter_kernel(CrcParams p, uint64_t 
 #endif  // NOVA_DIAG
 
 template <int G, int MODE, int VAR = 0>
-__global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p) {
+__global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p0) {
+  CrcParams p = p0;  // the log-stream follow-up narrows the batch below
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   constexpr uint32_t kByteTab = kMainBytes + kLevels * kTreeBytes;
@@ -1654,6 +1663,22 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   constexpr uint64_t kStep = 64 * G;
   constexpr uint32_t kGroups = 64 / G;
   static_assert(kByteTab == kMainBytes + kLevels * kTreeBytes, "byte table follows the tree");
+#ifdef NOVA_DIAG
+  if (p.gate) {  // follow-up of the log-stream kernel
+    // gate[0]: precondition flag -> the whole batch; else gate[2] leftover
+    // records listed at p.perm (and the log-stream mismatches fold into n_bad)
+    if (*(volatile const uint32_t*)p.gate == 0) {
+      if (kLog && blockIdx.x == 0 && threadIdx.x == 0 && p.n_bad && p.ls_bad)
+        atomicAdd(p.n_bad, *(volatile const uint32_t*)p.ls_bad);
+      const uint32_t nl = *(volatile const uint32_t*)(p.gate + 2);
+      if (nl == 0) return;
+      p.n_blocks = nl;
+      p.n_chunks = (nl + p.chunk - 1) / p.chunk;
+    } else {
+      p.perm = nullptr;
+    }
+  }
+#endif
   lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, p.tab_byte, 64);
   __syncthreads();
 
@@ -2360,6 +2385,444 @@ __global__ void __launch_bounds__(256) trailer_scatter_kernel(uint8_t* base, con
   }
 }
 
+#ifdef NOVA_DIAG
+// ---- crc32c_logstream_kernel<MODE>: a whole log image, record CRCs ----------
+// MANIFEST / write-ahead-log record CRCs for a log image
+// whose record offsets are in file order.  Each lane group of 8 lanes streams
+// one 32 KiB log block (db/log_format.h:27, kBlockSize) with the stream
+// kernel's uniform schedule -- 4-swath steps of one 128-B line per swath,
+// identical for every group of the wave, no per-record regions and no round
+// padding -- and resolves the block's records on the fly:
+//
+//   * A record's CRC input is [a, b) = [header+6, header+7+length) (type byte +
+//     payload, db/log_writer.cc:99-114).  The group's four stream registers per
+//     lane hold the CURRENT record only.  A swath holding a, a byte of the init
+//     window [a, a+4), or b takes the slow path: each lane masks its 16-B piece
+//     to [a, b) with two 16-B prefix masks from LDS and xors ~0 into [a, a+4)
+//     (Extend's init, as the units kernel); a record that starts in the swath
+//     starts from zero.  Between records (headers, block trailers, records
+//     left to the follow-up) the registers run on unmasked data: the next
+//     record's first swath resets them.
+//   * Only records of >= kLsMinN CRC bytes are streamed, so a group meets at
+//     most one record end and one record start per 128-B swath and the slow
+//     path is straight-line code (no loop, no global memory access -- either
+//     would make the compiler drain the step's prefetch).  Shorter records,
+//     records the reader would not read (bounds / zero records: status only)
+//     and whole blocks of more than 64 records go to a leftover list that the
+//     gated rounds kernel processes right after (crc32c_rounds_kernel, gate).
+//   * At b the group spills its 32 stream words to a per-wave LDS slot
+//     ("snapshot").  Streams whose word of the last swath lies entirely at or
+//     after b keep their value from the swath before (the rounds kernel's
+//     rotation), so the snapshot is a virtual 128-B message ending at the
+//     4-byte word holding b-1: pad = 0..3 bytes.
+//   * Snapshots are folded after the swath once a wave holds kLsFlush of them
+//     (the fold phase): four lanes per record run one Horner chain each (M16
+//     over every 4th word), a 3-step merge (M4) gives the pending word V,
+//     register = M4(V), and `pad` inverse zero-byte steps (bitwise) give the
+//     register at b.  Write: Mask(crc) into the header; verify: compare with
+//     the stored CRC (one status byte per record, mismatches counted).
+//   * Descriptors: a 64-record window per group (8 per lane), decoded at the
+//     start of each block from the offsets and the 7-byte record headers.
+//   * Preconditions (else the follow-up reruns the whole batch): offsets
+//     ascending (pre-pass, flag bit 0) and no streamed record starting before
+//     the previous one ended (flag bit 1).
+// Fast swaths cost what the stream kernel's do; the per-record work runs
+// wave-wide on the swaths that hold a record boundary.
+constexpr int kLsG = 8;                      // lanes per group (one 128-B line per swath)
+constexpr int kLsWaves = 8;                  // waves per workgroup
+constexpr uint32_t kLsSlots = 16;            // snapshot slots per wave
+constexpr uint32_t kLsFlush = kLsSlots - 8;  // fold after a swath leaving this many (<= 8 per swath)
+constexpr uint32_t kLsSlotBytes = 144;       // 32 stream words + 16 B of meta (bank spread)
+constexpr uint32_t kLsM4 = kMainBytes;       // LDS: M4 byte tables (4 KiB)
+constexpr uint32_t kLsM16 = kMainBytes + 4096;
+constexpr uint32_t kLsLM = kMainBytes + 8192;  // 17 x 16-B prefix masks: LM[n] = bytes [0, n)
+constexpr uint32_t kLsTabBytes = 8192 + 17 * 16;
+constexpr uint32_t kLsSlot0 = kMainBytes + kLsTabBytes;
+constexpr uint32_t kLsLds = kLsSlot0 + kLsWaves * kLsSlots * kLsSlotBytes;
+static_assert(kLsLds <= 160 * 1024, "log-stream LDS exceeds the CU");
+static_assert(kLsSlot0 % 16 == 0, "slots are 16-B aligned");
+constexpr int kLsWin = 8;                    // decoded descriptors per lane (64 per group)
+constexpr uint32_t kLsMinN = 128;            // CRC bytes of a streamed record (>= one swath)
+constexpr int32_t kLsFar = 1 << 28;          // "no record": past every swath
+
+__device__ __forceinline__ uint32_t lds_apply(uint32_t tab, uint32_t x) {
+  const uint32_t t0 = lds_u32(nullptr, tab + ((x & 255u) << 2));
+  const uint32_t t1 = lds_u32(nullptr, tab + 1024u + (((x >> 8) & 255u) << 2));
+  const uint32_t t2 = lds_u32(nullptr, tab + 2048u + (((x >> 16) & 255u) << 2));
+  const uint32_t t3 = lds_u32(nullptr, tab + 3072u + ((x >> 24) << 2));
+  return xor3(t0, t1, t2) ^ t3;
+}
+__device__ __forceinline__ uint4 lds_u128(uint32_t a) {
+  const u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const u32x4*>(a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void lds_st128(uint32_t a, uint4 v) {
+  u32x4 w;
+  w.x = v.x;
+  w.y = v.y;
+  w.z = v.z;
+  w.w = v.w;
+  *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(a) = w;
+}
+// Inverse of one zero-byte step of the reflected register (M_1^-1): the forward
+// bit step x' = (x >> 1) ^ (P if x & 1) leaves x & 1 in bit 31 of x' (P has it).
+__device__ __forceinline__ uint32_t unstep_byte(uint32_t x) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t b = x >> 31;
+    x = ((x ^ (0x82F63B78u & (0u - b))) << 1) | b;
+  }
+  return x;
+}
+__device__ __forceinline__ int32_t clamp16(int32_t x) { return x < 0 ? 0 : (x > 16 ? 16 : x); }
+
+typedef __attribute__((address_space(1))) const u32_unaligned gcu32u;
+
+// Pre-pass: first[k] = first record of log block k (record i belongs to block
+// min(off_i / 32 KiB, nb - 1): a record past the image lands in the last block,
+// whose status logic rejects it), first[nb] = n.  Unsorted offsets set bit 0
+// of *flag (the log-stream kernel then leaves the batch to the follow-up).
+__global__ void __launch_bounds__(256) log_first_kernel(const uint64_t* __restrict__ offs, uint64_t n,
+                                                        uint64_t nb, uint32_t* __restrict__ first,
+                                                        uint32_t* flag) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += nth) {
+    const uint64_t o = i < n ? offs[i] : 0;
+    const uint64_t k = i < n ? ((o >> 15) < nb - 1 ? (o >> 15) : nb - 1) : nb;
+    uint64_t k_lo = 0;
+    if (i > 0) {
+      const uint64_t op = offs[i - 1];
+      if (i < n && o < op) atomicOr(flag, 1u);
+      k_lo = ((op >> 15) < nb - 1 ? (op >> 15) : nb - 1) + 1;
+    }
+    for (uint64_t kk = k_lo; kk <= k; kk++) first[kk] = (uint32_t)i;
+  }
+}
+
+template <int MODE, int VAR = 0>
+__global__ void __launch_bounds__(kLsWaves * 64) crc32c_logstream_kernel(CrcParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  static_assert(MODE == kLogWrite || MODE == kLogVerify, "log modes only");
+  constexpr bool kVerifyMode = MODE == kLogVerify;
+  if (*(volatile const uint32_t*)p.ls_flag & 1u) return;  // unsorted: the follow-up takes it
+  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLsTabBytes / 16, nullptr, 0);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane & 7;
+  const int grp = lane >> 3;
+  const uint32_t rep = (uint32_t)(lane & 31) << 2;
+  const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
+  const uint64_t base = (uint64_t)p.base;
+  const uint64_t nb = p.n_lblocks;
+  const uint64_t R = (nb + 7) / 8;                     // rounds: 8 log blocks (one per group)
+  const int32_t off0 = (int32_t)(base & 127u);         // every block starts off0 into its line
+  const uint32_t KG = ((uint32_t)off0 + kLogBlock + 511u) / 512u;  // 4-line steps per block
+  const uint64_t zl = (uint64_t)p.zline;
+  const uint64_t lo_ok = base & ~15ull, hi_ok = (base + p.buf_len + 15) & ~15ull;
+  const uint32_t slots = kLsSlot0 + (uint32_t)wave * kLsSlots * kLsSlotBytes;
+  const uint32_t nwaves = blockDim.x >> 6;
+  const uint32_t nwg = gridDim.x;
+  const uint4 zero4 = make_uint4(0, 0, 0, 0);
+
+  // ---- round claims (per-workgroup counters, bounded stealing)
+  uint32_t victim = blockIdx.x, tried = 0, req = 0;
+  auto claim = [&](uint32_t v) {
+    uint32_t r = 0;
+    if (lane == 0)
+      r = __hip_atomic_fetch_add(p.sched + v * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    req = r;
+  };
+  auto round_of = [&](uint32_t v, uint32_t idx) -> uint64_t {
+    const uint64_t r = ((uint64_t)idx + nwaves) * nwg + v;
+    return r < R ? r : ~0ull;
+  };
+  auto collect = [&]() -> uint64_t {
+    uint64_t r = round_of(victim, __builtin_amdgcn_readfirstlane(req));
+    while (r == ~0ull && ++tried < p.steal_limit + 1) {
+      victim = (victim + 1) % nwg;
+      claim(victim);
+      r = round_of(victim, __builtin_amdgcn_readfirstlane(req));
+    }
+    return r;
+  };
+
+  // ---- per-group block state (group-uniform values, in every lane of it)
+  uint64_t k = 0;                      // log block of the group
+  uint32_t r_lo = 0, nrec = 0;         // its records [r_lo, r_lo + nrec)
+  uint32_t nwin = 0;                   // records in the window (0: dense block, all leftover)
+  uint32_t j = 0;                      // current window position
+  int32_t a_c = kLsFar, b_c = kLsFar;  // current record's CRC range, region-relative
+  uint32_t n_c = 0, ax_c = 0;          // its CRC length, aux (stored CRC)
+  int32_t prev_b = 0;                  // end of the previous streamed record (overlap check)
+  uint32_t wd[kLsWin], wa[kLsWin];     // window: desc = b_rel | n << 16 (n = 0: not streamed), aux
+  uint32_t np = 0;                     // pending snapshots of the wave (wave-uniform)
+  uint32_t ovl = 0;                    // this lane saw overlapping records
+  uint32_t nbad = 0;                   // this lane's mismatches (verify)
+  uint32_t* const left = p.ls_left;    // leftover record list, count at ls_flag[2]
+
+  // Decode the block's records (synchronous; once per block): offsets, then
+  // the 7-byte headers (a header past its block or the image is not read).
+  // Records not streamed here are appended to the leftover list.
+  auto decode_block = [&](uint64_t bk) {
+    const bool dense = nrec > 8u * kLsWin;
+    nwin = dense ? 0u : nrec;
+    uint64_t o[kLsWin];
+#pragma unroll
+    for (int m = 0; m < kLsWin; m++) {
+      const uint32_t jj = 8u * m + (uint32_t)q;
+      o[m] = jj < nwin ? p.offsets[r_lo + jj] : 0;
+    }
+    uint32_t nl = 0;  // this lane's leftovers
+#pragma unroll
+    for (int m = 0; m < kLsWin; m++) {
+      const uint32_t jj = 8u * m + (uint32_t)q;
+      const bool valid = jj < nwin;
+      const bool fits = valid && log_header_fits(o[m], p.buf_len);
+      const uint64_t h = fits ? base + o[m] : zl;
+      const uint32_t w0 = kVerifyMode ? *(gcu32u*)h : 0u;  // stored masked CRC
+      const uint32_t w1 = *(gcu32u*)(fits ? h + 4 : zl);    // length, type
+      const uint32_t length = w1 & 0xffffu;
+      const uint32_t st = fits ? log_status(o[m], length, kVerifyMode ? ((w1 >> 16) & 0xffu) : 1u,
+                                            p.buf_len)
+                               : NOVA_LOG_BAD_LENGTH;
+      const bool elig = st == NOVA_LOG_OK && 1u + length >= kLsMinN;
+      const uint64_t hrel = o[m] - bk * kLogBlock;
+      wd[m] = elig ? ((uint32_t)hrel + 7u + length) | ((1u + length) << 16) : 0u;
+      wa[m] = kVerifyMode ? w0 : 0u;
+      nl += (valid && !elig) ? 1u : 0u;
+    }
+    // leftover list: the whole block if dense, else the records not streamed
+    uint32_t cnt = dense ? (nrec > (uint32_t)q ? (nrec - 1u - (uint32_t)q) / 8u + 1u : 0u) : nl;
+    uint32_t incl = cnt;  // inclusive prefix over the group's 8 lanes
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, (unsigned)d, 8);
+      if (q >= d) incl += y;
+    }
+    const uint32_t total = __shfl(incl, (grp << 3) | 7);
+    uint32_t at = 0;
+    if (q == 0 && total) at = atomicAdd(p.ls_flag + 2, total);
+    at = __shfl(at, grp << 3);
+    if (dense) {
+      for (uint32_t i = (uint32_t)q; i < nrec; i += 8) left[at + i] = r_lo + i;
+    } else {
+      uint32_t pos = at + incl - cnt;
+#pragma unroll
+      for (int m = 0; m < kLsWin; m++) {
+        const uint32_t jj = 8u * m + (uint32_t)q;
+        if (jj < nwin && (wd[m] >> 16) == 0) left[pos++] = r_lo + jj;
+      }
+    }
+  };
+  // Current record := the first streamed record at window position >= j.
+  auto fetch = [&]() {
+    for (;;) {
+      if (j >= nwin) {
+        a_c = b_c = kLsFar;
+        n_c = 0;
+        return;
+      }
+      const uint32_t m = j >> 3;
+      uint32_t dsel = wd[0], asel = wa[0];
+#pragma unroll
+      for (int mm = 1; mm < kLsWin; mm++) {
+        if (m == (uint32_t)mm) {
+          dsel = wd[mm];
+          asel = wa[mm];
+        }
+      }
+      const int src = (grp << 3) | (int)(j & 7u);
+      const uint32_t d = __shfl(dsel, src);
+      if ((d >> 16) != 0) {
+        n_c = d >> 16;
+        b_c = off0 + (int32_t)(d & 0xffffu);
+        a_c = b_c - (int32_t)n_c;
+        ax_c = kVerifyMode ? __shfl(asel, src) : 0u;
+        if (a_c - 6 < prev_b) ovl = 1;  // starts inside the previous streamed record
+        prev_b = b_c;
+        return;
+      }
+      j++;
+    }
+  };
+
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+
+  // ---- fold phase: four lanes per pending snapshot ----------------------------
+  // A wave's LDS operations execute in order, so other lanes' snapshot stores
+  // are visible to the reads below once the compiler keeps the order (memory
+  // clobber); a wavefront-scope fence would also drain the step's data loads.
+  auto lds_order = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  auto fold_phase = [&]() {
+    lds_order();
+    const uint32_t rec = (uint32_t)lane >> 2, sub = (uint32_t)lane & 3u;
+    const bool act = rec < np;
+    const uint32_t sa = slots + (act ? rec : 0u) * kLsSlotBytes;
+    const uint4 meta = lds_u128(sa + 128);
+    const uint32_t info = meta.w;
+    const uint32_t kb = (info >> 16) & 31u, pad = (info >> 21) & 3u;
+    // chain `sub`: words kb+1+jj (mod 32) of the rotated message, jj = sub, sub+4, ...
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t jj = 0; jj < 32; jj += 4)
+      v = lds_apply(kLsM16, v) ^ lds_u32(nullptr, sa + (((kb + 1u + jj + sub) & 31u) << 2));
+    const int b4 = lane & ~3;
+    const uint32_t u0 = __shfl(v, b4), u1 = __shfl(v, b4 + 1), u2 = __shfl(v, b4 + 2);
+    const uint32_t u3 = __shfl(v, b4 + 3);
+    const uint32_t V = lds_apply(kLsM4, lds_apply(kLsM4, lds_apply(kLsM4, u0) ^ u1) ^ u2) ^ u3;
+    uint32_t reg = lds_apply(kLsM4, V);
+    if (pad >= 1) reg = unstep_byte(reg);
+    if (pad >= 2) reg = unstep_byte(reg);
+    if (pad >= 3) reg = unstep_byte(reg);
+    const uint32_t crc = ~reg;
+    if (act && sub == 0) {
+      if constexpr (MODE == kLogWrite) {
+        const uint64_t h = base + (uint64_t)meta.z * kLogBlock + (info & 0xffffu);
+        store_u32_unaligned((uint8_t*)h, mask_crc(crc));
+      } else {
+        const bool ok = unmask_crc(meta.y) == crc;
+        *(__attribute__((address_space(1))) uint8_t*)(p.ok_out + meta.x) =
+            (uint8_t)(ok ? NOVA_LOG_OK : NOVA_LOG_CHECKSUM_MISMATCH);
+        nbad += ok ? 0u : 1u;
+      }
+    }
+    np = 0;
+    lds_order();
+  };
+
+  // ---- one swath: line L0 (region-relative byte) of the group's block --------
+  auto swath = [&](const uint4 d, int32_t L0) {
+    const bool st = (a_c + 4 > L0) && (a_c < L0 + 128);
+    const bool en = b_c <= L0 + 128;
+    if ((VAR & kVarLsFast) != 0 || __builtin_amdgcn_ballot_w64(st || en) == 0) {
+      swath4(lds, c0, c1, c2, c3, d, lo0, lo1, lo2, lo3);
+      return;
+    }
+    // slow path: a record of some group starts or ends in this swath
+    const int32_t P = L0 + 16 * q;
+    const uint32_t o0 = c0, o1 = c1, o2 = c2, o3 = c3;
+    uint32_t t0 = c0, t1 = c1, t2 = c2, t3 = c3;
+    swath4(lds, t0, t1, t2, t3, zero4, lo0, lo1, lo2, lo3);  // T(c): the record goes on
+    const bool cont = a_c < L0;  // the current record began in an earlier swath
+    const uint32_t km = cont ? ~0u : 0u;
+    uint32_t r0, r1, r2, r3;
+    {  // r = (cont ? T(c) : 0) ^ (((d & LM[hi]) ^ LM[lo4]) & ~LM[lo])
+      const int32_t lo = clamp16(a_c - P), hi = clamp16(b_c - P), lo4 = clamp16(a_c + 4 - P);
+      const uint4 A = lds_u128(kLsLM + 16u * (uint32_t)hi);
+      const uint4 B = lds_u128(kLsLM + 16u * (uint32_t)lo);
+      const uint4 Cm = lds_u128(kLsLM + 16u * (uint32_t)lo4);
+      r0 = (t0 & km) ^ (((d.x & A.x) ^ Cm.x) & ~B.x);
+      r1 = (t1 & km) ^ (((d.y & A.y) ^ Cm.y) & ~B.y);
+      r2 = (t2 & km) ^ (((d.z & A.z) ^ Cm.z) & ~B.z);
+      r3 = (t3 & km) ^ (((d.w & A.w) ^ Cm.w) & ~B.w);
+    }
+    const uint64_t eb = __builtin_amdgcn_ballot_w64(en);
+    if (eb == 0) {  // starts only
+      c0 = r0;
+      c1 = r1;
+      c2 = r2;
+      c3 = r3;
+      return;
+    }
+    const uint64_t leaders = eb & 0x0101010101010101ull;
+    if (en) {  // snapshot the ending record, then take the group's next one
+      const int32_t kb = (b_c - 1 - L0) >> 2;  // stream holding byte b-1 (b > L0: n >= 128)
+      const uint32_t pad = (uint32_t)(4 * (kb + 1) - (b_c - L0));
+      const int k0 = 4 * q;
+      uint4 sn;
+      sn.x = (k0 + 0 > kb) ? (o0 & km) : r0;
+      sn.y = (k0 + 1 > kb) ? (o1 & km) : r1;
+      sn.z = (k0 + 2 > kb) ? (o2 & km) : r2;
+      sn.w = (k0 + 3 > kb) ? (o3 & km) : r3;
+      const uint64_t below = leaders & ((1ull << (grp * 8)) - 1ull);
+      const uint32_t sa = slots + (np + (uint32_t)__popcll(below)) * kLsSlotBytes;
+      lds_st128(sa + 16u * (uint32_t)q, sn);
+      if (q == 0) {
+        const uint32_t hrel = (uint32_t)(a_c - off0) - 6u;  // the record's header
+        lds_st128(sa + 128, make_uint4(r_lo + j, ax_c, (uint32_t)k,
+                                       hrel | ((uint32_t)kb << 16) | (pad << 21)));
+      }
+      j++;
+      fetch();
+    }
+    np += (uint32_t)__popcll(leaders);
+    // the ending groups' next record starts from zero (it may start in this swath;
+    // it cannot also end in it)
+    const int32_t lo = clamp16(a_c - P), hi = clamp16(b_c - P), lo4 = clamp16(a_c + 4 - P);
+    const uint4 A = lds_u128(kLsLM + 16u * (uint32_t)hi);
+    const uint4 B = lds_u128(kLsLM + 16u * (uint32_t)lo);
+    const uint4 Cm = lds_u128(kLsLM + 16u * (uint32_t)lo4);
+    c0 = en ? (((d.x & A.x) ^ Cm.x) & ~B.x) : r0;
+    c1 = en ? (((d.y & A.y) ^ Cm.y) & ~B.y) : r1;
+    c2 = en ? (((d.z & A.z) ^ Cm.z) & ~B.z) : r2;
+    c3 = en ? (((d.w & A.w) ^ Cm.w) & ~B.w) : r3;
+  };
+
+  // ---- rounds ---------------------------------------------------------------
+  uint64_t r = (uint64_t)wave * nwg + blockIdx.x;  // implicit first round
+  if (r >= R) {
+    claim(victim);
+    r = collect();
+  }
+  while (r != ~0ull) {
+    claim(victim);  // the next round (collected after this one)
+    k = r * 8 + (uint64_t)grp;
+    const bool act = k < nb;
+    r_lo = act ? p.first[k] : 0u;
+    nrec = act ? p.first[k + 1] - r_lo : 0u;
+    const uint64_t bstart = k * kLogBlock;
+    const uint32_t blen =
+        act ? (uint32_t)(p.buf_len - bstart < kLogBlock ? p.buf_len - bstart : kLogBlock) : 0u;
+    const uint64_t RS = base + bstart - (uint64_t)off0;  // region start: 128-B aligned
+    const uint32_t lines = act ? ((uint32_t)off0 + blen + 127u) / 128u : 0u;
+    decode_block(k);
+    j = 0;
+    prev_b = 0;
+    fetch();
+    c0 = c1 = c2 = c3 = 0;
+    auto piece = [&](uint32_t line) -> uint64_t {
+      const uint64_t a = RS + 128ull * line + 16u * (uint32_t)q;
+      return (line < lines && a >= lo_ok && a < hi_ok) ? a : zl;
+    };
+    uint4 b0 = gload16(piece(0)), b1 = gload16(piece(1));
+    uint4 b2 = gload16(piece(2)), b3 = gload16(piece(3));
+    for (uint32_t s = 0; s < KG; s++) {
+      const uint4 x0 = b0, x1 = b1, x2 = b2, x3 = b3;
+      const uint32_t ln = 4 * s + 4;
+      b0 = gload16(piece(ln));
+      b1 = gload16(piece(ln + 1));
+      b2 = gload16(piece(ln + 2));
+      b3 = gload16(piece(ln + 3));
+      const int32_t L = (int32_t)(512 * s);
+      swath(x0, L);
+      if (np >= kLsFlush) fold_phase();
+      swath(x1, L + 128);
+      if (np >= kLsFlush) fold_phase();
+      swath(x2, L + 256);
+      if (np >= kLsFlush) fold_phase();
+      swath(x3, L + 384);
+      if (np >= kLsFlush) fold_phase();
+    }
+    r = collect();
+  }
+  if (np) fold_phase();
+  if constexpr ((VAR & kVarLsFast) != 0)  // keep the ablation's stream live
+    if ((c0 ^ c1 ^ c2 ^ c3) == 0x9e3779b9u) atomicOr(p.ls_flag, 4u);
+  if (__builtin_amdgcn_ballot_w64(ovl != 0) && lane == 0) atomicOr(p.ls_flag, 2u);
+  if constexpr (kVerifyMode) {
+    if (__builtin_amdgcn_ballot_w64(nbad != 0)) {
+      uint32_t v = nbad;
+      for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) atomicAdd(p.ls_bad, v);
+    }
+  }
+  sched_release(p.sched);
+}
+
+#endif  // NOVA_DIAG
+
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
 __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                        uint64_t first_word) {
@@ -2442,6 +2905,7 @@ struct DevTables {
   uint32_t* byte8 = nullptr;      // M_1 byte table (flat kernel tail steps)
   uint32_t* op1024 = nullptr;     // M_1024 byte tables (burst kernel stream step)
   uint32_t* op1024r = nullptr;    // the same, 16-way bank-replicated
+  uint32_t* ls_tabs = nullptr;    // log-stream kernel LDS tail: M4, M16 byte tables, 17 prefix masks
   int cus = 0;
   int err = 0;
   // Claim counters, one 16 KiB slot per HIP stream (256 workgroups x 64 B).
@@ -2651,6 +3115,30 @@ void init_device(int dev, DevTables* t) {
     if ((t->err = upload(&t->op1024r, rep))) return;
 #endif
   }
+#ifdef NOVA_DIAG  // log-stream experiment
+  {
+    std::vector<uint32_t> ls;
+    append_op(power(m1, 4), ls);
+    append_op(power(m1, 16), ls);
+    for (uint32_t nbytes = 0; nbytes <= 16; nbytes++)
+      for (uint32_t w = 0; w < 4; w++) {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 4; b++)
+          if (4 * w + b < nbytes) v |= 0xffu << (8 * b);
+        ls.push_back(v);
+      }
+    if ((t->err = upload(&t->ls_tabs, ls))) return;
+    for (const void* f : {reinterpret_cast<const void*>(&crc32c_logstream_kernel<kLogWrite>),
+                          reinterpret_cast<const void*>(&crc32c_logstream_kernel<kLogVerify>),
+#ifdef NOVA_DIAG
+                          reinterpret_cast<const void*>(&crc32c_logstream_kernel<kLogWrite, kVarLsFast>),
+#endif
+                          })
+      if ((t->err = (int)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)kLsLds)))
+        return;
+  }
+#endif
   if ((t->err = set_lds_attrs_rounds<kStore>())) return;
   if ((t->err = set_lds_attrs_rounds<kTrailer>())) return;
   if ((t->err = set_lds_attrs_rounds<kVerify>())) return;
@@ -2754,7 +3242,7 @@ uint64_t flat_waves() {
   const int w = waves_per_wg(kFlatWaves);
   return w > kFlatMaxWaves ? kFlatMaxWaves : w;
 }
-enum VarKernel { kAuto = 0, kUnitsK = 1, kFlatK = 2, kRoundsK = 3 };
+enum VarKernel { kAuto = 0, kUnitsK = 1, kFlatK = 2, kRoundsK = 3, kLogStreamK = 4 };
 thread_local std::atomic<int> g_tune_kernel{0};
 struct Plan {
   int kernel;
@@ -2789,7 +3277,7 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, b
   const int tk = g_tune_kernel.load();
   const int tg = g_tune_g.load();
   const uint32_t ts = g_tune_seg.load();
-  if (tk != kAuto) pl.kernel = tk;
+  if (tk != kAuto && tk != kLogStreamK) pl.kernel = tk;
   if (ts) pl.kernel = kUnitsK;  // a forced segment size is a units-kernel setting
   if (tg == 1 || tg == 2 || tg == 4 || tg == 8 || tg == 16) pl.G = tg;
   if (ts) pl.seg = ts & ~15u;
@@ -3074,7 +3562,7 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_
     p.init = t->zero_word;
     p.imask = 0;
   }
-  p.perm = nullptr;
+  if (!p.gate) p.perm = nullptr;  // (the log-stream follow-up passes its leftover list)
   const int sort = g_tune_sort.load();  // 0 none, 1 whole batch (pre-pass), 2 per chunk
   p.sort_local = sort == 2 ? 1u : 0u;
 #ifdef NOVA_DIAG
@@ -3236,6 +3724,60 @@ int launch_burst_g(int V, CrcParams& p, DevTables* t, hipStream_t stream) {
   return launch_burst<64, MODE>(p, t, stream);
 }
 
+#ifdef NOVA_DIAG
+// Log-stream experiment (nova_diag_set_variable_kernel(4)):
+// a pre-pass finds each 32 KiB block's first record, the log-stream kernel
+// streams the image, and the rounds kernel follows, gated: the leftover list,
+// or the whole batch if a precondition failed.  Measured slower than the
+// rounds kernel on 2 KiB-average records, so the product does not use it.
+template <int MODE>
+int launch_logstream(CrcParams& p, DevTables* t, hipStream_t stream) {
+  const uint64_t nb = (p.buf_len + kLogBlock - 1) / kLogBlock;
+  // [flag, mismatches, leftovers, -, first[0..nb], leftover list[n]], freed in stream order
+  StreamScratch sc;
+  const uint64_t left_at = (4 + nb + 1 + 3) & ~3ull;
+  if (sc.alloc((left_at + p.n_blocks) * sizeof(uint32_t), stream)) return NOVA_E_NOMEM;
+  uint32_t* w = static_cast<uint32_t*>(sc.p);
+  hipError_t e = hipMemsetAsync(w, 0, 16, stream);
+  if (e != hipSuccess) return (int)e;
+  uint32_t* first = w + 4;
+  uint64_t fwgs = (p.n_blocks + 1 + 255) / 256;
+  if (fwgs > (uint64_t)t->cus * 8) fwgs = (uint64_t)t->cus * 8;
+  hipLaunchKernelGGL(log_first_kernel, dim3(fwgs), dim3(256), 0, stream, p.offsets, p.n_blocks, nb,
+                     first, w);
+  CrcParams s = p;
+  s.first = first;
+  s.n_lblocks = nb;
+  s.ls_flag = w;
+  s.ls_bad = w + 1;
+  s.ls_left = w + left_at;
+  s.tab_main = t->main[gindex(kLsG)];
+  s.tab_tree = t->ls_tabs;
+  s.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
+  const uint64_t R = (nb + 7) / 8;
+  uint64_t wgs = (R + kLsWaves - 1) / kLsWaves;
+  if (wgs > (uint64_t)t->cus) wgs = t->cus;
+  if (wgs > 256) wgs = 256;
+  s.steal_limit = R <= wgs * kLsWaves ? 0u : 8u;
+  s.sched = sched_slot(t, stream);
+  if (!s.sched) return NOVA_E_NOMEM;
+#ifdef NOVA_DIAG
+  if (MODE == kLogWrite && g_tune_var.load() == kVarLsFast)
+    hipLaunchKernelGGL((crc32c_logstream_kernel<kLogWrite, kVarLsFast>), dim3(wgs), dim3(64 * kLsWaves),
+                       kLsLds, stream, s);
+  else
+#endif
+    hipLaunchKernelGGL(crc32c_logstream_kernel<MODE>, dim3(wgs), dim3(64 * kLsWaves), kLsLds, stream, s);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  CrcParams f = p;  // follow-up: the leftover list, or the whole batch if flagged
+  f.gate = w;
+  f.ls_bad = w + 1;
+  f.perm = w + left_at;
+  const Plan pl = plan(p.n_blocks, 0, false, MODE, false, (uint32_t)t->cus);
+  return launch_rounds<MODE>(pl.G, f, t, stream, pl.chunk);
+}
+#endif  // NOVA_DIAG
+
 int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStream_t stream) {
   int err = 0;
   DevTables* t = tables(&err);
@@ -3248,6 +3790,12 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
       default: return launch_burst_g<kVerify>(bg, p, t, stream);
     }
   }
+#ifdef NOVA_DIAG
+  if ((mode == kLogWrite || mode == kLogVerify) && p.n_blocks < (1ull << 31) &&
+      g_tune_kernel.load() == kLogStreamK)
+    return mode == kLogWrite ? launch_logstream<kLogWrite>(p, t, stream)
+                             : launch_logstream<kLogVerify>(p, t, stream);
+#endif
   if (mode == kStore && uniform && !g_tune_seg.load()) {
     const int sg = stream_lanes(p);
     if (sg) return launch_stream(sg, p, t, stream);

@@ -702,13 +702,23 @@ def test_concurrent_host_threads(torch_gpu, oracle):
             assert np.array_equal(r, want)
 
 
-def test_log_records_write_verify(torch_gpu, golden, oracle):
+@pytest.mark.parametrize("kernel", ["default", "logstream"])
+def test_log_records_write_verify(torch_gpu, golden, oracle, kernel):
     """MANIFEST/WAL record CRCs (db/log_writer.cc:99-114,
     db/log_reader.cc:196-262) against the reference-generated log fixture (a
     log::Writer layout with FULL/FIRST/MIDDLE/LAST fragments over ~20 blocks),
-    then the reader's per-record statuses against the oracle."""
+    then the reader's per-record statuses against the oracle.  "logstream"
+    forces the whole-image kernel (the product picks it for logs >= 64 MiB)."""
+    if kernel == "logstream":
+        with C.diagnostics() as L:
+            L.nova_diag_set_variable_kernel(4)
+            _golden_log_checks(torch_gpu, golden, oracle)
+    else:
+        _golden_log_checks(torch_gpu, golden, oracle)
+
+
+def _golden_log_checks(torch, golden, oracle):
     from tests.test_oracle_golden import golden_log_image
-    torch = torch_gpu
     host, offs = golden_log_image(golden)
     buf = dev(torch, host)
     doffs = dev(torch, offs, torch.int64)
@@ -728,7 +738,7 @@ def test_log_records_write_verify(torch_gpu, golden, oracle):
     assert np.array_equal(ok.cpu().numpy(), oracle.log_check(buf.cpu().numpy(), offs))
 
 
-@pytest.mark.parametrize("kernel", ["default", "units"])
+@pytest.mark.parametrize("kernel", ["default", "units", "logstream"])
 def test_log_record_bounds(torch_gpu, golden, oracle, kernel):
     """ADVICE r01 / db/log_reader.cc:196-247: a record whose length field runs
     past its 32 KiB block or the image is never read (bad length, counted; or
@@ -756,10 +766,13 @@ def test_log_record_bounds(torch_gpu, golden, oracle, kernel):
     offs_x = np.concatenate([offs, np.array([cut - 2, cut + 100], np.uint64)])
     buf = dev(torch, np.concatenate([host, np.zeros(256, np.uint8)]))
     doffs = dev(torch, offs_x, torch.int64)
-    ctx = C.diagnostics() if kernel == "units" else None
+    ctx = C.diagnostics() if kernel != "default" else None
     if ctx:
-        ctx.__enter__()
-        C.set_tuning(16, 4096)  # forced segments: the units kernel's log path
+        L = ctx.__enter__()
+        if kernel == "units":
+            C.set_tuning(16, 4096)  # forced segments: the units kernel's log path
+        else:
+            L.nova_diag_set_variable_kernel(4)
     try:
         st, bad = C.log_verify_records(buf, doffs, buf_len=cut)
         want = oracle.log_check(host, offs_x, buf_len=cut)
@@ -878,12 +891,14 @@ def _many_blocks_checks(torch, oracle, lanes, chunk, waves):
 @pytest.mark.parametrize("kernel,lanes,chunk", [
     (0, 0, 0), (1, 4, 0), (1, 16, 0), (2, 0, 0), (2, 2, 0), (2, 4, 0), (2, 8, 0), (2, 16, 0),
     (2, 8, 16), (2, 4, 17), (2, 16, 64), (3, 0, 0), (3, 2, 0), (3, 4, 0), (3, 16, 0),
-    (3, 8, 16), (3, 8, 32), (3, 16, 16), (3, 8, 8)])
+    (3, 8, 16), (3, 8, 32), (3, 16, 16), (3, 8, 8), (4, 0, 0)])
 def test_log_many_records(torch_gpu, oracle, kernel, lanes, chunk):
     """Log record CRC write + verify over a log::Writer image (db/log_writer.cc:
     53-114) with enough records to exercise every kernel's header pipeline
     (db/log_reader.cc:249-262), every lane count and chunk size; kernel 0 is
-    the product dispatch, 1-3 force units / flat / rounds (diagnostics build)."""
+    the product dispatch, 1-3 force units / flat / rounds, 4 the log-stream
+    kernel (diagnostics build).  ~90 records per 32 KiB block: the log-stream
+    kernel reloads its 64-record windows and folds mid-swath."""
     torch = torch_gpu
     if kernel == 0:
         _log_many_checks(torch, oracle, lanes, chunk)
@@ -1007,3 +1022,140 @@ def test_batch_size_dispatch_thresholds(torch_gpu, oracle, n):
     else:
         want_chunk = 32 if n >= 196608 else 16 if n >= 98304 else 8
         assert d["chunk_blocks"] == want_chunk and d["lanes_per_block"] == 8
+
+
+def _log_stream_image(torch, seed, plen, pad=256, shift=0):
+    """A log::Writer image (novalsm_amd/synth.log_image) on the device, placed
+    `shift` bytes into its allocation (the image start need not be aligned)."""
+    from novalsm_amd.synth import log_image
+    host, offs, _, _ = log_image(seed, plen)
+    full = np.zeros(shift + host.size + pad, np.uint8)
+    full[shift:shift + host.size] = host
+    t = dev(torch, full)
+    return host, offs, t[shift:shift + host.size]
+
+
+@pytest.mark.parametrize("shape", ["u4096", "tiny", "fragments", "mixed"])
+@pytest.mark.parametrize("shift", [0, 5, 64, 127])
+def test_logstream_kernel(torch_gpu, oracle, shape, shift):
+    """The log-stream kernel (DESIGN.md 3.5e) on log::Writer images of every
+    record-size regime -- U[1,4096] B payloads (the bench shape), tiny records
+    (payload 0..40 B: hundreds per block, several ending in one swath, window
+    reloads), 30-70 KB logical records (every block one fragment) and a mix --
+    at image starts 0/5/64/127 bytes into a 128-B line.  Write equals the
+    oracle's log::Writer CRCs byte for byte over the whole image; verify
+    reports every record OK, then exactly the corrupted ones."""
+    torch = torch_gpu
+    rng = np.random.default_rng(hash((shape, shift)) % 2**32)
+    if shape == "u4096":
+        plen = rng.integers(1, 4097, 3000)
+    elif shape == "tiny":
+        plen = rng.integers(0, 41, 40000)
+    elif shape == "fragments":
+        plen = rng.integers(30000, 70000, 60)
+    else:
+        plen = np.concatenate([rng.integers(0, 4, 2000), rng.integers(1, 4097, 2000),
+                               rng.integers(30000, 70000, 10), rng.integers(0, 300, 3000)])
+        rng.shuffle(plen)
+    host, offs, buf = _log_stream_image(torch, 17 + shift, plen, shift=shift)
+    doffs = dev(torch, offs, torch.int64)
+    want = host.copy()
+    oracle.log_write(want, offs)
+    with C.diagnostics() as L:
+        L.nova_diag_set_variable_kernel(4)
+        for _ in range(2):  # dynamic schedule: two launches
+            C.log_write_crcs(buf, doffs)
+            got = buf.cpu().numpy()
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (bad[:8], np.searchsorted(offs.astype(np.int64), bad[:8], "right") - 1)
+        ok, nbad = C.log_verify_records(buf, doffs)
+        assert (ok.cpu().numpy() == C.LOG_OK).all() and int(nbad.item()) == 0
+        victims = rng.choice(len(offs), min(40, len(offs)), replace=False)
+        for v in victims:
+            buf[int(offs[v]) + 6] ^= 0x02  # type byte: covered by the CRC, record stays readable
+        ok, nbad = C.log_verify_records(buf, doffs)
+        okh = ok.cpu().numpy()
+        assert np.array_equal(okh, oracle.log_check(buf.cpu().numpy(), offs))
+        assert sorted(np.nonzero(okh == C.LOG_CHECKSUM_MISMATCH)[0].tolist()) == sorted(victims.tolist())
+        assert int(nbad.item()) == len(victims)
+
+
+@pytest.mark.parametrize("case", ["unsorted", "overlap", "subset", "gaps"])
+def test_logstream_preconditions(torch_gpu, oracle, case):
+    """The log-stream kernel's preconditions and their gated fallback: offsets
+    out of file order (pre-pass flag) or a read record starting inside the
+    previous one (in-kernel flag) rerun the batch on the rounds kernel -- the
+    statuses and the mismatch count equal the oracle's and are counted once.
+    A sparse subset of records ("subset") and every other record ("gaps") stay
+    on the log-stream kernel: the skipped records are masked out like block
+    trailers, and write touches only the selected headers."""
+    torch = torch_gpu
+    rng = np.random.default_rng(31)
+    plen = rng.integers(1, 2000, 4000)
+    host, offs, buf = _log_stream_image(torch, 5, plen)
+    blank = host.copy()  # CRC fields not yet written
+    oracle.log_write(host, offs)
+    n = len(offs)
+    for v in rng.choice(n, 30, replace=False):
+        host[int(offs[v]) + 9] ^= 0x10  # payload byte (or the next header): mismatches
+    buf.copy_(torch.from_numpy(host))
+    o = offs.copy()
+    if case == "unsorted":
+        o = o[rng.permutation(n)]
+    elif case == "overlap":
+        o = np.sort(np.concatenate([o, o[rng.choice(n, 5, replace=False)] + 3])).astype(np.uint64)
+    elif case == "subset":
+        o = np.sort(o[rng.choice(n, n // 7, replace=False)]).astype(np.uint64)
+    else:
+        o = o[::2].copy()
+    want = oracle.log_check(host, o)
+    with C.diagnostics() as L:
+        L.nova_diag_set_variable_kernel(4)
+        ok, nbad = C.log_verify_records(buf, dev(torch, o, torch.int64))
+    assert np.array_equal(ok.cpu().numpy(), want)
+    assert int(nbad.item()) == int(((want == 0) | (want == 2)).sum())
+    if case in ("subset", "gaps"):  # write: the selected records only
+        fresh = dev(torch, blank)
+        exp = blank.copy()
+        oracle.log_write(exp, o)
+        with C.diagnostics() as L:
+            L.nova_diag_set_variable_kernel(4)
+            C.log_write_crcs(fresh, dev(torch, o, torch.int64))
+        assert np.array_equal(fresh.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("kernel", ["default", "logstream"])
+def test_log_96mib(torch_gpu, oracle, kernel):
+    """A 96 MiB log::Writer image with U[1,4096] B payloads (the bench_ops log
+    shape): write is bit-exact over the whole image vs the oracle, verify is
+    clean, and after 64 type bytes are flipped the statuses and the count
+    equal the oracle's -- through the product dispatch and through the
+    log-stream experiment (diagnostics build)."""
+    if kernel == "logstream":
+        with C.diagnostics() as L:
+            L.nova_diag_set_variable_kernel(4)
+            _log_96mib_checks(torch_gpu, oracle)
+    else:
+        _log_96mib_checks(torch_gpu, oracle)
+
+
+def _log_96mib_checks(torch_gpu, oracle):
+    torch = torch_gpu
+    rng = np.random.default_rng(8)
+    plen = rng.integers(1, 4097, (96 << 20) // 2055)
+    host, offs, buf = _log_stream_image(torch, 23, plen)
+    assert host.size >= 64 << 20
+    doffs = dev(torch, offs, torch.int64)
+    want = host.copy()
+    oracle.log_write(want, offs)
+    C.log_write_crcs(buf, doffs)
+    assert np.array_equal(buf.cpu().numpy(), want)
+    ok, nbad = C.log_verify_records(buf, doffs)
+    assert (ok.cpu().numpy() == C.LOG_OK).all() and int(nbad.item()) == 0
+    victims = rng.choice(len(offs), 64, replace=False)
+    for v in victims:
+        buf[int(offs[v]) + 6] ^= 0x02  # type byte (covered by the CRC)
+    ok, nbad = C.log_verify_records(buf, doffs)
+    want_st = oracle.log_check(buf.cpu().numpy(), offs)
+    assert np.array_equal(ok.cpu().numpy(), want_st)
+    assert int(nbad.item()) == int(((want_st == 0) | (want_st == 2)).sum()) >= 60

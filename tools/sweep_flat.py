@@ -9,7 +9,8 @@ Workloads (all device-resident, splitmix64 data):
 
 Variants: "flat:G:chunk:waves:var" (flat kernel), "units:G:seg:waves:var"
 (units kernel, segment size forced) or "rounds:G:chunk*4+sort:waves:var"
-(sort 0 none, 1 batch pre-pass, 2 or 3 per chunk; chunk 0 = default).  var 1 = no-lookup ablation (timing only).
+(sort 0 none, 1 batch pre-pass, 2 or 3 per chunk; chunk 0 = default), or
+"logstream:0:0:0:0" (the whole-image log-record kernel).  var 1 = no-lookup ablation (timing only).
 Prints one line per (workload, variant); writes gpurun_out/sweep_flat.json.
 """
 from __future__ import annotations
@@ -102,7 +103,11 @@ def set_variant(C, v: str) -> None:
     g, x, w, var = int(g), int(x), int(w), int(var)
     L.nova_diag_set_variant(var)
     L.nova_diag_set_stream_waves(w)
-    if kind == "flat":
+    if kind == "logstream":  # whole-image log kernel (log workloads only)
+        L.nova_diag_set_variable_kernel(4)
+        C.set_tuning(0, 0)
+        L.nova_diag_set_chunk_blocks(0)
+    elif kind == "flat":
         L.nova_diag_set_variable_kernel(2)
         C.set_tuning(g, 0)
         L.nova_diag_set_chunk_blocks(x)
