@@ -153,6 +153,7 @@ constexpr int kVarStaticClaims = 8;  // stream kernel: claims without atomics (d
 constexpr int kVarNarrow = 16;  // flat/rounds/units: one word's lookups in flight (fold4, A/B)
 constexpr int kVarWide = 32;    // stream kernel: a swath's 16 lookups in flight (fold4w, A/B)
 constexpr int kVarLsFast = 64;  // log-stream kernel: every swath on the fast path (ablation: WRONG CRCs)
+constexpr int kVarInit = 128;   // rounds kernel, store mode: per-block init values (general head masking)
 
 // 16-byte load through the global (not flat) address space.  Block bytes are
 // read exactly once, so production loads carry the nt policy: on gfx950 it
@@ -366,6 +367,40 @@ __device__ __forceinline__ void store_trailer(uint8_t* d, uint32_t type, uint32_
   *(__attribute__((address_space(1))) uint8_t*)d = (uint8_t)type;
   store_u32_unaligned(d + 1, quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m);
 }
+
+// LDS helpers for tables at absolute LDS addresses (the dynamic region starts
+// at 0): a 4-lookup operator application, 16-B loads/stores, and the 16-B
+// prefix masks LM[n] (bytes [0, n) set) indexed by a clamped byte count.
+__device__ __forceinline__ uint32_t lds_apply(uint32_t tab, uint32_t x) {
+  const uint32_t t0 = lds_u32(nullptr, tab + ((x & 255u) << 2));
+  const uint32_t t1 = lds_u32(nullptr, tab + 1024u + (((x >> 8) & 255u) << 2));
+  const uint32_t t2 = lds_u32(nullptr, tab + 2048u + (((x >> 16) & 255u) << 2));
+  const uint32_t t3 = lds_u32(nullptr, tab + 3072u + ((x >> 24) << 2));
+  return xor3(t0, t1, t2) ^ t3;
+}
+__device__ __forceinline__ uint4 lds_u128(uint32_t a) {
+  const u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const u32x4*>(a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void lds_st128(uint32_t a, uint4 v) {
+  u32x4 w;
+  w.x = v.x;
+  w.y = v.y;
+  w.z = v.z;
+  w.w = v.w;
+  *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(a) = w;
+}
+// Inverse of one zero-byte step of the reflected register (M_1^-1): the forward
+// bit step x' = (x >> 1) ^ (P if x & 1) leaves x & 1 in bit 31 of x' (P has it).
+__device__ __forceinline__ uint32_t unstep_byte(uint32_t x) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t b = x >> 31;
+    x = ((x ^ (0x82F63B78u & (0u - b))) << 1) | b;
+  }
+  return x;
+}
+__device__ __forceinline__ int32_t clamp16(int32_t x) { return x < 0 ? 0 : (x > 16 ? 16 : x); }
 
 // Fold the 4G pending stream words of a lane group (4 per lane, lane q holds
 // the words at byte offsets 16q+0,4,8,12 of each 16G-byte swath) into the
@@ -1064,6 +1099,8 @@ struct FlatSet {
   uint64_t u0, u1, rec;  // the block's CRC input range and its index
   uint32_t ninit, st;    // ~init (0 in RAW mode); stored CRC (log verify)
   bool valid, last;
+  bool head;             // rounds kernel: the step holds a byte of [u0, u0+4) (group-uniform)
+  bool l3;               // rounds kernel: the lane's last-swath piece is in the region
 };
 
 constexpr uint64_t kNoChunk = ~0ull;
@@ -1531,7 +1568,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
   A.d0 = A.d1 = A.d2 = A.d3 = A.t = A.t2 = make_uint4(0, 0, 0, 0);
   A.pa = A.u0 = A.u1 = A.rec = 0;
   A.ninit = A.st = 0;
-  A.valid = A.last = false;
+  A.valid = A.last = A.head = A.l3 = false;
   for (;;) {
     take(true);
     issue(B);
@@ -1679,8 +1716,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     }
   }
 #endif
-  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, p.tab_byte, 64);
+  // byte table (1 KiB) + 17 x 16-B prefix masks (LM[n] = bytes [0, n)), one image
+  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, p.tab_byte, 64 + 17);
   __syncthreads();
+  constexpr uint32_t kLM = kByteTab + 1024u;
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1693,6 +1732,9 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   const uint64_t zl = (uint64_t)p.zline;
   const uint64_t base = (uint64_t)p.base;
   const uint32_t C = p.chunk;  // sorted positions per chunk: R rounds of kGroups, <= 64
+  // per-block init values (store mode with an init array): the general head
+  // masking, in its own instantiation (the common path keeps fewer registers)
+  constexpr bool any_init = MODE == kStore && (VAR & kVarInit) != 0;
   const uint32_t R = C / kGroups;
   const uint32_t nwg = gridDim.x;
   const uint32_t nwaves = blockDim.x >> 6;
@@ -1741,7 +1783,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   // Sort the loaded chunk's slots by step count, largest first (rank by
   // shuffles, inverse permutation through the wave's LDS scratch), so each
   // round's blocks have similar lengths while the chunk keeps its locality.
-  uint32_t* const sortbuf = reinterpret_cast<uint32_t*>(lds + kByteTab + 1024u) + wave * 64;
+  uint32_t* const sortbuf = reinterpret_cast<uint32_t*>(lds + kByteTab + 1024u + 272u) + wave * 64;
   auto sort_nxt = [&]() {
     n_ok = t_ok;
     if (!p.sort_local) return;
@@ -1845,6 +1887,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   uint32_t r_idx = R, r_step = 0, r_S = 0;
   constexpr uint64_t kLine = 16 * G;  // one swath of a lane group
   uint64_t g_le = 0;                  // the group's region end on the line grid
+  uint32_t g_w0 = 0, g_hs = 0, g_hs2 = 0;  // first region swath of this lane; head steps
+  bool g_l3 = false, g_nz = false, g_hneed = false;
   // Take the next non-empty round (switching chunks as needed).  Returns with
   // r_S == 0 if the switch must wait for nxt (stall) or the work is done.
   auto next_round = [&]() {
@@ -1898,6 +1942,21 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     }
     g_lp = g_le - (uint64_t)r_S * kStep;
     r_step = 0;
+    // Per-lane 32-bit thresholds for the round's steps (issue/fold run no 64-bit
+    // compares): lane q's piece of swath w (w = 4 * step + k) is at
+    // g_lp + 16q + 16G*w; it is a region piece iff w >= g_w0 (at or after the
+    // line holding A0 = u0 & ~15) and, for the last swath, below E.  The
+    // head steps hold the bytes [u0, u0+4) that need masking / ~init.
+    {
+      const int64_t a0d = (int64_t)((g_u0 & ~15ull) - g_lp) - 16 * q;
+      g_w0 = a0d <= 0 ? 0u : (uint32_t)((uint64_t)(a0d + (int64_t)kLine - 1) / kLine);
+      g_l3 = g_lp + 16 * q + kLine * (4ull * r_S - 1) < g_end;
+      const uint64_t u0rel = g_u0 - g_lp;
+      g_hs = (uint32_t)(u0rel / kStep);
+      g_hs2 = (uint32_t)((u0rel + 3) / kStep);
+      g_nz = g_valid && g_u1 > g_u0;
+      g_hneed = g_nz && ((g_u0 & 15) != 0 || g_ninit != 0);
+    }
   };
 
   // Values loaded in one take and used only later are consumed at fixed points
@@ -1942,7 +2001,25 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     const bool run = r_S != 0;             // a round is active (else: stalled, empty step)
     const bool v = g_valid && run;
     const bool last = run && r_step + 1 == r_S;  // wave-uniform
-    load_step<G, VAR, kTail2, true>(X, g_lp, g_u0, g_u1, g_end, v, v && last, zl, q);
+    {
+      const bool vz = g_nz && run;
+      const uint32_t w = 4 * r_step;
+      const uint64_t pa = g_lp + 16 * q;
+      X.d0 = gload16<VAR>((vz && w >= g_w0) ? pa : zl);
+      X.d1 = gload16<VAR>((vz && w + 1 >= g_w0) ? pa + 16 * G : zl);
+      X.d2 = gload16<VAR>((vz && w + 2 >= g_w0) ? pa + 32 * G : zl);
+      X.d3 = gload16<VAR>((vz && w + 3 >= g_w0 && (!last || g_l3)) ? pa + 48 * G : zl);
+      const bool vl = v && last;
+      if constexpr (kTail2) {
+        const uint64_t ta = vl ? g_end : zl;  // holds the stored CRC's first byte
+        X.t = gload16<VAR>(ta);
+        X.t2 = gload16<VAR>((vl && g_u1 + 4 > g_end + 16) ? g_end + 16 : ta);
+      } else {
+        X.t = gload16<VAR>((vl && vz && (g_u1 & 15)) ? g_end : zl);
+      }
+      X.head = vz && g_hneed && (r_step == g_hs || r_step == g_hs2);
+      X.l3 = g_l3;  // (fold runs after the next round may have started)
+    }
     X.pa = g_lp;
     X.u0 = g_u0;
     X.u1 = g_u1;
@@ -1965,7 +2042,54 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   uint64_t wb_a = 0;
   uint32_t wb_v = 0;
   auto fold = [&](FlatSet& Y) {
-    fold_step<G, VAR, kTail2, true>(lds, Y, q, c0, c1, c2, c3, lo0, lo1, lo2, lo3);
+    uint4 d0 = Y.d0, d1 = Y.d1, d2 = Y.d2, d3 = Y.d3;
+    if (__builtin_amdgcn_ballot_w64(Y.head)) {  // wave-uniform: some group's head step
+      // h = u0 - (lane's piece of swath 0 of the step); pieces wholly before u0
+      // came from the zero line, so only [u0, u0+4) and the bytes before u0 in
+      // u0's piece need work.  Non-head groups keep their data (h <= -16).
+      const int32_t h = Y.head ? (int32_t)(Y.u0 - Y.pa) - 16 * q : -64;
+      if constexpr (any_init) {  // per-block init values: byte-exact head_piece
+        d0 = head_piece(d0, h, Y.ninit);
+        d1 = head_piece(d1, h - 16 * G, Y.ninit);
+        d2 = head_piece(d2, h - 32 * G, Y.ninit);
+        d3 = head_piece(d3, h - 48 * G, Y.ninit);
+      } else {  // ~init is ~0 (Value) or 0 (RAW, n < 4): ((d ^ LM[lo4]) & ~LM[lo])
+        const int32_t i4 = Y.ninit ? 4 : 0;
+        auto mask = [&](uint4& d, int32_t hk) {
+          const uint4 B = lds_u128(kLM + 16u * (uint32_t)clamp16(hk));
+          const uint4 I = lds_u128(kLM + 16u * (uint32_t)clamp16(hk + i4));
+          d.x = (d.x ^ I.x) & ~B.x;
+          d.y = (d.y ^ I.y) & ~B.y;
+          d.z = (d.z ^ I.z) & ~B.z;
+          d.w = (d.w ^ I.w) & ~B.w;
+        };
+        mask(d0, h);
+        mask(d1, h - 16 * G);
+        mask(d2, h - 32 * G);
+        mask(d3, h - 48 * G);
+      }
+    }
+    if (Y.last) {  // wave-uniform: the region's last line may end past E
+      swath4<VAR>(lds, c0, c1, c2, c3, d0, lo0, lo1, lo2, lo3);
+      swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);
+      swath4<VAR>(lds, c0, c1, c2, c3, d2, lo0, lo1, lo2, lo3);
+      const uint32_t k0 = c0, k1 = c1, k2 = c2, k3 = c3;
+      swath4<VAR>(lds, c0, c1, c2, c3, d3, lo0, lo1, lo2, lo3);
+      if (!Y.l3) {  // piece at or after E: not in the region
+        c0 = k0;
+        c1 = k1;
+        c2 = k2;
+        c3 = k3;
+      }
+    } else if constexpr ((VAR & kVarNarrow) != 0) {
+      fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+    } else {
+      fold4w<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+    }
+    // the tail line(s) are used only on a block's last step: consume anyway, so
+    // the compiler resolves their loads here with an exact count
+    asm volatile("" ::"v"(Y.t.x), "v"(Y.t.y), "v"(Y.t.z), "v"(Y.t.w));
+    if constexpr (kTail2) asm volatile("" ::"v"(Y.t2.x), "v"(Y.t2.y), "v"(Y.t2.z), "v"(Y.t2.w));
     if (Y.last) {  // wave-uniform: every group ends its block on this step
       // On the line grid lane q's pieces sit at position (q - e) mod G of the
       // 16G-byte swaths that end at E (e = (E mod 16G) / 16); group_fold wants
@@ -2017,7 +2141,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   A.d0 = A.d1 = A.d2 = A.d3 = A.t = A.t2 = make_uint4(0, 0, 0, 0);
   A.pa = A.u0 = A.u1 = A.rec = 0;
   A.ninit = A.st = 0;
-  A.valid = A.last = false;
+  A.valid = A.last = A.head = A.l3 = false;
   for (;;) {
     take(true);
     issue(B);
@@ -2445,36 +2569,6 @@ constexpr int kLsWin = 8;                    // decoded descriptors per lane (64
 constexpr uint32_t kLsMinN = 128;            // CRC bytes of a streamed record (>= one swath)
 constexpr int32_t kLsFar = 1 << 28;          // "no record": past every swath
 
-__device__ __forceinline__ uint32_t lds_apply(uint32_t tab, uint32_t x) {
-  const uint32_t t0 = lds_u32(nullptr, tab + ((x & 255u) << 2));
-  const uint32_t t1 = lds_u32(nullptr, tab + 1024u + (((x >> 8) & 255u) << 2));
-  const uint32_t t2 = lds_u32(nullptr, tab + 2048u + (((x >> 16) & 255u) << 2));
-  const uint32_t t3 = lds_u32(nullptr, tab + 3072u + ((x >> 24) << 2));
-  return xor3(t0, t1, t2) ^ t3;
-}
-__device__ __forceinline__ uint4 lds_u128(uint32_t a) {
-  const u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const u32x4*>(a);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void lds_st128(uint32_t a, uint4 v) {
-  u32x4 w;
-  w.x = v.x;
-  w.y = v.y;
-  w.z = v.z;
-  w.w = v.w;
-  *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(a) = w;
-}
-// Inverse of one zero-byte step of the reflected register (M_1^-1): the forward
-// bit step x' = (x >> 1) ^ (P if x & 1) leaves x & 1 in bit 31 of x' (P has it).
-__device__ __forceinline__ uint32_t unstep_byte(uint32_t x) {
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t b = x >> 31;
-    x = ((x ^ (0x82F63B78u & (0u - b))) << 1) | b;
-  }
-  return x;
-}
-__device__ __forceinline__ int32_t clamp16(int32_t x) { return x < 0 ? 0 : (x > 16 ? 16 : x); }
 
 typedef __attribute__((address_space(1))) const u32_unaligned gcu32u;
 
@@ -2903,6 +2997,7 @@ struct DevTables {
   uint32_t* sh16 = nullptr;
   uint32_t* zero_word = nullptr;  // 16 zero bytes: the NULL-init stand-in
   uint32_t* byte8 = nullptr;      // M_1 byte table (flat kernel tail steps)
+  uint32_t* byte8lm = nullptr;    // the same + 17 x 16-B prefix masks (rounds kernel head steps)
   uint32_t* op1024 = nullptr;     // M_1024 byte tables (burst kernel stream step)
   uint32_t* op1024r = nullptr;    // the same, 16-way bank-replicated
   uint32_t* ls_tabs = nullptr;    // log-stream kernel LDS tail: M4, M16 byte tables, 17 prefix masks
@@ -3102,6 +3197,14 @@ void init_device(int dev, DevTables* t) {
     std::vector<uint32_t> b8(256);
     for (uint32_t b = 0; b < 256; b++) b8[b] = m1(b);
     if ((t->err = upload(&t->byte8, b8))) return;
+    for (uint32_t nbytes = 0; nbytes <= 16; nbytes++)  // LM[n]: bytes [0, n) set
+      for (uint32_t w = 0; w < 4; w++) {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 4; b++)
+          if (4 * w + b < nbytes) v |= 0xffu << (8 * b);
+        b8.push_back(v);
+      }
+    if ((t->err = upload(&t->byte8lm, b8))) return;
   }
   {
     std::vector<uint32_t> op;
@@ -3140,6 +3243,7 @@ void init_device(int dev, DevTables* t) {
   }
 #endif
   if ((t->err = set_lds_attrs_rounds<kStore>())) return;
+  if ((t->err = set_lds_attrs_rounds<kStore, kVarInit>())) return;
   if ((t->err = set_lds_attrs_rounds<kTrailer>())) return;
   if ((t->err = set_lds_attrs_rounds<kVerify>())) return;
   if ((t->err = set_lds_attrs_rounds<kLogWrite>())) return;
@@ -3543,7 +3647,7 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_
   if (G < 2) G = 2;
   p.tab_main = t->main[gindex(G)];
   p.tab_tree = t->tree;
-  p.tab_byte = t->byte8;
+  p.tab_byte = t->byte8lm;
   p.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
   p.omask = p.lmask = p.imask = ~0ull;
   if (p.offsets) {
@@ -3604,13 +3708,15 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_
   p.sched = sched_slot(t, stream);
   if (!p.sched) return NOVA_E_NOMEM;
   const dim3 block(64 * nwaves);
-  const size_t lds = flat_lds_g(G) + nwaves * 64 * 4;  // + per-wave sort scratch
+  const size_t lds = flat_lds_g(G) + 272 + nwaves * 64 * 4;  // + prefix masks, per-wave sort scratch
 #ifdef NOVA_DIAG
   if (MODE == kStore && g_tune_var.load() == kVarNoLookup)
     return launch_rounds_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
   if (MODE == kStore && g_tune_var.load() == kVarNarrow)
     return launch_rounds_g<kStore, kVarNarrow>(G, dim3(wgs), block, lds, stream, p);
 #endif
+  if (MODE == kStore && p.imask != 0)
+    return launch_rounds_g<kStore, kVarInit>(G, dim3(wgs), block, lds, stream, p);
   return launch_rounds_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
 }
 
