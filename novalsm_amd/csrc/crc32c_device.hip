@@ -104,6 +104,11 @@ struct CrcParams {
   uint32_t* ls_bad;          // log-stream mismatch count (added to n_bad unless it falls back)
   uint32_t* ls_left;         // records the log-stream kernel leaves to the rounds follow-up
   const uint32_t* gate;      // rounds kernel: run only if *gate != 0 (else fold ls_bad in)
+  // trailer writer (rounds kernel): *tr_flag == 0 (trailer_layout_kernel found
+  // the blocks ascending, disjoint and >= 32 B) lets each block but the last
+  // rewrite the whole 32-B sectors holding its trailer; null
+  // or nonzero: byte stores
+  const uint32_t* tr_flag;
 };
 
 // ---- log records: bounds and status (db/log_reader.cc:228-262) ------------
@@ -366,6 +371,21 @@ __device__ __forceinline__ void store_u32_unaligned(uint8_t* d, uint32_t v) {
 __device__ __forceinline__ void store_trailer(uint8_t* d, uint32_t type, uint32_t m, bool quirk) {
   *(__attribute__((address_space(1))) uint8_t*)d = (uint8_t)type;
   store_u32_unaligned(d + 1, quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m);
+}
+
+// Patch the trailer bytes [u1, u1+5) (tv: type | LE32 << 8) into the 16-B
+// piece at address pa (the bytes of the piece outside the trailer keep d).
+__device__ __forceinline__ uint4 patch_trailer(uint4 d, uint64_t pa, uint64_t u1, uint64_t tv) {
+  const int32_t o = (int32_t)(int64_t)(u1 - pa);  // trailer start relative to the piece
+  auto dw = [&](uint32_t w, int32_t j) -> uint32_t {
+    const int32_t r = 4 * j - o;  // byte of the trailer at the dword's first byte
+    if (r >= 5 || r <= -4) return w;
+    const uint64_t m40 = 0xffffffffffull;
+    const uint64_t bits = r >= 0 ? tv >> (8 * r) : tv << (-8 * r);
+    const uint64_t msk = r >= 0 ? m40 >> (8 * r) : m40 << (-8 * r);
+    return (w & ~(uint32_t)msk) | ((uint32_t)bits & (uint32_t)msk);
+  };
+  return make_uint4(dw(d.x, 0), dw(d.y, 1), dw(d.z, 2), dw(d.w, 3));
 }
 
 // LDS helpers for tables at absolute LDS addresses (the dynamic region starts
@@ -1101,6 +1121,7 @@ struct FlatSet {
   bool valid, last;
   bool head;             // rounds kernel: the step holds a byte of [u0, u0+4) (group-uniform)
   bool l3;               // rounds kernel: the lane's last-swath piece is in the region
+  bool wsec;             // rounds kernel, trailer writer: t2 holds this lane's sector piece
 };
 
 constexpr uint64_t kNoChunk = ~0ull;
@@ -1568,7 +1589,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
   A.d0 = A.d1 = A.d2 = A.d3 = A.t = A.t2 = make_uint4(0, 0, 0, 0);
   A.pa = A.u0 = A.u1 = A.rec = 0;
   A.ninit = A.st = 0;
-  A.valid = A.last = A.head = A.l3 = false;
+  A.valid = A.last = A.head = A.l3 = A.wsec = false;
   for (;;) {
     take(true);
     issue(B);
@@ -1738,6 +1759,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   const uint32_t R = C / kGroups;
   const uint32_t nwg = gridDim.x;
   const uint32_t nwaves = blockDim.x >> 6;
+  // trailer writer: whole-sector trailer stores allowed (trailer_layout_kernel)
+  const bool sect = MODE == kTrailer && G >= 4 && p.tr_flag && *p.tr_flag == 0;
 
   // ---- chunk claims (as the flat kernel) ---------------------------------------
   uint32_t victim = blockIdx.x, tried = 0, req = 0;
@@ -2015,7 +2038,19 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         X.t = gload16<VAR>(ta);
         X.t2 = gload16<VAR>((vl && g_u1 + 4 > g_end + 16) ? g_end + 16 : ta);
       } else {
-        X.t = gload16<VAR>((vl && vz && (g_u1 & 15)) ? g_end : zl);
+        uint64_t ta = (vl && vz && (g_u1 & 15)) ? g_end : zl;
+        if constexpr (MODE == kTrailer) {
+          // whole-sector trailer stores: the 32-B sector(s) holding the trailer
+          // [u1, u1+5) are pieces s0 + 16k, k < 2 (4 when the trailer crosses a
+          // sector); lane q < np loads piece q instead of the tail line, which
+          // is piece (E - s0) / 16 -- fold shuffles it to the group
+          const uint64_t s0 = g_u1 & ~31ull;
+          const uint32_t np = ((g_u1 + 4) & ~31ull) != s0 ? 4u : 2u;
+          const bool w = vl && sect && g_rec + 1 < p.n_blocks && (uint32_t)q < np;
+          if (w) ta = s0 + 16 * q;
+          X.wsec = w;
+        }
+        X.t = gload16<VAR>(ta);
       }
       X.head = vz && g_hneed && (r_step == g_hs || r_step == g_hs2);
       X.l3 = g_l3;  // (fold runs after the next round may have started)
@@ -2038,9 +2073,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   };
 
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-  bool wb_on = false;
+  bool wb_on = false, wb_sec = false;
   uint64_t wb_a = 0;
   uint32_t wb_v = 0;
+  uint4 wb_w = make_uint4(0, 0, 0, 0);  // trailer writer: the patched sector piece
   auto fold = [&](FlatSet& Y) {
     uint4 d0 = Y.d0, d1 = Y.d1, d2 = Y.d2, d3 = Y.d3;
     if (__builtin_amdgcn_ballot_w64(Y.head)) {  // wave-uniform: some group's head step
@@ -2102,13 +2138,48 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       c3 = __shfl(c3, src);
       const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
       c0 = c1 = c2 = c3 = 0;
+      bool elig = false;
+      uint4 piece = Y.t;
+      if constexpr (MODE == kTrailer) {
+        // whole-sector form (group-uniform eligibility): the tail line is the
+        // group's sector piece (E - s0) / 16; every lane takes it from there
+        elig = sect && Y.valid && Y.rec + 1 < p.n_blocks;
+        const uint32_t k = (uint32_t)((Y.u1 >> 4) & 1u);  // (E - s0) / 16
+        const int src = elig ? grp * G + (int)k : lane;
+        Y.t.x = __shfl(piece.x, src);
+        Y.t.y = __shfl(piece.y, src);
+        Y.t.z = __shfl(piece.z, src);
+        Y.t.w = __shfl(piece.w, src);
+      }
       finish_block<MODE>(lds, kByteTab, p, raw, v, Y, wb_a, wb_v);
       wb_on = q == 0 && Y.valid;  // written after the next step's loads are issued
+      if constexpr (MODE == kTrailer) {
+        // lanes holding a sector piece store it patched with the trailer;
+        // lane 0's byte stores are not used
+        wb_sec = elig;
+        if (elig) {
+          wb_on = Y.wsec;
+          const bool quirk = (p.flags & NOVA_TRAILER_TB_QUIRK) != 0;
+          const uint32_t m = quirk ? ((wb_v & 0x00ffffffu) | ((uint32_t)'!' << 24)) : wb_v;
+          const uint64_t tv = (uint64_t)((p.flags >> 8) & 0xffu) | ((uint64_t)m << 8);
+          wb_a = (Y.u1 & ~31ull) + 16u * (uint32_t)q;
+          wb_w = patch_trailer(piece, wb_a, Y.u1, tv);
+        }
+      }
     }
   };
   auto writeback = [&]() {
     if (wb_on) {
-      write_result<MODE>(p, wb_a, wb_v);
+      if (MODE == kTrailer && wb_sec) {
+        u32x4 w;
+        w.x = wb_w.x;
+        w.y = wb_w.y;
+        w.z = wb_w.z;
+        w.w = wb_w.w;
+        *(__attribute__((address_space(1))) u32x4*)wb_a = w;
+      } else {
+        write_result<MODE>(p, wb_a, wb_v);
+      }
       wb_on = false;
     }
   };
@@ -2141,7 +2212,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   A.d0 = A.d1 = A.d2 = A.d3 = A.t = A.t2 = make_uint4(0, 0, 0, 0);
   A.pa = A.u0 = A.u1 = A.rec = 0;
   A.ninit = A.st = 0;
-  A.valid = A.last = A.head = A.l3 = false;
+  A.valid = A.last = A.head = A.l3 = A.wsec = false;
   for (;;) {
     take(true);
     issue(B);
@@ -2498,6 +2569,31 @@ __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, co
 // byte for TableBuilder's ordering (table/table_builder.cc:202-206,
 // ltc/stoc_file_client_impl.cpp:713-719).  Inside the streaming kernel the
 // trailer stores per block cost ~12 points of HBM throughput.
+// Trailer writer pre-pass: may the rounds kernel rewrite whole 32-B sectors
+// around each trailer?  A block's trailer [u1, u1+5) lies in at most two
+// aligned 32-B sectors, all inside [u1-31, u1+36).  When every block is
+// >= 32 B and block i+1 starts at or after block i's trailer end, that window
+// starts inside block i and ends before block i+1's trailer (>= u1+37), so
+// no two blocks' windows share a sector and every byte a block rewrites that
+// is not its trailer is image data nobody writes (it is stored back
+// unchanged).  The last block's window may run past the image: it keeps byte
+// stores.  Any violation sets *flag (then every block uses byte stores).
+__global__ void __launch_bounds__(256) trailer_layout_kernel(const uint64_t* offsets, uint64_t omask,
+                                                             const uint32_t* lengths, uint64_t lmask,
+                                                             uint64_t stride, uint32_t len, uint64_t n,
+                                                             uint32_t* flag) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
+    const uint64_t u0 = offsets[i & omask] + i * stride;
+    const uint64_t m = (uint64_t)lengths[i & lmask] + len;
+    bool b = m < 32;
+    if (i + 1 < n) b = b || offsets[(i + 1) & omask] + (i + 1) * stride < u0 + m + 5;
+    bad = bad || b;
+  }
+  if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
 __global__ void __launch_bounds__(256) trailer_scatter_kernel(uint8_t* base, const uint64_t* offsets,
                                                               const uint32_t* sizes,
                                                               const uint32_t* crc, uint64_t n,
@@ -3629,7 +3725,7 @@ int launch_sort(CrcParams& p, DevTables* t, hipStream_t stream, uint64_t kStep, 
 #endif
 
 thread_local std::atomic<int> g_tune_sort{2};  // rounds kernel: 0 in order, 1 whole-batch sort, 2 per chunk
-thread_local std::atomic<int> g_tune_trailer_1pass{0};  // trailer writer: 1 = single pass in the rounds kernel
+thread_local std::atomic<int> g_tune_trailer_1pass{0};  // trailer writer (large batches): 0 = one pass, whole-sector stores when the layout allows; 1 = one pass, byte stores; 2 = two passes (CRC array + scatter)
 
 template <int MODE, int VAR>
 int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
@@ -3914,7 +4010,30 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // write their trailers from the CRC kernel: a second launch would add its
   // whole fixed cost to the call.
   const bool small = p.n_blocks <= 2ull * t->cus * flat_waves();
-  if (pl.kernel == kRoundsK && mode == kTrailer && !g_tune_trailer_1pass.load() && !small) {
+  if (pl.kernel == kRoundsK && mode == kTrailer && g_tune_trailer_1pass.load() == 0 && !small) {
+    // One pass with whole-sector trailer stores when the layout allows it
+    // (trailer_layout_kernel): a partial sector write costs an
+    // HBM read-modify-write per trailer, a whole one does not.
+    StreamScratch sc;  // the layout flag, freed in stream order after the CRC kernel
+    if (sc.alloc(sizeof(uint32_t), stream)) return NOVA_E_NOMEM;
+    uint32_t* flag = static_cast<uint32_t*>(sc.p);
+    hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return (int)e;
+    uint64_t wgs = (p.n_blocks + 255) / 256;
+    const uint64_t cap = (uint64_t)t->cus * 8;
+    if (wgs > cap) wgs = cap;
+    // descriptors as launch_rounds normalises them (absent arrays: stride / len)
+    const uint64_t* lo = p.offsets ? p.offsets : reinterpret_cast<const uint64_t*>(t->zero_word);
+    const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
+    hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, lo,
+                       p.offsets ? ~0ull : 0ull, ll, p.lengths ? ~0ull : 0ull,
+                       p.offsets ? 0ull : p.stride, p.lengths ? 0u : p.len, p.n_blocks, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    CrcParams q = p;
+    q.tr_flag = flag;
+    return launch_rounds<kTrailer>(G, q, t, stream, pl.chunk);
+  }
+  if (pl.kernel == kRoundsK && mode == kTrailer && g_tune_trailer_1pass.load() == 2 && !small) {
     // Two passes: CRCs (type byte appended, masked) into this call's own
     // stream-ordered array, then the trailer bytes (trailer_scatter_kernel).
     StreamScratch sc;  // freed in stream order after the scatter

@@ -343,8 +343,9 @@ def test_no_device_memory_growth(torch_gpu, oracle):
 
 def test_shared_stream_trailer_threads(torch_gpu, oracle):
     """several host threads writing trailers of large batches (the
-    two-pass path, > 6144 blocks) on the SAME stream (the default one) each get
-    their own CRC scratch: every trailer matches the oracle."""
+    rounds kernel, > 6144 blocks; blocks of 1..599 B, so the byte-store form) on
+    the SAME stream (the default one) each get their own layout-flag scratch:
+    every trailer matches the oracle."""
     torch = torch_gpu
     import threading
     n = 9000
@@ -381,6 +382,47 @@ def test_shared_stream_trailer_threads(torch_gpu, oracle):
         for i in range(0, n, 7):
             o, ln = int(offs[i]), int(lens[i])
             assert oracle.trailer(host[o:o + ln].tobytes(), 0, True) == got[o + ln:o + ln + 5].tobytes()
+
+
+@pytest.mark.parametrize("layout", ["packed", "gaps", "tiny", "permuted", "aligned"])
+@pytest.mark.parametrize("quirk,ctype", [(True, 0), (False, 1)])
+def test_trailer_sector_stores(torch_gpu, oracle, layout, quirk, ctype):
+    """Large trailer batches (the rounds kernel, > 6144 blocks) rewrite the whole
+    32-B sectors around each trailer when trailer_layout_kernel finds the blocks
+    ascending, disjoint and >= 32 B ("packed", "gaps", "aligned"); otherwise
+    ("tiny": some blocks < 32 B, "permuted": descriptors out of address order)
+    every trailer is written with byte stores.  Either way the WHOLE image must
+    equal the input with each block's trailer (table/table_builder.cc:202-206,
+    ltc/stoc_file_client_impl.cpp:713-719) in place: no byte outside the
+    trailers changes, including gap bytes and the bytes after the last block."""
+    torch = torch_gpu
+    n = 9000
+    rng = np.random.default_rng(["packed", "gaps", "tiny", "permuted", "aligned"].index(layout) * 2 + quirk)
+    lens = rng.integers(32, 3000, n).astype(np.uint32)
+    if layout == "tiny":
+        lens[rng.choice(n, 40, replace=False)] = rng.integers(0, 32, 40).astype(np.uint32)
+    if layout == "aligned":
+        lens = (lens + 31) & ~np.uint32(31)  # every trailer at a sector start
+    gaps = rng.integers(0, 40, n).astype(np.uint64) if layout == "gaps" else np.zeros(n, np.uint64)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5) + gaps[:-1])
+    total = int(offs[-1]) + int(lens[-1]) + 5 + 64
+    host = splitmix64_bytes(77, total)  # trailer bytes start as noise
+    want = host.copy()
+    for i in range(n):
+        o, ln = int(offs[i]), int(lens[i])
+        want[o + ln:o + ln + 5] = np.frombuffer(oracle.trailer(host[o:o + ln].tobytes(), ctype, quirk),
+                                                dtype=np.uint8)
+    order = rng.permutation(n) if layout == "permuted" else np.arange(n)
+    buf = dev(torch, host)
+    C.write_trailers(buf, dev(torch, offs[order], torch.int64), dev(torch, lens[order], torch.int32),
+                     ctype, quirk)
+    got = buf.cpu().numpy()
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:10], got[bad[:10]], want[bad[:10]])
+    if not quirk:  # StoC order: every block verifies
+        ok, nbad = C.verify_blocks(buf, dev(torch, offs, torch.int64), dev(torch, lens, torch.int32))
+        assert ok.cpu().numpy().all() and int(nbad.item()) == 0
 
 
 @pytest.mark.parametrize("pinned", [True, False])

@@ -137,12 +137,16 @@ def main() -> int:
                 blk = buf[o:o + ln + 5].cpu().numpy().tobytes()
                 ok &= orc.trailer(blk[:ln], 0, True) == blk[ln:]
             emit("trailers", wl, sum_len + 5 * n, sec, ok, {"image": image})
-            with C.diagnostics() as D:  # A/B: trailer bytes stored by the CRC kernel
-                D.nova_diag_set_trailer_single_pass(1)
-                sec1 = timed(torch, tw, args.steps, args.warmup, stream)
-            gbs1 = (sum_len + 5 * n) / sec1 / 1e9
-            print(json.dumps({"sweep": "trailers_single_pass", "image": image, "GBps": round(gbs1, 1),
-                              "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
+            # A/B: 1 = one pass with byte stores, 2 = two passes (CRC array +
+            # scatter); the default is one pass with whole-sector stores
+            for var, name in ((1, "trailers_single_pass_bytes"), (2, "trailers_two_pass")):
+                with C.diagnostics() as D:
+                    D.nova_diag_set_trailer_single_pass(var)
+                    sec1 = timed(torch, tw, args.steps, args.warmup, stream)
+                    D.nova_diag_set_trailer_single_pass(0)
+                gbs1 = (sum_len + 5 * n) / sec1 / 1e9
+                print(json.dumps({"sweep": name, "image": image, "GBps": round(gbs1, 1),
+                                  "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
             sweep("trailers", tw, sum_len + 5 * n)
         if "verify" in ops:
             C.write_trailers(buf, offs, lens, 0, False, stream=stream)  # StoC order: verifiable

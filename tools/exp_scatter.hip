@@ -42,6 +42,15 @@ __global__ void __launch_bounds__(256) scatter(uint8_t* base, const uint64_t* of
     __builtin_memcpy((void*)(t + 1), &m, 4);
   } else if constexpr (V == 4) {
     for (int k = 0; k < 5; k++) ((uint8_t*)t)[k] = tr[k];
+  } else if constexpr (V >= 10) {
+    // write-only: whole aligned pieces of W bytes holding the trailer, no read
+    // (garbage values: measures the store shape's HBM cost only)
+    constexpr uint64_t W = V == 10 ? 16 : V == 11 ? 32 : 64;
+    const uint64_t a0 = t & ~(W - 1), a1 = (t + 4) & ~(W - 1);
+    const u32x4 v = {m, m, m, m};
+    for (uint64_t a = a0; a <= a1; a += W)
+#pragma unroll
+      for (int k = 0; k < (int)(W / 16); k++) *(u32x4*)(a + 16 * k) = v;
   } else {
     constexpr uint64_t P = V == 1 ? 32 : V == 2 ? 64 : 128;
     const uint64_t a0 = t & ~(P - 1), a1 = (t + 4) & ~(P - 1);
@@ -132,6 +141,23 @@ int main() {
     readall<<<2048, 256>>>(d, n16, sink);
     scatter<3><<<g, 256>>>(d, doff, dsz, dcrc, n);
   });
+  run("read+write16_noread", [&] {
+    readall<<<2048, 256>>>(d, n16, sink);
+    scatter<10><<<g, 256>>>(d, doff, dsz, dcrc, n);
+  });
+  run("read+write32_noread", [&] {
+    readall<<<2048, 256>>>(d, n16, sink);
+    scatter<11><<<g, 256>>>(d, doff, dsz, dcrc, n);
+  });
+  run("read+write64_noread", [&] {
+    readall<<<2048, 256>>>(d, n16, sink);
+    scatter<12><<<g, 256>>>(d, doff, dsz, dcrc, n);
+  });
+  run("read+scatter_5bytes", [&] {
+    readall<<<2048, 256>>>(d, n16, sink);
+    scatter<4><<<g, 256>>>(d, doff, dsz, dcrc, n);
+  });
+  run("read_image_nt_again", [&] { readall<<<2048, 256>>>(d, n16, sink); });
   CK(hipDeviceSynchronize());
   return 0;
 }

@@ -67,6 +67,15 @@ def make_workload(wl: str, stream):
         total = int(offs[-1]) + int(lens[-1]) + 128
     elif wl == "log":
         offs, lens, types, total = log_layout(4 << 30, 6)
+    elif wl.startswith("log_"):  # log_uN: payload U[1,N]; log_fN: every payload N (4 GiB)
+        from novalsm_amd.synth import log_layout as writer_layout
+        k, v = wl[4], int(wl[5:])
+        n = (4 << 30) // (7 + (v // 2 if k == "u" else v))
+        r = splitmix64_words(6, 0, n)
+        plens = (r % np.uint64(v) + np.uint64(1)).astype(np.int64) if k == "u" else np.full(n, v, np.int64)
+        offs, lens, types, _, total = writer_layout(plens)
+        lens = lens.astype(np.uint64)
+        wl = "log"
     else:
         raise SystemExit(wl)
     buf = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
