@@ -105,9 +105,9 @@ struct CrcParams {
   uint32_t* ls_left;         // records the log-stream kernel leaves to the rounds follow-up
   const uint32_t* gate;      // rounds kernel: run only if *gate != 0 (else fold ls_bad in)
   // trailer writer (rounds kernel): *tr_flag == 0 (trailer_layout_kernel found
-  // the blocks ascending, disjoint and >= 32 B) lets each block but the last
-  // rewrite the whole 32-B sectors holding its trailer; null
-  // or nonzero: byte stores
+  // the blocks ascending and disjoint) lets each block with init[i] != 0 (the
+  // pre-pass's eligibility array) rewrite the whole 64-B pieces holding its
+  // trailer; null or nonzero: byte stores
   const uint32_t* tr_flag;
 };
 
@@ -373,14 +373,16 @@ __device__ __forceinline__ void store_trailer(uint8_t* d, uint32_t type, uint32_
   store_u32_unaligned(d + 1, quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m);
 }
 
-// Patch the trailer bytes [u1, u1+5) (tv: type | LE32 << 8) into the 16-B
-// piece at address pa (the bytes of the piece outside the trailer keep d).
+// Patch the NB little-endian bytes of tv (a trailer: type | LE32 << 8, NB 5;
+// a log header's CRC field, NB 4) at address u1 into the 16-B line at address
+// pa (the line's other bytes keep d).
+template <int NB = 5>
 __device__ __forceinline__ uint4 patch_trailer(uint4 d, uint64_t pa, uint64_t u1, uint64_t tv) {
-  const int32_t o = (int32_t)(int64_t)(u1 - pa);  // trailer start relative to the piece
+  const int32_t o = (int32_t)(int64_t)(u1 - pa);  // field start relative to the line
   auto dw = [&](uint32_t w, int32_t j) -> uint32_t {
-    const int32_t r = 4 * j - o;  // byte of the trailer at the dword's first byte
-    if (r >= 5 || r <= -4) return w;
-    const uint64_t m40 = 0xffffffffffull;
+    const int32_t r = 4 * j - o;  // byte of the field at the dword's first byte
+    if (r >= NB || r <= -4) return w;
+    const uint64_t m40 = (1ull << (8 * NB)) - 1;
     const uint64_t bits = r >= 0 ? tv >> (8 * r) : tv << (-8 * r);
     const uint64_t msk = r >= 0 ? m40 >> (8 * r) : m40 << (-8 * r);
     return (w & ~(uint32_t)msk) | ((uint32_t)bits & (uint32_t)msk);
@@ -1495,7 +1497,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
       g_rec = rec;
       // ~init goes into the data's first 4 bytes; a block shorter than 4 bytes
       // gets it at the end instead (R ^= M_n(~init), see fold).
-      g_ninit = (raw || n < 4) ? 0u : ~(kLog ? 0u : aux);  // log records: Value(), init 0
+      g_ninit = (raw || n < 4) ? 0u : ~((kLog || MODE == kTrailer) ? 0u : aux);  // log records: Value(), init 0
       g_st = aux;
       const uint64_t E = g_u1 & ~15ull;
       const uint64_t A0 = a & ~15ull;
@@ -1759,8 +1761,12 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   const uint32_t R = C / kGroups;
   const uint32_t nwg = gridDim.x;
   const uint32_t nwaves = blockDim.x >> 6;
-  // trailer writer: whole-sector trailer stores allowed (trailer_layout_kernel)
-  const bool sect = MODE == kTrailer && G >= 4 && p.tr_flag && *p.tr_flag == 0;
+  // trailer writer: whole-piece trailer stores allowed (trailer_layout_kernel;
+  // a block's eligibility comes in as its init word)
+  // log write: the same for the 64-B piece holding each record's CRC field
+  // (log_window_kernel)
+  const bool sect = (MODE == kTrailer || MODE == kLogWrite) && G >= 8 && p.tr_flag &&
+                    *p.tr_flag == 0;
 
   // ---- chunk claims (as the flat kernel) ---------------------------------------
   uint32_t victim = blockIdx.x, tried = 0, req = 0;
@@ -1848,6 +1854,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       if constexpr (!kLog) {
         t_len = p.lengths[t_rec & p.lmask];
         t_aux = p.init[t_rec & p.imask];
+      } else if constexpr (MODE == kLogWrite) {
+        t_aux = p.init[t_rec & p.imask];  // whole-piece eligibility (log_window_kernel)
       }
       stage = 3;
     } else if (st == 3) {
@@ -1885,7 +1893,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
                               : log_cut_status(o, p.buf_len);
       n_n = ls == NOVA_LOG_OK ? 1u + length : 0u;  // 0: not read, n_aux = status
       n_rec = t_rec;
-      n_aux = ls == NOVA_LOG_OK ? (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)) : ls;
+      n_aux = ls == NOVA_LOG_OK ? (MODE == kLogWrite ? t_aux : (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)))
+                                : ls;
       n_chunk = t_chunk;
       sort_nxt();
       fl |= fReady;
@@ -1949,7 +1958,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       g_rec = rec;
       // ~init goes into the data's first 4 bytes; a block shorter than 4 bytes
       // gets it at the end instead (finish_block)
-      g_ninit = (raw || n < 4) ? 0u : ~(kLog ? 0u : aux);
+      g_ninit = (raw || n < 4) ? 0u : ~((kLog || MODE == kTrailer) ? 0u : aux);
       g_st = aux;
       g_end = g_u1 & ~15ull;
       // steps on the group's 16G-byte line grid: lines from the one holding
@@ -2040,14 +2049,22 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       } else {
         uint64_t ta = (vl && vz && (g_u1 & 15)) ? g_end : zl;
         if constexpr (MODE == kTrailer) {
-          // whole-sector trailer stores: the 32-B sector(s) holding the trailer
-          // [u1, u1+5) are pieces s0 + 16k, k < 2 (4 when the trailer crosses a
-          // sector); lane q < np loads piece q instead of the tail line, which
-          // is piece (E - s0) / 16 -- fold shuffles it to the group
-          const uint64_t s0 = g_u1 & ~31ull;
-          const uint32_t np = ((g_u1 + 4) & ~31ull) != s0 ? 4u : 2u;
-          const bool w = vl && sect && g_rec + 1 < p.n_blocks && (uint32_t)q < np;
+          // whole-piece trailer stores: the 64-B piece(s) holding the trailer
+          // [u1, u1+5) are 16-B lines s0 + 16k, k < 4 (8 when the trailer crosses
+          // a piece); lane q < np loads line q instead of the tail line, which
+          // is line (E - s0) / 16 -- fold shuffles it to the group
+          const uint64_t s0 = g_u1 & ~63ull;
+          const uint32_t np = ((g_u1 + 4) & ~63ull) != s0 ? 8u : 4u;
+          const bool w = vl && sect && g_st != 0 && (uint32_t)q < np;
           if (w) ta = s0 + 16 * q;
+          X.wsec = w;
+        }
+        if constexpr (MODE == kLogWrite) {
+          // whole-piece CRC-field stores: lanes q < 4 load the 64-B piece holding
+          // the header's CRC field [u0-6, u0-2); lanes 4.. load the tail line,
+          // which fold shuffles to the group (G >= 8)
+          const bool w = vl && vz && sect && g_st != 0 && (uint32_t)q < 4;
+          if (w) ta = ((g_u0 - 6) & ~63ull) + 16 * q;
           X.wsec = w;
         }
         X.t = gload16<VAR>(ta);
@@ -2140,11 +2157,19 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       c0 = c1 = c2 = c3 = 0;
       bool elig = false;
       uint4 piece = Y.t;
+      if constexpr (MODE == kLogWrite) {
+        elig = sect && Y.valid && Y.st != 0 && Y.u1 != Y.u0;  // (status-only records: Y.st = status)
+        const int src = elig ? grp * G + 4 : lane;
+        Y.t.x = __shfl(piece.x, src);
+        Y.t.y = __shfl(piece.y, src);
+        Y.t.z = __shfl(piece.z, src);
+        Y.t.w = __shfl(piece.w, src);
+      }
       if constexpr (MODE == kTrailer) {
-        // whole-sector form (group-uniform eligibility): the tail line is the
-        // group's sector piece (E - s0) / 16; every lane takes it from there
-        elig = sect && Y.valid && Y.rec + 1 < p.n_blocks;
-        const uint32_t k = (uint32_t)((Y.u1 >> 4) & 1u);  // (E - s0) / 16
+        // whole-piece form (group-uniform eligibility): the tail line is the
+        // group's window line (E - s0) / 16; every lane takes it from there
+        elig = sect && Y.valid && Y.st != 0;
+        const uint32_t k = (uint32_t)((Y.u1 >> 4) & 3u);  // (E - s0) / 16
         const int src = elig ? grp * G + (int)k : lane;
         Y.t.x = __shfl(piece.x, src);
         Y.t.y = __shfl(piece.y, src);
@@ -2162,15 +2187,23 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
           const bool quirk = (p.flags & NOVA_TRAILER_TB_QUIRK) != 0;
           const uint32_t m = quirk ? ((wb_v & 0x00ffffffu) | ((uint32_t)'!' << 24)) : wb_v;
           const uint64_t tv = (uint64_t)((p.flags >> 8) & 0xffu) | ((uint64_t)m << 8);
-          wb_a = (Y.u1 & ~31ull) + 16u * (uint32_t)q;
+          wb_a = (Y.u1 & ~63ull) + 16u * (uint32_t)q;
           wb_w = patch_trailer(piece, wb_a, Y.u1, tv);
+        }
+      }
+      if constexpr (MODE == kLogWrite) {
+        wb_sec = elig;
+        if (elig) {
+          wb_on = Y.wsec;
+          wb_a = ((Y.u0 - 6) & ~63ull) + 16u * (uint32_t)q;
+          wb_w = patch_trailer<4>(piece, wb_a, Y.u0 - 6, wb_v);
         }
       }
     }
   };
   auto writeback = [&]() {
     if (wb_on) {
-      if (MODE == kTrailer && wb_sec) {
+      if ((MODE == kTrailer || MODE == kLogWrite) && wb_sec) {
         u32x4 w;
         w.x = wb_w.x;
         w.y = wb_w.y;
@@ -2569,27 +2602,68 @@ __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, co
 // byte for TableBuilder's ordering (table/table_builder.cc:202-206,
 // ltc/stoc_file_client_impl.cpp:713-719).  Inside the streaming kernel the
 // trailer stores per block cost ~12 points of HBM throughput.
-// Trailer writer pre-pass: may the rounds kernel rewrite whole 32-B sectors
-// around each trailer?  A block's trailer [u1, u1+5) lies in at most two
-// aligned 32-B sectors, all inside [u1-31, u1+36).  When every block is
-// >= 32 B and block i+1 starts at or after block i's trailer end, that window
-// starts inside block i and ends before block i+1's trailer (>= u1+37), so
-// no two blocks' windows share a sector and every byte a block rewrites that
-// is not its trailer is image data nobody writes (it is stored back
-// unchanged).  The last block's window may run past the image: it keeps byte
-// stores.  Any violation sets *flag (then every block uses byte stores).
+// Trailer writer pre-pass.  HBM writes whole 64-B pieces; a store that
+// covers only part of one (a 5-B trailer) costs a read-modify-write at the
+// memory, so the rounds kernel rewrites the whole aligned
+// 64-B piece(s) holding a trailer -- its "window", one piece or two when the
+// trailer crosses a piece boundary -- patched with the trailer bytes.  The
+// window's other bytes are stored back unchanged, which is safe when no other
+// block's trailer lies in it: then nobody else writes those bytes (block data
+// is only read) and no two windows share a piece (every window piece holds a
+// byte of its own trailer).
+//   *flag |= 1 unless the blocks are ascending and disjoint, trailer
+//   included (offset[i+1] >= offset[i] + size[i] + 5): then only the
+//   neighbours' trailers can reach a window, and
+//   elig[i] = 1 iff block i's window holds neither neighbour's trailer, lies
+//   above the first block's start (i == 0) and is not the last block's (its
+//   window may run past the image).  Window bytes outside every block (gaps)
+//   lie between two blocks of the image, so inside the caller's allocation.
 __global__ void __launch_bounds__(256) trailer_layout_kernel(const uint64_t* offsets, uint64_t omask,
                                                              const uint32_t* lengths, uint64_t lmask,
                                                              uint64_t stride, uint32_t len, uint64_t n,
-                                                             uint32_t* flag) {
+                                                             uint32_t* elig, uint32_t* flag) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  auto u0_of = [&](uint64_t i) { return offsets[i & omask] + i * stride; };
+  auto u1_of = [&](uint64_t i) { return u0_of(i) + lengths[i & lmask] + len; };
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
+    const uint64_t u0 = u0_of(i), u1 = u1_of(i);
+    const uint64_t ws = u1 & ~63ull, we = ((u1 + 4) & ~63ull) + 64;
+    bool e = i + 1 < n;
+    if (i + 1 < n) {
+      bad = bad || u0_of(i + 1) < u1 + 5;
+      e = e && u1_of(i + 1) >= we;
+    }
+    e = e && (i == 0 ? ws >= u0 : u1_of(i - 1) + 5 <= ws);
+    elig[i] = e ? 1u : 0u;
+  }
+  if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+// Log write pre-pass (same reasoning as trailer_layout_kernel): the rounds
+// kernel rewrites the whole 64-B piece holding a record's 4-byte CRC field
+// [o, o+4) (db/log_writer.cc:113) instead of storing 4 bytes into it.
+//   *flag |= 1 unless the record offsets are non-decreasing (then only the
+//   neighbours' CRC fields can reach a piece);
+//   elig[i] = 1 iff the field lies in one piece, the piece lies inside the
+//   image (buf_len) and holds neither neighbour's CRC field.  Every other byte
+//   of the piece (payloads, length and type bytes, block padding) is only read
+//   and is stored back unchanged.
+__global__ void __launch_bounds__(256) log_window_kernel(const uint64_t* offs, uint64_t n,
+                                                         uint64_t buf_len, uint32_t* elig,
+                                                         uint32_t* flag) {
   const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
   bool bad = false;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
-    const uint64_t u0 = offsets[i & omask] + i * stride;
-    const uint64_t m = (uint64_t)lengths[i & lmask] + len;
-    bool b = m < 32;
-    if (i + 1 < n) b = b || offsets[(i + 1) & omask] + (i + 1) * stride < u0 + m + 5;
-    bad = bad || b;
+    const uint64_t o = offs[i], ws = o & ~63ull;
+    bool e = (o & 63) <= 60 && ws + 64 <= buf_len;
+    if (i + 1 < n) {
+      const uint64_t on = offs[i + 1];
+      bad = bad || on < o;
+      e = e && on >= ws + 64;
+    }
+    if (i > 0) e = e && offs[i - 1] + 4 <= ws;
+    elig[i] = e ? 1u : 0u;
   }
   if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
@@ -3725,7 +3799,8 @@ int launch_sort(CrcParams& p, DevTables* t, hipStream_t stream, uint64_t kStep, 
 #endif
 
 thread_local std::atomic<int> g_tune_sort{2};  // rounds kernel: 0 in order, 1 whole-batch sort, 2 per chunk
-thread_local std::atomic<int> g_tune_trailer_1pass{0};  // trailer writer (large batches): 0 = one pass, whole-sector stores when the layout allows; 1 = one pass, byte stores; 2 = two passes (CRC array + scatter)
+constexpr uint64_t kLogWindowMin = 1u << 15;  // log records: whole-piece CRC-field stores from here
+thread_local std::atomic<int> g_tune_trailer_1pass{0};  // large trailer / log-write batches: 0 = whole-64-B-piece stores where the layout allows; 1 = byte stores; 2 = trailers in two passes (CRC array + scatter)
 
 template <int MODE, int VAR>
 int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
@@ -4011,12 +4086,13 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // whole fixed cost to the call.
   const bool small = p.n_blocks <= 2ull * t->cus * flat_waves();
   if (pl.kernel == kRoundsK && mode == kTrailer && g_tune_trailer_1pass.load() == 0 && !small) {
-    // One pass with whole-sector trailer stores when the layout allows it
-    // (trailer_layout_kernel): a partial sector write costs an
+    // One pass with whole-64-B-piece trailer stores where the layout allows it
+    // (trailer_layout_kernel): a partial piece write costs an
     // HBM read-modify-write per trailer, a whole one does not.
-    StreamScratch sc;  // the layout flag, freed in stream order after the CRC kernel
-    if (sc.alloc(sizeof(uint32_t), stream)) return NOVA_E_NOMEM;
+    StreamScratch sc;  // flag + eligibility, freed in stream order after the CRC kernel
+    if (sc.alloc(sizeof(uint32_t) * (p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
     uint32_t* flag = static_cast<uint32_t*>(sc.p);
+    uint32_t* elig = flag + 1;
     hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return (int)e;
     uint64_t wgs = (p.n_blocks + 255) / 256;
@@ -4027,11 +4103,34 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
     hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, lo,
                        p.offsets ? ~0ull : 0ull, ll, p.lengths ? ~0ull : 0ull,
-                       p.offsets ? 0ull : p.stride, p.lengths ? 0u : p.len, p.n_blocks, flag);
+                       p.offsets ? 0ull : p.stride, p.lengths ? 0u : p.len, p.n_blocks, elig, flag);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     CrcParams q = p;
     q.tr_flag = flag;
+    q.init = elig;  // trailer mode reads each block's eligibility in place of an init
     return launch_rounds<kTrailer>(G, q, t, stream, pl.chunk);
+  }
+  if (pl.kernel == kRoundsK && mode == kLogWrite && g_tune_trailer_1pass.load() == 0 &&
+      p.n_blocks >= kLogWindowMin && p.offsets) {
+    // Whole-64-B-piece CRC-field stores where the layout allows it
+    // (log_window_kernel).  Small logs skip the pre-pass: its
+    // two launches would add to a latency-bound call.
+    StreamScratch sc;  // flag + eligibility, freed in stream order after the CRC kernel
+    if (sc.alloc(sizeof(uint32_t) * (p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
+    uint32_t* flag = static_cast<uint32_t*>(sc.p);
+    uint32_t* elig = flag + 1;
+    hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return (int)e;
+    uint64_t wgs = (p.n_blocks + 255) / 256;
+    const uint64_t cap = (uint64_t)t->cus * 8;
+    if (wgs > cap) wgs = cap;
+    hipLaunchKernelGGL(log_window_kernel, dim3(wgs), dim3(256), 0, stream, p.offsets, p.n_blocks,
+                       p.buf_len, elig, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    CrcParams q = p;
+    q.tr_flag = flag;
+    q.init = elig;  // log write reads each record's eligibility in place of an init
+    return launch_rounds<kLogWrite>(G, q, t, stream, pl.chunk);
   }
   if (pl.kernel == kRoundsK && mode == kTrailer && g_tune_trailer_1pass.load() == 2 && !small) {
     // Two passes: CRCs (type byte appended, masked) into this call's own

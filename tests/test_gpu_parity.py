@@ -384,28 +384,35 @@ def test_shared_stream_trailer_threads(torch_gpu, oracle):
             assert oracle.trailer(host[o:o + ln].tobytes(), 0, True) == got[o + ln:o + ln + 5].tobytes()
 
 
-@pytest.mark.parametrize("layout", ["packed", "gaps", "tiny", "permuted", "aligned"])
+@pytest.mark.parametrize("layout", ["packed", "gaps", "tiny", "small", "permuted", "aligned"])
 @pytest.mark.parametrize("quirk,ctype", [(True, 0), (False, 1)])
 def test_trailer_sector_stores(torch_gpu, oracle, layout, quirk, ctype):
     """Large trailer batches (the rounds kernel, > 6144 blocks) rewrite the whole
-    32-B sectors around each trailer when trailer_layout_kernel finds the blocks
-    ascending, disjoint and >= 32 B ("packed", "gaps", "aligned"); otherwise
-    ("tiny": some blocks < 32 B, "permuted": descriptors out of address order)
-    every trailer is written with byte stores.  Either way the WHOLE image must
-    equal the input with each block's trailer (table/table_builder.cc:202-206,
-    ltc/stoc_file_client_impl.cpp:713-719) in place: no byte outside the
-    trailers changes, including gap bytes and the bytes after the last block."""
+    64-B pieces around each trailer when trailer_layout_kernel finds the blocks
+    ascending and disjoint and no neighbour's trailer shares the pieces
+    ("packed", "gaps", "aligned"; "tiny" and "small" mix both forms: blocks of
+    0..31 B and 0..99 B put neighbouring trailers into one piece); descriptors
+    out of address order ("permuted") use byte stores for every block.  Either
+    way the WHOLE image must equal the input with each block's trailer
+    (table/table_builder.cc:202-206, ltc/stoc_file_client_impl.cpp:713-719) in
+    place: no byte outside the trailers changes, including gap bytes, the bytes
+    before the first block and after the last one."""
     torch = torch_gpu
     n = 9000
-    rng = np.random.default_rng(["packed", "gaps", "tiny", "permuted", "aligned"].index(layout) * 2 + quirk)
+    layouts = ["packed", "gaps", "tiny", "small", "permuted", "aligned"]
+    rng = np.random.default_rng(layouts.index(layout) * 2 + quirk)
     lens = rng.integers(32, 3000, n).astype(np.uint32)
     if layout == "tiny":
-        lens[rng.choice(n, 40, replace=False)] = rng.integers(0, 32, 40).astype(np.uint32)
+        lens[rng.choice(n, 400, replace=False)] = rng.integers(0, 32, 400).astype(np.uint32)
+    if layout == "small":
+        lens = rng.integers(0, 100, n).astype(np.uint32)
     if layout == "aligned":
-        lens = (lens + 31) & ~np.uint32(31)  # every trailer at a sector start
-    gaps = rng.integers(0, 40, n).astype(np.uint64) if layout == "gaps" else np.zeros(n, np.uint64)
+        lens = (lens + 63) & ~np.uint32(63)  # lengths a multiple of 64
+    gaps = rng.integers(0, 80, n).astype(np.uint64) if layout == "gaps" else np.zeros(n, np.uint64)
+    lead = 48 if layout != "aligned" else 0  # first block starts inside a piece
     offs = np.zeros(n, np.uint64)
-    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5) + gaps[:-1])
+    offs[0] = lead
+    offs[1:] = lead + np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5) + gaps[:-1])
     total = int(offs[-1]) + int(lens[-1]) + 5 + 64
     host = splitmix64_bytes(77, total)  # trailer bytes start as noise
     want = host.copy()
@@ -976,6 +983,52 @@ def _log_many_checks(torch, oracle, lanes, chunk):
     okh = ok.cpu().numpy()
     assert sorted(np.nonzero(okh == C.LOG_CHECKSUM_MISMATCH)[0].tolist()) == sorted(victims.tolist())
     assert int(bad.item()) == len(victims)
+
+
+@pytest.mark.parametrize("case", ["clean", "corrupt", "permuted"])
+def test_log_write_piece_stores(torch_gpu, oracle, case):
+    """Large log writes (>= 32768 records) rewrite the whole 64-B piece holding
+    each record's CRC field where log_window_kernel allows it.  Over a big
+    log::Writer image with bad-length and zero records, an image cut inside a
+    record (buf_len), descriptors past the image and (case "permuted")
+    descriptors out of file order, the WHOLE image must equal what the
+    byte-store form (the diagnostics knob) writes, and on the clean image what
+    the oracle's log::Writer restatement writes (db/log_writer.cc:99-114)."""
+    from novalsm_amd.synth import log_image
+    torch = torch_gpu
+    rng = np.random.default_rng(["clean", "corrupt", "permuted"].index(case) + 5)
+    n = 40000
+    plen = rng.integers(0, 300, n)
+    plen[rng.integers(0, n, 300)] = rng.integers(0, 3, 300)
+    host, offs, _, _ = log_image(3, plen)
+    offs = np.asarray(offs, np.uint64)
+    buf_len = host.size
+    if case != "clean":
+        for k, v in enumerate(rng.choice(len(offs) - 1, 200, replace=False)):
+            o = int(offs[v])
+            if k % 2 == 0:
+                host[o + 5] = 0xFF  # bad length: not read, not written
+            else:
+                host[o + 4:o + 7] = 0  # zero record
+        buf_len = host.size - 3  # the last record is cut (EOF)
+        offs = np.concatenate([offs, np.array([buf_len - 2, buf_len + 100], np.uint64)])
+    if case == "permuted":
+        offs = offs[rng.permutation(len(offs))]
+    img = np.concatenate([host, np.zeros(256, np.uint8)])
+    doffs = dev(torch, offs, torch.int64)
+    a = dev(torch, img)
+    C.log_write_crcs(a, doffs, buf_len=buf_len)
+    b = dev(torch, img)
+    with C.diagnostics() as L:
+        L.nova_diag_set_trailer_single_pass(1)  # byte stores
+        C.log_write_crcs(b, doffs, buf_len=buf_len)
+    ga, gb = a.cpu().numpy(), b.cpu().numpy()
+    diff = np.nonzero(ga != gb)[0]
+    assert diff.size == 0, (diff[:10], ga[diff[:10]], gb[diff[:10]])
+    if case == "clean":
+        want = img.copy()
+        oracle.log_write(want, offs)
+        assert np.array_equal(ga, want)
 
 
 @pytest.mark.parametrize("mode", ["store", "trailers", "verify"])
