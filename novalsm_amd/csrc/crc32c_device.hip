@@ -109,6 +109,7 @@ struct CrcParams {
   // pre-pass's eligibility array) rewrite the whole 64-B pieces holding its
   // trailer; null or nonzero: byte stores
   const uint32_t* tr_flag;
+  uint32_t wvar;  // diagnostics (timing): 1 = whole-piece stores non-temporal, 2 = no result writes
 };
 
 // ---- log records: bounds and status (db/log_reader.cc:228-262) ------------
@@ -157,7 +158,7 @@ constexpr int kVarStamps = 4;    // record per-wave s_memrealtime stamps (diagno
 constexpr int kVarStaticClaims = 8;  // stream kernel: claims without atomics (diagnostics)
 constexpr int kVarNarrow = 16;  // flat/rounds/units: one word's lookups in flight (fold4, A/B)
 constexpr int kVarWide = 32;    // stream kernel: a swath's 16 lookups in flight (fold4w, A/B)
-constexpr int kVarLsFast = 64;  // log-stream kernel: every swath on the fast path (ablation: WRONG CRCs)
+[[maybe_unused]] constexpr int kVarLsFast = 64;  // log-stream kernel: every swath on the fast path (ablation: WRONG CRCs)
 constexpr int kVarInit = 128;   // rounds kernel, store mode: per-block init values (general head masking)
 
 // 16-byte load through the global (not flat) address space.  Block bytes are
@@ -393,7 +394,7 @@ __device__ __forceinline__ uint4 patch_trailer(uint4 d, uint64_t pa, uint64_t u1
 // LDS helpers for tables at absolute LDS addresses (the dynamic region starts
 // at 0): a 4-lookup operator application, 16-B loads/stores, and the 16-B
 // prefix masks LM[n] (bytes [0, n) set) indexed by a clamped byte count.
-__device__ __forceinline__ uint32_t lds_apply(uint32_t tab, uint32_t x) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t lds_apply(uint32_t tab, uint32_t x) {
   const uint32_t t0 = lds_u32(nullptr, tab + ((x & 255u) << 2));
   const uint32_t t1 = lds_u32(nullptr, tab + 1024u + (((x >> 8) & 255u) << 2));
   const uint32_t t2 = lds_u32(nullptr, tab + 2048u + (((x >> 16) & 255u) << 2));
@@ -404,7 +405,7 @@ __device__ __forceinline__ uint4 lds_u128(uint32_t a) {
   const u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const u32x4*>(a);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ void lds_st128(uint32_t a, uint4 v) {
+[[maybe_unused]] __device__ __forceinline__ void lds_st128(uint32_t a, uint4 v) {
   u32x4 w;
   w.x = v.x;
   w.y = v.y;
@@ -414,7 +415,7 @@ __device__ __forceinline__ void lds_st128(uint32_t a, uint4 v) {
 }
 // Inverse of one zero-byte step of the reflected register (M_1^-1): the forward
 // bit step x' = (x >> 1) ^ (P if x & 1) leaves x & 1 in bit 31 of x' (P has it).
-__device__ __forceinline__ uint32_t unstep_byte(uint32_t x) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t unstep_byte(uint32_t x) {
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint32_t b = x >> 31;
@@ -1254,7 +1255,7 @@ __device__ __forceinline__ void finish_block(const uint8_t* lds, uint32_t byte_t
   // the prefetch at the loop head).
   const uint32_t nn = (uint32_t)(Y.u1 - Y.u0);
   if (nn < 4 && !raw) {
-    uint32_t l = ~(kLog ? 0u : Y.st);
+    uint32_t l = ~((kLog || MODE == kTrailer) ? 0u : Y.st);  // (trailer mode: Y.st is the piece eligibility)
     for (uint32_t i = 0; i < 3; i++) {
       const uint32_t r = (l >> 8) ^ lds_u32(lds, byte_tab + (l & 255u) * 4u);
       l = i < nn ? r : l;
@@ -1765,8 +1766,12 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   // a block's eligibility comes in as its init word)
   // log write: the same for the 64-B piece holding each record's CRC field
   // (log_window_kernel)
+#ifdef NOVA_DIAG
   const bool sect = (MODE == kTrailer || MODE == kLogWrite) && G >= 8 && p.tr_flag &&
                     *p.tr_flag == 0;
+#else
+  constexpr bool sect = false;
+#endif
 
   // ---- chunk claims (as the flat kernel) ---------------------------------------
   uint32_t victim = blockIdx.x, tried = 0, req = 0;
@@ -2209,9 +2214,17 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         w.y = wb_w.y;
         w.z = wb_w.z;
         w.w = wb_w.w;
-        *(__attribute__((address_space(1))) u32x4*)wb_a = w;
+#ifdef NOVA_DIAG
+        if (p.wvar == 1)
+          __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x4*)wb_a);
+        else if (p.wvar != 2)
+#endif
+          *(__attribute__((address_space(1))) u32x4*)wb_a = w;
       } else {
-        write_result<MODE>(p, wb_a, wb_v);
+#ifdef NOVA_DIAG
+        if (p.wvar != 2)
+#endif
+          write_result<MODE>(p, wb_a, wb_v);
       }
       wb_on = false;
     }
@@ -2602,6 +2615,10 @@ __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, co
 // byte for TableBuilder's ordering (table/table_builder.cc:202-206,
 // ltc/stoc_file_client_impl.cpp:713-719).  Inside the streaming kernel the
 // trailer stores per block cost ~12 points of HBM throughput.
+#ifdef NOVA_DIAG
+// Store-form experiments for the trailer writer and log CRC fields (DESIGN.md
+// 3.5b): measured, not faster than the CRC kernel's own byte stores.
+
 // Trailer writer pre-pass.  HBM writes whole 64-B pieces; a store that
 // covers only part of one (a 5-B trailer) costs a read-modify-write at the
 // memory, so the rounds kernel rewrites the whole aligned
@@ -2678,6 +2695,7 @@ __global__ void __launch_bounds__(256) trailer_scatter_kernel(uint8_t* base, con
                   (flags & NOVA_TRAILER_TB_QUIRK) != 0);
   }
 }
+#endif  // NOVA_DIAG
 
 #ifdef NOVA_DIAG
 // ---- crc32c_logstream_kernel<MODE>: a whole log image, record CRCs ----------
@@ -3799,8 +3817,10 @@ int launch_sort(CrcParams& p, DevTables* t, hipStream_t stream, uint64_t kStep, 
 #endif
 
 thread_local std::atomic<int> g_tune_sort{2};  // rounds kernel: 0 in order, 1 whole-batch sort, 2 per chunk
-constexpr uint64_t kLogWindowMin = 1u << 15;  // log records: whole-piece CRC-field stores from here
-thread_local std::atomic<int> g_tune_trailer_1pass{0};  // large trailer / log-write batches: 0 = whole-64-B-piece stores where the layout allows; 1 = byte stores; 2 = trailers in two passes (CRC array + scatter)
+#ifdef NOVA_DIAG
+thread_local std::atomic<int> g_tune_trailer_1pass{0};  // diagnostics: trailer / log-write store forms (run())
+constexpr uint64_t kLogWindowMin = 1u << 15;  // diagnostics: log records, whole-piece CRC-field stores from here
+#endif
 
 template <int MODE, int VAR>
 int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
@@ -4084,11 +4104,22 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // Batches that fit the implicit per-wave chunks (SSTable-sized, latency-bound)
   // write their trailers from the CRC kernel: a second launch would add its
   // whole fixed cost to the call.
+  // Trailers and log CRC fields are stored by the CRC kernel itself (byte
+  // stores).  The image writes cost ~13 points on SSTable-like images whatever
+  // their form -- two passes, whole 64-B pieces, non-temporal -- while the
+  // same kernels without the writes run at the verify rate;
+  // those forms stay in the diagnostics build as measured experiments.
+#ifdef NOVA_DIAG
   const bool small = p.n_blocks <= 2ull * t->cus * flat_waves();
-  if (pl.kernel == kRoundsK && mode == kTrailer && g_tune_trailer_1pass.load() == 0 && !small) {
-    // One pass with whole-64-B-piece trailer stores where the layout allows it
-    // (trailer_layout_kernel): a partial piece write costs an
-    // HBM read-modify-write per trailer, a whole one does not.
+  // g_tune_trailer_1pass: 2 = trailers in two passes; 3 = whole-64-B-piece
+  // stores; 4 = the same non-temporal; 5 = whole-piece form without result
+  // writes; 6 = no result writes (timing ablations: 5 and 6 write nothing)
+  const int tkn = g_tune_trailer_1pass.load();
+  p.wvar = tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : 0u;
+  const bool tk_piece = tkn == 3 || tkn == 4 || tkn == 5;
+  if (pl.kernel == kRoundsK && mode == kTrailer && tk_piece && !small) {
+    // whole-64-B-piece trailer stores where the layout allows it
+    // (trailer_layout_kernel)
     StreamScratch sc;  // flag + eligibility, freed in stream order after the CRC kernel
     if (sc.alloc(sizeof(uint32_t) * (p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
     uint32_t* flag = static_cast<uint32_t*>(sc.p);
@@ -4110,11 +4141,10 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     q.init = elig;  // trailer mode reads each block's eligibility in place of an init
     return launch_rounds<kTrailer>(G, q, t, stream, pl.chunk);
   }
-  if (pl.kernel == kRoundsK && mode == kLogWrite && g_tune_trailer_1pass.load() == 0 &&
+  if (pl.kernel == kRoundsK && mode == kLogWrite && tk_piece &&
       p.n_blocks >= kLogWindowMin && p.offsets) {
-    // Whole-64-B-piece CRC-field stores where the layout allows it
-    // (log_window_kernel).  Small logs skip the pre-pass: its
-    // two launches would add to a latency-bound call.
+    // whole-64-B-piece CRC-field stores where the layout allows it
+    // (log_window_kernel)
     StreamScratch sc;  // flag + eligibility, freed in stream order after the CRC kernel
     if (sc.alloc(sizeof(uint32_t) * (p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
     uint32_t* flag = static_cast<uint32_t*>(sc.p);
@@ -4132,7 +4162,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     q.init = elig;  // log write reads each record's eligibility in place of an init
     return launch_rounds<kLogWrite>(G, q, t, stream, pl.chunk);
   }
-  if (pl.kernel == kRoundsK && mode == kTrailer && g_tune_trailer_1pass.load() == 2 && !small) {
+  if (pl.kernel == kRoundsK && mode == kTrailer && tkn == 2 && !small) {
     // Two passes: CRCs (type byte appended, masked) into this call's own
     // stream-ordered array, then the trailer bytes (trailer_scatter_kernel).
     StreamScratch sc;  // freed in stream order after the scatter
@@ -4150,6 +4180,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
                        const_cast<uint8_t*>(p.base), p.offsets, p.lengths, tmp, p.n_blocks, p.flags);
     return (int)hipGetLastError();
   }
+#endif
   if (pl.kernel == kRoundsK) {
     switch (mode) {
       case kStore: return launch_rounds<kStore>(G, p, t, stream, pl.chunk);

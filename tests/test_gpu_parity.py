@@ -384,19 +384,20 @@ def test_shared_stream_trailer_threads(torch_gpu, oracle):
             assert oracle.trailer(host[o:o + ln].tobytes(), 0, True) == got[o + ln:o + ln + 5].tobytes()
 
 
+@pytest.mark.parametrize("form", [0, 2, 3])
 @pytest.mark.parametrize("layout", ["packed", "gaps", "tiny", "small", "permuted", "aligned"])
 @pytest.mark.parametrize("quirk,ctype", [(True, 0), (False, 1)])
-def test_trailer_sector_stores(torch_gpu, oracle, layout, quirk, ctype):
-    """Large trailer batches (the rounds kernel, > 6144 blocks) rewrite the whole
-    64-B pieces around each trailer when trailer_layout_kernel finds the blocks
-    ascending and disjoint and no neighbour's trailer shares the pieces
-    ("packed", "gaps", "aligned"; "tiny" and "small" mix both forms: blocks of
-    0..31 B and 0..99 B put neighbouring trailers into one piece); descriptors
-    out of address order ("permuted") use byte stores for every block.  Either
-    way the WHOLE image must equal the input with each block's trailer
-    (table/table_builder.cc:202-206, ltc/stoc_file_client_impl.cpp:713-719) in
-    place: no byte outside the trailers changes, including gap bytes, the bytes
-    before the first block and after the last one."""
+def test_trailer_store_forms(torch_gpu, oracle, layout, quirk, ctype, form):
+    """Large trailer batches (the rounds kernel, > 6144 blocks) in every store
+    form: 0 the product's byte stores from the CRC kernel; diagnostics 2 (CRC
+    array + scatter pass) and 3 (whole 64-B pieces around each trailer where
+    trailer_layout_kernel allows: blocks ascending and disjoint, no neighbour's
+    trailer in the piece -- "tiny" and "small" mix both forms, "permuted" falls
+    back to byte stores).  The WHOLE image must equal the input with each
+    block's trailer (table/table_builder.cc:202-206,
+    ltc/stoc_file_client_impl.cpp:713-719) in place: no byte outside the
+    trailers changes, including gap bytes, the bytes before the first block and
+    after the last one."""
     torch = torch_gpu
     n = 9000
     layouts = ["packed", "gaps", "tiny", "small", "permuted", "aligned"]
@@ -422,8 +423,13 @@ def test_trailer_sector_stores(torch_gpu, oracle, layout, quirk, ctype):
                                                 dtype=np.uint8)
     order = rng.permutation(n) if layout == "permuted" else np.arange(n)
     buf = dev(torch, host)
-    C.write_trailers(buf, dev(torch, offs[order], torch.int64), dev(torch, lens[order], torch.int32),
-                     ctype, quirk)
+    do, dl = dev(torch, offs[order], torch.int64), dev(torch, lens[order], torch.int32)
+    if form:
+        with C.diagnostics() as D:
+            D.nova_diag_set_trailer_single_pass(form)
+            C.write_trailers(buf, do, dl, ctype, quirk)
+    else:
+        C.write_trailers(buf, do, dl, ctype, quirk)
     got = buf.cpu().numpy()
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, (bad[:10], got[bad[:10]], want[bad[:10]])
@@ -986,14 +992,14 @@ def _log_many_checks(torch, oracle, lanes, chunk):
 
 
 @pytest.mark.parametrize("case", ["clean", "corrupt", "permuted"])
-def test_log_write_piece_stores(torch_gpu, oracle, case):
-    """Large log writes (>= 32768 records) rewrite the whole 64-B piece holding
-    each record's CRC field where log_window_kernel allows it.  Over a big
-    log::Writer image with bad-length and zero records, an image cut inside a
-    record (buf_len), descriptors past the image and (case "permuted")
-    descriptors out of file order, the WHOLE image must equal what the
-    byte-store form (the diagnostics knob) writes, and on the clean image what
-    the oracle's log::Writer restatement writes (db/log_writer.cc:99-114)."""
+def test_log_write_store_forms(torch_gpu, oracle, case):
+    """The diagnostics build's whole-64-B-piece form of large log writes
+    (>= 32768 records; log_window_kernel decides per record) against the
+    product's byte stores.  Over a big log::Writer image with bad-length and
+    zero records, an image cut inside a record (buf_len), descriptors past the
+    image and (case "permuted") descriptors out of file order, the WHOLE images
+    must be equal, and on the clean image equal to what the oracle's
+    log::Writer restatement writes (db/log_writer.cc:99-114)."""
     from novalsm_amd.synth import log_image
     torch = torch_gpu
     rng = np.random.default_rng(["clean", "corrupt", "permuted"].index(case) + 5)
@@ -1020,7 +1026,7 @@ def test_log_write_piece_stores(torch_gpu, oracle, case):
     C.log_write_crcs(a, doffs, buf_len=buf_len)
     b = dev(torch, img)
     with C.diagnostics() as L:
-        L.nova_diag_set_trailer_single_pass(1)  # byte stores
+        L.nova_diag_set_trailer_single_pass(3)  # whole-piece stores
         C.log_write_crcs(b, doffs, buf_len=buf_len)
     ga, gb = a.cpu().numpy(), b.cpu().numpy()
     diff = np.nonzero(ga != gb)[0]
@@ -1057,8 +1063,8 @@ def test_large_blocks_hint_same_results(torch_gpu, oracle, mode):
             buf = dev(torch, host)
             C.write_trailers(buf, do, dl, 0, True, hint_large=hint)
             bufs.append(buf.cpu().numpy())
-        with C.diagnostics() as L:  # the single-pass A/B (trailer bytes from the CRC kernel)
-            L.nova_diag_set_trailer_single_pass(1)
+        with C.diagnostics() as L:  # the two-pass A/B (CRC array + scatter)
+            L.nova_diag_set_trailer_single_pass(2)
             buf = dev(torch, host)
             C.write_trailers(buf, do, dl, 0, True)
             bufs.append(buf.cpu().numpy())

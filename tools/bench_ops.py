@@ -137,9 +137,13 @@ def main() -> int:
                 blk = buf[o:o + ln + 5].cpu().numpy().tobytes()
                 ok &= orc.trailer(blk[:ln], 0, True) == blk[ln:]
             emit("trailers", wl, sum_len + 5 * n, sec, ok, {"image": image})
-            # A/B: 1 = one pass with byte stores, 2 = two passes (CRC array +
-            # scatter); the default is one pass with whole-sector stores
-            for var, name in ((1, "trailers_single_pass_bytes"), (2, "trailers_two_pass")):
+            # store-form A/B (diagnostics build; the product stores the trailer
+            # bytes from the CRC kernel): 2 = two passes (CRC array + scatter),
+            # 3 = whole 64-B pieces, 4 = the same non-temporal, 5 = pieces and
+            # 6 = the product form without result writes (timing only)
+            for var, name in ((2, "trailers_two_pass"), (3, "trailers_pieces"),
+                              (4, "trailers_pieces_nt"), (5, "trailers_pieces_no_writes"),
+                              (6, "trailers_no_writes")):
                 with C.diagnostics() as D:
                     D.nova_diag_set_trailer_single_pass(var)
                     sec1 = timed(torch, tw, args.steps, args.warmup, stream)
@@ -160,6 +164,13 @@ def main() -> int:
             ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
             emit("verify", wl, sum_len + 6 * n, sec, ok, {"image": image})
             sweep("verify", vf, sum_len + 6 * n)
+            with C.diagnostics() as D:  # timing ablation: no ok/mismatch writes
+                D.nova_diag_set_trailer_single_pass(6)
+                sec1 = timed(torch, vf, args.steps, args.warmup, stream)
+                D.nova_diag_set_trailer_single_pass(0)
+            gbs1 = (sum_len + 6 * n) / sec1 / 1e9
+            print(json.dumps({"sweep": "verify_no_writes", "image": image, "GBps": round(gbs1, 1),
+                              "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
         del buf
         torch.cuda.empty_cache()
 
@@ -188,6 +199,16 @@ def main() -> int:
                 ok &= int.from_bytes(rec[:4].tobytes(), "little") == want
             emit("log_write", wl, sum_rec, sec, ok)
             sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
+            for var, name in ((3, "log_write_pieces"), (4, "log_write_pieces_nt"),
+                              (5, "log_write_pieces_no_writes"), (6, "log_write_no_writes")):
+                with C.diagnostics() as D:
+                    D.nova_diag_set_trailer_single_pass(var)
+                    sec1 = timed(torch, lambda: C.log_write_crcs(buf, o, stream=stream), args.steps,
+                                 args.warmup, stream)
+                    D.nova_diag_set_trailer_single_pass(0)
+                gbs1 = sum_rec / sec1 / 1e9
+                print(json.dumps({"sweep": name, "GBps": round(gbs1, 1),
+                                  "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
         if "log_verify" in ops:
             C.log_write_crcs(buf, o, stream=stream)
             okb = torch.empty(n, dtype=torch.uint8, device="cuda")
