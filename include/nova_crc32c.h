@@ -260,8 +260,11 @@ void nova_diag_set_variable_kernel(int kernel);
 /* Rounds kernel: take the batch in order (0), sort it by block step count
  * first (1, a pre-pass), or sort each claimed chunk of 64 blocks (2, default). */
 void nova_diag_set_rounds_sort(int on);
-/* Trailer writer on the rounds kernel: 1 = one pass (trailer bytes stored by
- * the CRC kernel), 0 = two passes (default). */
+/* Store form of large trailer-writer and log-write batches:
+ * 0 = the product's (trailer bytes / CRC fields stored by the CRC kernel),
+ * 2 = trailers in two passes (CRC array + scatter), 3 = whole 64-B pieces
+ * where the layout allows, 4 = the same non-temporal; timing ablations that
+ * write NO results: 5 = whole-piece form, 6 = product form (any mode). */
 void nova_diag_set_trailer_single_pass(int on);
 /* Burst (one-SSTable) kernel: 0 automatic, 16 or 64 lanes per block forced for
  * any batch size of store / trailer / verify, -1 never. */
