@@ -2455,14 +2455,30 @@ __global__ void __launch_bounds__(BurstCfg<V>::kWaves * 64) crc32c_burst_kernel(
     if constexpr (kTail2) Y.t2 = gload16(valid && u1 + 4 > E + 16 ? E + 16 : zl);
     if (Kw) load_pass(d, 0);
   };
+#ifdef NOVA_DIAG
+  // per-wave phase stamps (s_memrealtime, 100 MHz): entry, descriptors used,
+  // tables + first data landed, first block folded, first result written
+  uint64_t st[5] = {0, 0, 0, 0, 0};
+  const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (p.stamps) st[0] = __builtin_amdgcn_s_memrealtime();
+#endif
   const bool live0 = bw < n_all;
   if (live0) start_blocks();
+#ifdef NOVA_DIAG
+  if (p.stamps) {
+    asm volatile("" ::"v"((uint32_t)Kw));
+    st[1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   // tables by LDS-DMA while the first block's loads are in flight
   glds_copy(0, p.tab_main, Cfg::kTree);
   glds_copy(Cfg::kTree, p.tab_tree, Cfg::kLevels * kTreeBytes);
   glds_copy(burst_byte_tab<V>(), p.tab_byte, 1024);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+#ifdef NOVA_DIAG
+  if (p.stamps) st[2] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (!live0) return;
 
   for (;;) {
@@ -2496,8 +2512,25 @@ __global__ void __launch_bounds__(BurstCfg<V>::kWaves * 64) crc32c_burst_kernel(
     }
     uint64_t wb_a = 0;
     uint32_t wb_v = 0;
+#ifdef NOVA_DIAG
+    if (p.stamps && !st[3]) {
+      asm volatile("" ::"v"(v));
+      st[3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     finish_block<MODE, Cfg::kTree>(lds, burst_byte_tab<V>(), p, raw, v, Y, wb_a, wb_v);
     if (q == 0 && Y.valid) write_result<MODE>(p, wb_a, wb_v);
+#ifdef NOVA_DIAG
+    if (p.stamps && !st[4]) {
+      __builtin_amdgcn_s_waitcnt(0);
+      st[4] = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) {
+        for (int k = 0; k < 5; k++) p.stamps[8 * wid + k] = st[k];
+        p.stamps[8 * wid + 5] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // XCC id
+        p.stamps[8 * wid + 6] = Kw;
+      }
+    }
+#endif
     bw += step_blocks;
     if (bw >= n_all) break;
     start_blocks();
@@ -4006,6 +4039,9 @@ int launch_burst(CrcParams& p, DevTables* t, hipStream_t stream) {
     }
     if (wgs > cus) wgs = cus;  // the rest by the grid-stride loop
   }
+#ifdef NOVA_DIAG
+  if (g_tune_var.load() == kVarStamps) p.stamps = g_diag_stamps.load();
+#endif
   hipLaunchKernelGGL((crc32c_burst_kernel<V, MODE>), dim3(wgs), dim3(64 * nw), burst_lds<V>(),
                      stream, p);
   return (int)hipGetLastError();
