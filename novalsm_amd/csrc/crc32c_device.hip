@@ -2181,6 +2181,12 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         Y.t.z = __shfl(piece.z, src);
         Y.t.w = __shfl(piece.w, src);
       }
+#ifdef NOVA_DIAG
+      if (p.wvar == 3) {  // timing ablation: no per-block epilogue, no result (WRONG)
+        wb_a = 0;
+        wb_v = v;
+      } else
+#endif
       finish_block<MODE>(lds, kByteTab, p, raw, v, Y, wb_a, wb_v);
       wb_on = q == 0 && Y.valid;  // written after the next step's loads are issued
       if constexpr (MODE == kTrailer) {
@@ -2222,7 +2228,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
           *(__attribute__((address_space(1))) u32x4*)wb_a = w;
       } else {
 #ifdef NOVA_DIAG
-        if (p.wvar != 2)
+        if (p.wvar < 2)
 #endif
           write_result<MODE>(p, wb_a, wb_v);
       }
@@ -4151,7 +4157,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // stores; 4 = the same non-temporal; 5 = whole-piece form without result
   // writes; 6 = no result writes (timing ablations: 5 and 6 write nothing)
   const int tkn = g_tune_trailer_1pass.load();
-  p.wvar = tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : 0u;
+  p.wvar = tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : tkn == 7 ? 3u : 0u;
   const bool tk_piece = tkn == 3 || tkn == 4 || tkn == 5;
   if (pl.kernel == kRoundsK && mode == kTrailer && tk_piece && !small) {
     // whole-64-B-piece trailer stores where the layout allows it

@@ -143,7 +143,7 @@ def main() -> int:
             # 6 = the product form without result writes (timing only)
             for var, name in ((2, "trailers_two_pass"), (3, "trailers_pieces"),
                               (4, "trailers_pieces_nt"), (5, "trailers_pieces_no_writes"),
-                              (6, "trailers_no_writes")):
+                              (6, "trailers_no_writes"), (7, "trailers_no_epilogue")):
                 with C.diagnostics() as D:
                     D.nova_diag_set_trailer_single_pass(var)
                     sec1 = timed(torch, tw, args.steps, args.warmup, stream)
@@ -200,7 +200,8 @@ def main() -> int:
             emit("log_write", wl, sum_rec, sec, ok)
             sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
             for var, name in ((3, "log_write_pieces"), (4, "log_write_pieces_nt"),
-                              (5, "log_write_pieces_no_writes"), (6, "log_write_no_writes")):
+                              (5, "log_write_pieces_no_writes"), (6, "log_write_no_writes"),
+                              (7, "log_write_no_epilogue")):
                 with C.diagnostics() as D:
                     D.nova_diag_set_trailer_single_pass(var)
                     sec1 = timed(torch, lambda: C.log_write_crcs(buf, o, stream=stream), args.steps,

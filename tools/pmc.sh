@@ -8,7 +8,7 @@ CFG=${1:-2}
 mkdir -p gpurun_out/pmc$CFG
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc$CFG/$ctr -o pmc \
-    -- python3 bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --verify 0 \
+    -- python3 bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --verify 0 --secondary none --settle-ms 0 \
     > gpurun_out/pmc$CFG/$ctr.log 2>&1 || { echo "pmc $ctr failed rc=$?"; exit 1; }
 done
 python3 tools/pmc_summary.py $CFG
