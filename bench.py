@@ -207,16 +207,20 @@ def launch_ranks(n: int, argv) -> int:
 # ---- one device-resident config ------------------------------------------------
 
 class Ctx:
-    def __init__(self, world, rank, dev, dist):
-        self.world, self.rank, self.dev, self.dist = world, rank, dev, dist
+    """world/rank of this run; `on` when a process group exists (every run
+    started by torch.distributed.run, a world of 1 included, so the RCCL path
+    is the one a 1-GPU torchrun exercises)."""
+
+    def __init__(self, world, rank, dev, dist, on):
+        self.world, self.rank, self.dev, self.dist, self.on = world, rank, dev, dist, on
 
     def barrier(self):
-        if self.world > 1:
+        if self.on:
             self.dist.barrier()
 
     def all_gather_f64(self, x: float):
         import torch
-        if self.world == 1:
+        if not self.on:
             return [x]
         t = torch.tensor([x], dtype=torch.float64, device=self.dev)
         parts = [torch.empty_like(t) for _ in range(self.world)]
@@ -319,7 +323,7 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
     roof.update({"kernel_ms_avg": round(avg_launch_s * 1e3, 4),
                  "kernel_ms_min": round(min(kernel_ms), 4),
                  "kernel_ms_median": round(sorted(kernel_ms)[len(kernel_ms) // 2], 4)})
-    if ctx.world > 1:
+    if ctx.on:
         roof["kernel_ms_avg_per_rank"] = [round(x, 4) for x in rank_kernel_ms]
     del buf, out
     torch.cuda.empty_cache()
@@ -443,22 +447,26 @@ def main() -> int:
     import torch.distributed as dist
     from novalsm_amd import crc32c as C
 
-    if world > 1:
+    # under torch.distributed.run (WORLD_SIZE set, any world size): one rank
+    # per GPU, RCCL for the barriers and the max-over-ranks time
+    dist_on = "WORLD_SIZE" in os.environ
+    if dist_on:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = dist.get_world_size()  # the world RCCL reports
-    dev = torch.device("cuda", local if world > 1 else 0)
+        rank = dist.get_rank()
+    dev = torch.device("cuda", local if dist_on else 0)
     torch.cuda.set_device(dev)
     C.load()
     if args.lanes or args.seg:
         C.set_tuning(args.lanes, args.seg)
     if C.load().nova_device_init() != 0:
         raise SystemExit("nova_device_init failed")
-    ctx = Ctx(world, rank, dev, dist)
+    ctx = Ctx(world, rank, dev, dist, dist_on)
 
     if args.config == 5:
         rc = run_host_config(args, ctx)
-        if world > 1:
+        if dist_on:
             dist.barrier()
             dist.destroy_process_group()
         return rc
@@ -507,7 +515,7 @@ def main() -> int:
             # rank 0 at N=1 only: the CPU sample is the same at every N
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     return rc

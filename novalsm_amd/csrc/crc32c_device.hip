@@ -110,6 +110,8 @@ struct CrcParams {
   // trailer; null or nonzero: byte stores
   const uint32_t* tr_flag;
   uint32_t wvar;  // diagnostics (timing): 1 = whole-piece stores non-temporal, 2 = no result writes
+                  // 4 = whole pieces into wpieces (128 B per block), copied by a second pass
+  uint8_t* wpieces;
 };
 
 // ---- log records: bounds and status (db/log_reader.cc:228-262) ------------
@@ -2200,6 +2202,9 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
           const uint64_t tv = (uint64_t)((p.flags >> 8) & 0xffu) | ((uint64_t)m << 8);
           wb_a = (Y.u1 & ~63ull) + 16u * (uint32_t)q;
           wb_w = patch_trailer(piece, wb_a, Y.u1, tv);
+#ifdef NOVA_DIAG
+          if (p.wvar == 4) wb_a = (uint64_t)p.wpieces + 128ull * Y.rec + 16u * (uint32_t)q;
+#endif
         }
       }
       if constexpr (MODE == kLogWrite) {
@@ -2674,13 +2679,16 @@ __global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, co
 //   above the first block's start (i == 0) and is not the last block's (its
 //   window may run past the image).  Window bytes outside every block (gaps)
 //   lie between two blocks of the image, so inside the caller's allocation.
-__global__ void __launch_bounds__(256) trailer_layout_kernel(const uint64_t* offsets, uint64_t omask,
-                                                             const uint32_t* lengths, uint64_t lmask,
-                                                             uint64_t stride, uint32_t len, uint64_t n,
-                                                             uint32_t* elig, uint32_t* flag) {
+//   Windows are aligned in absolute addresses (ba = the image base), as the
+//   kernels that store them see them.
+__global__ void __launch_bounds__(256) trailer_layout_kernel(uint64_t ba, const uint64_t* offsets,
+                                                             uint64_t omask, const uint32_t* lengths,
+                                                             uint64_t lmask, uint64_t stride,
+                                                             uint32_t len, uint64_t n, uint32_t* elig,
+                                                             uint32_t* flag) {
   const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
   bool bad = false;
-  auto u0_of = [&](uint64_t i) { return offsets[i & omask] + i * stride; };
+  auto u0_of = [&](uint64_t i) { return ba + offsets[i & omask] + i * stride; };
   auto u1_of = [&](uint64_t i) { return u0_of(i) + lengths[i & lmask] + len; };
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
     const uint64_t u0 = u0_of(i), u1 = u1_of(i);
@@ -2722,6 +2730,74 @@ __global__ void __launch_bounds__(256) log_window_kernel(const uint64_t* offs, u
     elig[i] = e ? 1u : 0u;
   }
   if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+// Two-pass trailer writer with whole-piece stores, second pass: the CRC pass
+// left crc[i] = Mask(crc) (type appended); block i's trailer [u1, u1+5) is
+// patched into the aligned 64-B piece(s) holding it, which are read and
+// stored whole when trailer_layout_kernel found them private to the block
+// (*flag == 0, elig[i]); other blocks store their five bytes.  Eight lanes per
+// block: lane k owns the piece line s0 + 16k (k < 4, or < 8 when the trailer
+// crosses a piece).  The stores run after every read of the image, in their
+// own launch.
+__global__ void __launch_bounds__(256) trailer_rmw_kernel(uint8_t* base, const uint64_t* offsets,
+                                                          uint64_t omask, const uint32_t* lengths,
+                                                          uint64_t lmask, uint64_t stride, uint32_t len,
+                                                          const uint32_t* crc, const uint32_t* elig,
+                                                          const uint32_t* flag, uint64_t n,
+                                                          uint32_t flags) {
+  const uint64_t nth = ((uint64_t)gridDim.x * blockDim.x) >> 3;
+  const uint32_t k = threadIdx.x & 7u;
+  const bool layout_ok = *flag == 0;
+  const bool quirk = (flags & NOVA_TRAILER_TB_QUIRK) != 0;
+  const uint32_t type = (flags >> 8) & 0xffu;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3; i < n; i += nth) {
+    uint8_t* t = base + offsets[i & omask] + i * stride + lengths[i & lmask] + len;
+    const uint32_t m = crc[i];
+    if (layout_ok && elig[i]) {
+      const uint64_t u1 = (uint64_t)t, s0 = u1 & ~63ull;
+      const uint32_t np = ((u1 + 4) & ~63ull) != s0 ? 8u : 4u;
+      if (k < np) {
+        const uint32_t mq = quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m;
+        const uint64_t tv = (uint64_t)type | ((uint64_t)mq << 8);
+        const uint64_t a = s0 + 16u * k;
+        auto* pa = (__attribute__((address_space(1))) u32x4*)a;
+        u32x4 w = *pa;
+        const uint4 d = patch_trailer(make_uint4(w.x, w.y, w.z, w.w), a, u1, tv);
+        w.x = d.x;
+        w.y = d.y;
+        w.z = d.z;
+        w.w = d.w;
+        *pa = w;
+      }
+    } else if (k == 0) {
+      store_trailer(t, type, m, quirk);
+    }
+  }
+}
+
+// Whole-piece trailer form, second pass: the rounds kernel left block i's
+// patched window pieces at wpieces + 128 i (eligible blocks; the others stored
+// their bytes in place); copy them into the image after every read of it.
+__global__ void __launch_bounds__(256) trailer_piece_copy_kernel(uint8_t* base, const uint64_t* offsets,
+                                                                 uint64_t omask, const uint32_t* lengths,
+                                                                 uint64_t lmask, uint64_t stride,
+                                                                 uint32_t len, const uint8_t* wpieces,
+                                                                 const uint32_t* elig,
+                                                                 const uint32_t* flag, uint64_t n) {
+  const uint64_t nth = ((uint64_t)gridDim.x * blockDim.x) >> 3;
+  const uint32_t k = threadIdx.x & 7u;
+  if (*flag != 0) return;  // byte stores by the CRC kernel
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3; i < n; i += nth) {
+    if (!elig[i]) continue;
+    const uint64_t u1 = (uint64_t)(base + offsets[i & omask] + i * stride + lengths[i & lmask] + len);
+    const uint64_t s0 = u1 & ~63ull;
+    const uint32_t np = ((u1 + 4) & ~63ull) != s0 ? 8u : 4u;
+    if (k < np) {
+      const u32x4 w = *(const __attribute__((address_space(1))) u32x4*)(wpieces + 128 * i + 16 * k);
+      *(__attribute__((address_space(1))) u32x4*)(s0 + 16u * k) = w;
+    }
+  }
 }
 
 __global__ void __launch_bounds__(256) trailer_scatter_kernel(uint8_t* base, const uint64_t* offsets,
@@ -4158,14 +4234,18 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // writes; 6 = no result writes (timing ablations: 5 and 6 write nothing)
   const int tkn = g_tune_trailer_1pass.load();
   p.wvar = tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : tkn == 7 ? 3u : 0u;
-  const bool tk_piece = tkn == 3 || tkn == 4 || tkn == 5;
+  const bool tk_piece = tkn == 3 || tkn == 4 || tkn == 5 || tkn == 9;
+  if (tkn == 9) p.wvar = 4;
   if (pl.kernel == kRoundsK && mode == kTrailer && tk_piece && !small) {
     // whole-64-B-piece trailer stores where the layout allows it
     // (trailer_layout_kernel)
+    // (form 9: + the patched pieces, 128 B per block, copied by a second pass)
     StreamScratch sc;  // flag + eligibility, freed in stream order after the CRC kernel
-    if (sc.alloc(sizeof(uint32_t) * (p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
+    const size_t eb = (sizeof(uint32_t) * (p.n_blocks + 1) + 127) & ~size_t(127);
+    if (sc.alloc(eb + (tkn == 9 ? 128 * p.n_blocks : 0), stream)) return NOVA_E_NOMEM;
     uint32_t* flag = static_cast<uint32_t*>(sc.p);
     uint32_t* elig = flag + 1;
+    p.wpieces = static_cast<uint8_t*>(sc.p) + eb;
     hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return (int)e;
     uint64_t wgs = (p.n_blocks + 255) / 256;
@@ -4174,14 +4254,22 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     // descriptors as launch_rounds normalises them (absent arrays: stride / len)
     const uint64_t* lo = p.offsets ? p.offsets : reinterpret_cast<const uint64_t*>(t->zero_word);
     const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
-    hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, lo,
+    hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, lo,
                        p.offsets ? ~0ull : 0ull, ll, p.lengths ? ~0ull : 0ull,
                        p.offsets ? 0ull : p.stride, p.lengths ? 0u : p.len, p.n_blocks, elig, flag);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     CrcParams q = p;
     q.tr_flag = flag;
     q.init = elig;  // trailer mode reads each block's eligibility in place of an init
-    return launch_rounds<kTrailer>(G, q, t, stream, pl.chunk);
+    const int e2 = launch_rounds<kTrailer>(G, q, t, stream, pl.chunk);
+    if (e2 || tkn != 9) return e2;
+    uint64_t wgs8 = (p.n_blocks * 8 + 255) / 256;
+    if (wgs8 > cap) wgs8 = cap;
+    hipLaunchKernelGGL(trailer_piece_copy_kernel, dim3(wgs8), dim3(256), 0, stream,
+                       const_cast<uint8_t*>(p.base), lo, p.offsets ? ~0ull : 0ull, ll,
+                       p.lengths ? ~0ull : 0ull, p.offsets ? 0ull : p.stride, p.lengths ? 0u : p.len,
+                       p.wpieces, elig, flag, p.n_blocks);
+    return (int)hipGetLastError();
   }
   if (pl.kernel == kRoundsK && mode == kLogWrite && tk_piece &&
       p.n_blocks >= kLogWindowMin && p.offsets) {
@@ -4203,6 +4291,39 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     q.tr_flag = flag;
     q.init = elig;  // log write reads each record's eligibility in place of an init
     return launch_rounds<kLogWrite>(G, q, t, stream, pl.chunk);
+  }
+  if (pl.kernel == kRoundsK && mode == kTrailer && tkn == 8 && !small) {
+    // Two passes: CRCs into this call's own stream-ordered array (with the
+    // layout pre-pass's flag and eligibility), then trailer_rmw_kernel
+    StreamScratch sc;  // flag, eligibility, CRCs; freed in stream order after the second pass
+    if (sc.alloc(sizeof(uint32_t) * (2 * p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
+    uint32_t* flag = static_cast<uint32_t*>(sc.p);
+    uint32_t* elig = flag + 1;
+    uint32_t* tmp = elig + p.n_blocks;
+    hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return (int)e;
+    uint64_t wgs = (p.n_blocks + 255) / 256;
+    const uint64_t cap = (uint64_t)t->cus * 8;
+    if (wgs > cap) wgs = cap;
+    const uint64_t* lo = p.offsets ? p.offsets : reinterpret_cast<const uint64_t*>(t->zero_word);
+    const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
+    const uint64_t om = p.offsets ? ~0ull : 0ull, lm = p.lengths ? ~0ull : 0ull;
+    const uint64_t st = p.offsets ? 0ull : p.stride;
+    const uint32_t ln = p.lengths ? 0u : p.len;
+    hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, lo,
+                       om, ll, lm, st, ln, p.n_blocks, elig, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    CrcParams q = p;
+    q.out = tmp;
+    q.flags = (p.flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT;
+    const int e2 = launch_rounds<kStore>(G, q, t, stream, pl.chunk);
+    if (e2) return e2;
+    uint64_t wgs8 = (p.n_blocks * 8 + 255) / 256;
+    if (wgs8 > cap) wgs8 = cap;
+    hipLaunchKernelGGL(trailer_rmw_kernel, dim3(wgs8), dim3(256), 0, stream,
+                       const_cast<uint8_t*>(p.base), lo, om, ll, lm, st, ln, tmp, elig, flag,
+                       p.n_blocks, p.flags);
+    return (int)hipGetLastError();
   }
   if (pl.kernel == kRoundsK && mode == kTrailer && tkn == 2 && !small) {
     // Two passes: CRCs (type byte appended, masked) into this call's own

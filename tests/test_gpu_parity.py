@@ -384,7 +384,7 @@ def test_shared_stream_trailer_threads(torch_gpu, oracle):
             assert oracle.trailer(host[o:o + ln].tobytes(), 0, True) == got[o + ln:o + ln + 5].tobytes()
 
 
-@pytest.mark.parametrize("form", [0, 2, 3])
+@pytest.mark.parametrize("form", [0, 2, 3, 8, 9])
 @pytest.mark.parametrize("layout", ["packed", "gaps", "tiny", "small", "permuted", "aligned"])
 @pytest.mark.parametrize("quirk,ctype", [(True, 0), (False, 1)])
 def test_trailer_store_forms(torch_gpu, oracle, layout, quirk, ctype, form):

@@ -24,6 +24,7 @@ WORKLOADS=${WORKLOADS:-cfg3,sst4k,log}
 [[ $STEPS == *smoke* ]] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *pytest* ]] && step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 [[ $STEPS == *bench* ]] && step bench 600 python bench.py
+[[ $STEPS == *trun* ]] && step bench_torchrun 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr 127.0.0.1 --master-port=29533 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
 [[ $STEPS == *cfg3* ]] && step bench_config3 600 python bench.py --config 3 --no-cpu-baseline
 [[ $STEPS == *cfg4* ]] && step bench_config4 600 python bench.py --config 4 --no-cpu-baseline
 [[ $STEPS == *ops* ]] && step bench_ops 600 python -u tools/bench_ops.py
