@@ -139,10 +139,10 @@ def main() -> int:
             emit("trailers", wl, sum_len + 5 * n, sec, ok, {"image": image})
             # store-form A/B (diagnostics build; the product stores the trailer
             # bytes from the CRC kernel): 2 = two passes (CRC array + scatter),
-            # 3 = whole 64-B pieces, 4 = the same non-temporal, 5 = pieces and
+            # 8 = two passes, the second reading, patching and storing whole
+            # 64-B pieces, 3 = whole 64-B pieces, 4 = the same non-temporal, 5 = pieces and
             # 6 = the product form without result writes (timing only)
             for var, name in ((2, "trailers_two_pass"), (8, "trailers_two_pass_pieces"),
-                              (9, "trailers_pieces_deferred"),
                               (3, "trailers_pieces"),
                               (4, "trailers_pieces_nt"), (5, "trailers_pieces_no_writes"),
                               (6, "trailers_no_writes"), (7, "trailers_no_epilogue")):
