@@ -51,7 +51,11 @@ extern "C" {
  * (crc32c_units_kernel); without it blocks are checksummed whole in lockstep
  * rounds of similar-length blocks (crc32c_rounds_kernel), the faster choice
  * for NovaLSM's ~4 KiB data blocks.  Accepted by nova_crc32c_batch and
- * nova_sstable_write_trailers. */
+ * nova_sstable_write_trailers.  A hinted batch of at most 1024 blocks (and a
+ * fixed-stride batch of at most 8192 blocks over 64 KiB) is cut into pieces
+ * spread over the whole device and recombined (split-and-combine path): a few
+ * large blocks would otherwise run on a few waves.  Unhinted variable batches
+ * holding multi-MiB blocks should pass the hint. */
 #define NOVA_CRC32C_HINT_LARGE_BLOCKS 0x10u
 #define NOVA_CRC32C_TYPE(t) (((uint32_t)(uint8_t)(t)) << 8)
 
@@ -214,7 +218,8 @@ size_t nova_stream_slots(void);
 /* Lanes per block ("G") and segment bytes the dispatcher would pick for an
  * aligned fixed-stride batch; returns 1 for the streaming kernel, 0 for the
  * units kernel, 2 for the flat kernel, 3 for the rounds kernel, 4 for the
- * burst (one-SSTable latency) kernel.  nova_crc32c_describe writes a JSON object naming the kernel
+ * burst (one-SSTable latency) kernel, 5 for the split-and-combine path (a few
+ * large blocks cut into pieces over the whole device).  nova_crc32c_describe writes a JSON object naming the kernel
  * and its launch parameters (for reports and profiles); variable: 0 fixed-stride,
  * 1 variable-length, 2 variable-length with NOVA_CRC32C_HINT_LARGE_BLOCKS. */
 int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_unit,
@@ -269,6 +274,9 @@ void nova_diag_set_trailer_single_pass(int on);
 /* Burst (one-SSTable) kernel: 0 automatic, 16 or 64 lanes per block forced for
  * any batch size of store / trailer / verify, -1 never. */
 void nova_diag_set_burst_lanes(int lanes);
+/* Split-and-combine path for few large blocks: 0 automatic, 1 forced for any
+ * store / trailer / verify batch, -1 never. */
+void nova_diag_set_split(int on);
 /* XOR parity kernel variant: chunks per thread (bits 0-3), fragments loaded
  * together (bits 4-7), workgroups per CU (bits 8-15); 0 fields = default. */
 void nova_diag_set_parity_variant(int variant);

@@ -87,6 +87,7 @@ _DIAG_SIG = {
     "nova_diag_set_rounds_sort": (None, [_i32]),
     "nova_diag_set_trailer_single_pass": (None, [_i32]),
     "nova_diag_set_burst_lanes": (None, [_i32]),
+    "nova_diag_set_split": (None, [_i32]),
     "nova_diag_read_stream": (_i32, [_vp, _sz, _vp, _i32, _vp]),
     "nova_diag_read_ceiling": (_i32, [_vp, _sz, _vp, _i32, _i32, _vp]),
 }
@@ -176,6 +177,7 @@ def diagnostics():
         D.nova_diag_set_trailer_single_pass(0)
         D.nova_diag_set_parity_variant(0)
         D.nova_diag_set_burst_lanes(0)
+        D.nova_diag_set_split(0)
 
 
 def _check(rc: int, what: str) -> None:

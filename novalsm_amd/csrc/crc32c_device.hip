@@ -3220,6 +3220,120 @@ __global__ void __launch_bounds__(kLsWaves * 64) crc32c_logstream_kernel(CrcPara
 
 #endif  // NOVA_DIAG
 
+// ---- few large blocks: split and combine --------------------
+// Every kernel above gives a block to one lane group or one wave, so a batch
+// of a few large blocks (one 256 MiB buffer, 16 x 64 MiB) leaves the machine
+// idle: one 256 MiB block ran at 3.7 GB/s.  The split path cuts block i (its
+// n_i CRC input bytes: len_i, +1 type byte for verify) into pieces of S bytes
+// (S a multiple of 16) counted from the block's END -- piece j >= 1 is
+// [n_i - (K_i - j) S, n_i - (K_i - j - 1) S), piece 0 the head [0, n_i - (K_i - 1) S)
+// -- with K_i = min(kmax, ceil(n_i / S)) and slots j >= K_i empty.  A batch of
+// the pieces (the ordinary kernels, RAW) gives each piece's linear part raw_j;
+//   raw(block)            = xor_j M_{(K_i - 1 - j) S}(raw_j)      (split_fold_kernel)
+//   Extend(init, block)   = ~(M_{n_i}(~init) ^ raw(block))       (split_finish_kernel)
+// (util/crc32c.cc:487-588 computes the same value in one pass), and the finish
+// runs the mode's epilogue (store, trailer, verify) as the other kernels do.
+__device__ __forceinline__ uint64_t split_block_off(const CrcParams& p, uint64_t i) {
+  return p.offsets ? p.offsets[i] : i * p.stride;
+}
+__device__ __forceinline__ uint32_t split_block_len(const CrcParams& p, uint64_t i, uint32_t extra) {
+  return (p.lengths ? p.lengths[i] : p.len) + extra;
+}
+__device__ __forceinline__ uint32_t split_pieces(uint32_t n, uint32_t S, uint32_t kmax) {
+  const uint32_t k = n ? (uint32_t)(((uint64_t)n + S - 1) / S) : 1u;
+  return k < kmax ? k : kmax;
+}
+// M_{16 m} through the binary powers M_{16 * 2^b} (sh16 tables).
+__device__ __forceinline__ uint32_t shift16(const uint32_t* sh16, uint64_t m, uint32_t c) {
+  while (m) {
+    const int b = __builtin_ctzll(m);
+    c = gapply(sh16 + b * 1024, c);
+    m &= m - 1;
+  }
+  return c;
+}
+
+__global__ void __launch_bounds__(256) split_pieces_kernel(CrcParams p, uint32_t extra, uint32_t S,
+                                                           uint32_t kshift, uint64_t* poff,
+                                                           uint32_t* plen) {
+  const uint64_t slots = p.n_blocks << kshift;
+  const uint32_t kmax = 1u << kshift;
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < slots; s += nth) {
+    const uint64_t i = s >> kshift;
+    const uint32_t j = (uint32_t)s & (kmax - 1);
+    const uint64_t o = split_block_off(p, i);
+    const uint32_t n = split_block_len(p, i, extra);
+    const uint32_t k = split_pieces(n, S, kmax);
+    uint64_t po = o;
+    uint32_t pl = 0;
+    if (j == 0) {
+      pl = n - (k - 1) * S;
+    } else if (j < k) {
+      po = o + n - (uint64_t)(k - j) * S;
+      pl = S;
+    }
+    poff[s] = po;
+    plen[s] = pl;
+  }
+}
+
+// One thread per piece slot; the grid covers the slots exactly (whole waves
+// when kmax >= 64, whose 64 lanes then share one block).
+__global__ void __launch_bounds__(256) split_fold_kernel(CrcParams p, uint32_t extra, uint32_t S,
+                                                         uint32_t kshift, const uint32_t* praw,
+                                                         uint32_t* acc) {
+  const uint64_t slots = p.n_blocks << kshift;
+  const uint32_t kmax = 1u << kshift;
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t c = 0;
+  uint64_t i = 0;
+  uint32_t j = 0;
+  if (s < slots) {
+    i = s >> kshift;
+    j = (uint32_t)s & (kmax - 1);
+    const uint32_t k = split_pieces(split_block_len(p, i, extra), S, kmax);
+    if (j < k) c = shift16(p.tab_sh16, (uint64_t)(k - 1 - j) * (S >> 4), praw[s]);
+  }
+  // xor over the lanes of one block: all 64 (kmax >= 64) or aligned groups of kmax
+  const uint32_t span = kmax < 64 ? kmax : 64u;
+  for (uint32_t d = 1; d < span; d <<= 1) c ^= __shfl_xor(c, (int)d);
+  if (s < slots && (j & (span - 1)) == 0 && c) atomicXor(acc + i, c);
+}
+
+__global__ void __launch_bounds__(256) split_finish_kernel(CrcParams p, int mode, uint32_t extra,
+                                                           const uint32_t* acc) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
+  const uint32_t type = (p.flags >> 8) & 0xffu;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n_blocks; i += nth) {
+    const uint32_t n = split_block_len(p, i, extra);
+    uint32_t crc = acc[i];
+    if (!raw) {
+      uint32_t l = ~(p.init ? p.init[i] : 0u);  // M_n(~init): n & 15 byte steps, then M_{16 (n >> 4)}
+      for (uint32_t r = 0; r < (n & 15u); r++) l = byte_step(l, 0u);
+      crc = ~(shift16(p.tab_sh16, n >> 4, l) ^ crc);
+    }
+    const uint8_t* d = p.base + split_block_off(p, i);
+    if (mode == kVerify) {
+      const uint32_t stored = (uint32_t)d[n] | ((uint32_t)d[n + 1] << 8) |
+                              ((uint32_t)d[n + 2] << 16) | ((uint32_t)d[n + 3] << 24);
+      const bool ok = unmask_crc(stored) == crc;  // table/table.cc:435-437
+      p.ok_out[i] = ok ? 1 : 0;
+      if (!ok && p.n_bad) atomicAdd(p.n_bad, 1u);
+      continue;
+    }
+    if (p.flags & NOVA_CRC32C_APPEND_TYPE) crc = ~byte_step(~crc, type);  // table/table_builder.cc:203
+    if (mode == kTrailer) {
+      store_trailer(const_cast<uint8_t*>(d) + n, type, mask_crc(crc),
+                    (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
+    } else {
+      if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
+      p.out[i] = crc;
+    }
+  }
+}
+
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
 __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                        uint64_t first_word) {
@@ -4193,11 +4307,98 @@ int launch_logstream(CrcParams& p, DevTables* t, hipStream_t stream) {
 }
 #endif  // NOVA_DIAG
 
+// Few large blocks -> the split-and-combine path (split_*_kernel): uniform
+// blocks over kBurstMaxLen in a batch of at most kSplitMaxBlocks, or a batch of
+// at most kSplitMaxHinted blocks the caller marks HINT_LARGE_BLOCKS (the host
+// does not see variable lengths).  Read-verify carries no flags: it splits only
+// when tuning forces it.  tools/big_blocks.py measures both sides.
+thread_local std::atomic<int> g_tune_split{0};  // 0 auto, 1 force, -1 off
+constexpr uint64_t kBurstMaxLen = 65536;
+constexpr uint64_t kSplitMaxBlocks = 8192, kSplitMaxHinted = 1024;
+constexpr uint64_t kSplitTargetPieces = 65536;
+bool split_wanted(int mode, const CrcParams& p, bool uniform, uint64_t len) {
+  if (mode != kStore && mode != kTrailer && mode != kVerify) return false;
+  const int ts = g_tune_split.load();
+  if (ts) return ts > 0;
+  if (mode == kVerify) return false;
+  if (g_tune_g.load() || g_tune_seg.load() || g_tune_kernel.load() || g_tune_burst.load()) return false;
+  if (p.n_blocks > kSplitMaxBlocks) return false;
+  if (uniform) return len > kBurstMaxLen;
+  return (p.flags & NOVA_CRC32C_HINT_LARGE_BLOCKS) != 0 && p.n_blocks <= kSplitMaxHinted;
+}
+uint32_t ceil_log2(uint64_t x) {
+  uint32_t k = 0;
+  while ((1ull << k) < x) k++;
+  return k;
+}
+// Piece size S and kmax = 2^kshift slots per block: about kSplitTargetPieces
+// pieces of 4..64 KiB for a uniform batch; 16 KiB pieces and enough slots for
+// 1 GiB of blocks in total otherwise.
+void split_shape(uint64_t n, bool uniform, uint64_t len_in, uint32_t* S, uint32_t* kshift) {
+  if (uniform) {
+    const uint64_t total = n * (len_in ? len_in : 1);
+    uint64_t s = 1ull << ceil_log2((total + kSplitTargetPieces - 1) / kSplitTargetPieces);
+    s = s < 4096 ? 4096 : (s > 65536 ? 65536 : s);
+    *S = (uint32_t)s;
+    const uint32_t k = ceil_log2((len_in + s - 1) / s);
+    *kshift = k > 16 ? 16u : k;
+  } else {
+    *S = 16384;
+    const uint32_t k = ceil_log2((kSplitTargetPieces + n - 1) / n);
+    *kshift = k > 16 ? 16u : k;
+  }
+}
+
+int launch_split(int mode, CrcParams& p, bool uniform, uint64_t len, DevTables* t, hipStream_t stream) {
+  const uint32_t extra = mode == kVerify ? 1u : 0u;
+  uint32_t S = 0, kshift = 0;
+  split_shape(p.n_blocks, uniform, len + extra, &S, &kshift);
+  const uint64_t slots = p.n_blocks << kshift;
+  // [piece offsets u64][piece lengths u32][piece raws u32][per-block xor u32],
+  // freed in stream order after the finish
+  StreamScratch sc;
+  if (sc.alloc(slots * 16 + p.n_blocks * 4, stream)) return NOVA_E_NOMEM;
+  uint64_t* poff = static_cast<uint64_t*>(sc.p);
+  uint32_t* plen = reinterpret_cast<uint32_t*>(poff + slots);
+  uint32_t* praw = plen + slots;
+  uint32_t* acc = praw + slots;
+  hipError_t e = hipMemsetAsync(acc, 0, p.n_blocks * 4, stream);
+  if (e != hipSuccess) return (int)e;
+  p.tab_sh16 = t->sh16;
+  const uint64_t cap = (uint64_t)t->cus * 8;
+  uint64_t wgs = (slots + 255) / 256;
+  hipLaunchKernelGGL(split_pieces_kernel, dim3(wgs < cap ? wgs : cap), dim3(256), 0, stream, p, extra,
+                     S, kshift, poff, plen);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  CrcParams q{};
+  q.base = p.base;
+  q.offsets = poff;
+  q.lengths = plen;
+  q.out = praw;
+  q.n_blocks = slots;
+  const bool big = S >= 16384;
+  q.flags = NOVA_CRC32C_RAW | (big ? NOVA_CRC32C_HINT_LARGE_BLOCKS : 0u);
+  const Plan pl = plan(slots, 0, false, kStore, big, (uint32_t)t->cus);
+  q.seg = pl.seg;
+  const int rc = pl.kernel == kRoundsK ? launch_rounds<kStore>(pl.G, q, t, stream, pl.chunk)
+                                       : launch_mode<kStore>(pl.G, q, t, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(split_fold_kernel, dim3((slots + 255) / 256), dim3(256), 0, stream, p, extra, S,
+                     kshift, praw, acc);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  wgs = (p.n_blocks + 255) / 256;
+  hipLaunchKernelGGL(split_finish_kernel, dim3(wgs < cap ? wgs : cap), dim3(256), 0, stream, p, mode,
+                     extra, acc);
+  return (int)hipGetLastError();
+}
+
 int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStream_t stream) {
   int err = 0;
   DevTables* t = tables(&err);
   if (!t) return err;
   if (p.n_blocks == 0) return 0;
+  if (split_wanted(mode, p, uniform, bytes_per_block))
+    return launch_split(mode, p, uniform, bytes_per_block, t, stream);
   if (const int bg = burst_lanes(mode, p.n_blocks, (uint32_t)t->cus)) {
     switch (mode) {
       case kStore: return launch_burst_g<kStore>(bg, p, t, stream);
@@ -4543,6 +4744,13 @@ int nova_crc32c_plan(size_t n_blocks, uint64_t bytes_per_block, int* lanes_per_u
   p.len = (uint32_t)bytes_per_block;
   p.stride = bytes_per_block;
   p.n_blocks = n_blocks;
+  if (split_wanted(kStore, p, true, bytes_per_block)) {
+    uint32_t S = 0, ks = 0;
+    split_shape(n_blocks, true, bytes_per_block, &S, &ks);
+    if (lanes_per_unit) *lanes_per_unit = 0;
+    if (seg_bytes) *seg_bytes = S;
+    return 5;  // split and combine (pieces of S bytes)
+  }
   if (const int bg = burst_lanes(kStore, n_blocks, cus_hint())) {
     if (lanes_per_unit) *lanes_per_unit = bg;
     if (seg_bytes) *seg_bytes = 0;
@@ -4570,6 +4778,18 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
   int sg = 0;
   if (!variable && !g_tune_seg.load()) sg = stream_lanes(p);
   int n;
+  if (variable == 0 || variable == 2) {
+    p.flags = variable == 2 ? NOVA_CRC32C_HINT_LARGE_BLOCKS : 0u;
+    if (split_wanted(kStore, p, variable == 0, len)) {
+      uint32_t S = 0, ks = 0;
+      split_shape(n_blocks, variable == 0, len, &S, &ks);
+      n = snprintf(buf, buflen,
+                   "{\"kernel\": \"split\", \"piece_bytes\": %u, \"slots_per_block\": %u, "
+                   "\"pieces\": \"%s\"}", S, 1u << ks,
+                   S >= 16384 ? "crc32c_units_kernel<16, 0>" : "crc32c_rounds_kernel");
+      return n;
+    }
+  }
   const int bg = variable == 3 ? 0 : burst_lanes(kStore, n_blocks, cus_hint());
   if (bg) {
     n = snprintf(buf, buflen,
@@ -4648,6 +4868,7 @@ void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
 void nova_diag_set_trailer_single_pass(int on) { g_tune_trailer_1pass.store(on); }
 
 void nova_diag_set_burst_lanes(int lanes) { g_tune_burst.store(lanes); }
+void nova_diag_set_split(int on) { g_tune_split.store(on); }
 
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {

@@ -1261,3 +1261,91 @@ def _log_96mib_checks(torch_gpu, oracle):
     want_st = oracle.log_check(buf.cpu().numpy(), offs)
     assert np.array_equal(ok.cpu().numpy(), want_st)
     assert int(nbad.item()) == int(((want_st == 0) | (want_st == 2)).sum()) >= 60
+
+
+@pytest.mark.parametrize("flags", [0, C.MASK_OUTPUT | C.APPEND_TYPE | C.TYPE(1), C.RAW])
+def test_split_few_large_blocks(torch_gpu, oracle, flags):
+    """Few large blocks take the split-and-combine path (pieces over the whole
+    device, linear parts folded with M_{16 m} shifts, then Extend's init and the
+    mode epilogue): fixed-stride blocks over 64 KiB in small batches, and
+    variable batches of <= 1024 blocks with HINT_LARGE_BLOCKS.  Equal to the
+    oracle's util/crc32c.cc restatement for odd lengths, odd offsets, per-block
+    init values and every flag; the same batches with the split path turned
+    off (diagnostics) give the same words."""
+    torch = torch_gpu
+    rng = np.random.default_rng(314)
+    # fixed stride: 1 x (5 MiB + 13) at offset 3; 7 x (300 KiB + 5), stride + 11
+    for n, L, pad, base in ((1, (5 << 20) + 13, 0, 3), (7, (300 << 10) + 5, 11, 1)):
+        stride = L + pad
+        host = splitmix64_bytes(n + 40, base + n * stride + 16).copy()
+        init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        assert C.describe(n, L, stride)["kernel"] == "split"
+        buf = dev(torch, host)
+        if flags & C.RAW:  # raw(D) = Extend(0xFFFFFFFF, D) ^ 0xFFFFFFFF; init is ignored
+            want = oracle.batch_strided(host[base:], stride, L, n,
+                                        np.full(n, 0xFFFFFFFF, np.uint32)) ^ np.uint32(0xFFFFFFFF)
+        else:
+            want = oracle.batch_strided(host[base:], stride, L, n, init, flags)
+        for split in (0, -1):
+            out = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+            with C.diagnostics() as D:
+                D.nova_diag_set_split(split)
+                C.batch_strided(buf, stride, L, n, init=dev(torch, init.view(np.int32)), flags=flags,
+                                out=out, base_offset=base)
+            assert np.array_equal(u32(out), want), (n, L, split)
+    # variable with the hint: lengths 0 .. 33 MiB, out of address order
+    lens = np.array([1, (70 << 10) + 3, (2 << 20) + 7, 0, (33 << 20) + 1, 5000, 65536, 17],
+                    dtype=np.uint32)
+    n = len(lens)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(9))
+    offs += 5
+    perm = rng.permutation(n)
+    offs, lens = offs[perm], lens[perm]
+    host = splitmix64_bytes(77, int(offs.max() + lens.max()) + 64).copy()
+    if flags & C.RAW:
+        want = oracle.batch(host, offs, lens, np.full(n, 0xFFFFFFFF, np.uint32)) ^ np.uint32(
+            0xFFFFFFFF)
+    else:
+        want = oracle.batch(host, offs, lens, None, flags)
+    assert C.describe(n, 0, 0, variable=True, large=True)["kernel"] == "split"
+    out = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    C.batch(dev(torch, host), dev(torch, offs, torch.int64), dev(torch, lens, torch.int32),
+            flags=flags | C.HINT_LARGE_BLOCKS, out=out)
+    assert np.array_equal(u32(out), want)
+
+
+@pytest.mark.parametrize("n", [1, 3, 64, 1000])
+def test_split_trailers_and_verify(torch_gpu, oracle, n):
+    """Trailers (HINT_LARGE_BLOCKS, <= 1024 blocks: the split path) written
+    byte-for-byte as table/table_builder.cc:202-206 with the quirk, nothing
+    else in the image touched; read-verify through the split path (forced:
+    verify carries no hint) flags exactly the corrupted blocks."""
+    torch = torch_gpu
+    rng = np.random.default_rng(n)
+    lens = rng.choice([3, 4096, 70000, 300000, 1 << 20], n).astype(np.uint32)
+    lens = (lens + rng.integers(0, 50, n)).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5))
+    total = int(offs[-1]) + int(lens[-1]) + 5 + 64
+    host = splitmix64_bytes(n + 3, total).copy()
+    want = host.copy()
+    for i in range(n):
+        o, ln = int(offs[i]), int(lens[i])
+        want[o + ln:o + ln + 5] = np.frombuffer(oracle.trailer(host[o:o + ln].tobytes(), 0, True),
+                                                dtype=np.uint8)
+    do, dl = dev(torch, offs, torch.int64), dev(torch, lens, torch.int32)
+    buf = dev(torch, host)
+    C.write_trailers(buf, do, dl, 0, True, hint_large=True)
+    assert np.array_equal(buf.cpu().numpy(), want)
+    # StoC order (verifiable), then corrupt a few blocks
+    buf = dev(torch, host)
+    C.write_trailers(buf, do, dl, 0, False, hint_large=True)
+    victims = rng.choice(n, min(n, 3), replace=False)
+    for v in victims:
+        buf[int(offs[v]) + int(lens[v]) // 2] ^= 0x40
+    with C.diagnostics() as D:
+        D.nova_diag_set_split(1)
+        ok, bad = C.verify_blocks(buf, do, dl)
+    assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
+    assert int(bad.item()) == len(victims)
