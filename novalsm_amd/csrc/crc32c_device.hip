@@ -3230,7 +3230,7 @@ __global__ void __launch_bounds__(kLsWaves * 64) crc32c_logstream_kernel(CrcPara
 // -- with K_i = min(kmax, ceil(n_i / S)) and slots j >= K_i empty.  A batch of
 // the pieces (the ordinary kernels, RAW) gives each piece's linear part raw_j;
 //   raw(block)            = xor_j M_{(K_i - 1 - j) S}(raw_j)      (split_fold_kernel)
-//   Extend(init, block)   = ~(M_{n_i}(~init) ^ raw(block))       (split_finish_kernel)
+//   Extend(init, block)   = ~(M_{n_i}(~init) ^ raw(block))       (split_finish)
 // (util/crc32c.cc:487-588 computes the same value in one pass), and the finish
 // runs the mode's epilogue (store, trailer, verify) as the other kernels do.
 __device__ __forceinline__ uint64_t split_block_off(const CrcParams& p, uint64_t i) {
@@ -3255,7 +3255,7 @@ __device__ __forceinline__ uint32_t shift16(const uint32_t* sh16, uint64_t m, ui
 
 __global__ void __launch_bounds__(256) split_pieces_kernel(CrcParams p, uint32_t extra, uint32_t S,
                                                            uint32_t kshift, uint64_t* poff,
-                                                           uint32_t* plen) {
+                                                           uint32_t* plen, uint32_t* acc) {
   const uint64_t slots = p.n_blocks << kshift;
   const uint32_t kmax = 1u << kshift;
   const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
@@ -3275,14 +3275,49 @@ __global__ void __launch_bounds__(256) split_pieces_kernel(CrcParams p, uint32_t
     }
     poff[s] = po;
     plen[s] = pl;
+    if (j == 0) acc[i] = 0;  // the block's xor word (split_fold_kernel, kmax > 64)
+  }
+}
+
+// Extend's init and the mode epilogue for block i with raw(block) = x.
+__device__ void split_finish(const CrcParams& p, int mode, uint32_t extra, uint64_t i, uint32_t x) {
+  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
+  const uint32_t type = (p.flags >> 8) & 0xffu;
+  const uint32_t n = split_block_len(p, i, extra);
+  uint32_t crc = x;
+  if (!raw) {
+    uint32_t l = ~(p.init ? p.init[i] : 0u);  // M_n(~init): n & 15 byte steps, then M_{16 (n >> 4)}
+    for (uint32_t r = 0; r < (n & 15u); r++) l = byte_step(l, 0u);
+    crc = ~(shift16(p.tab_sh16, n >> 4, l) ^ crc);
+  }
+  const uint8_t* d = p.base + split_block_off(p, i);
+  if (mode == kVerify) {
+    const uint32_t stored = (uint32_t)d[n] | ((uint32_t)d[n + 1] << 8) |
+                            ((uint32_t)d[n + 2] << 16) | ((uint32_t)d[n + 3] << 24);
+    const bool ok = unmask_crc(stored) == crc;  // table/table.cc:435-437
+    p.ok_out[i] = ok ? 1 : 0;
+    if (!ok && p.n_bad) atomicAdd(p.n_bad, 1u);
+    return;
+  }
+  if (p.flags & NOVA_CRC32C_APPEND_TYPE) crc = ~byte_step(~crc, type);  // table/table_builder.cc:203
+  if (mode == kTrailer) {
+    store_trailer(const_cast<uint8_t*>(d) + n, type, mask_crc(crc), (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
+  } else {
+    if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
+    p.out[i] = crc;
   }
 }
 
 // One thread per piece slot; the grid covers the slots exactly (whole waves
-// when kmax >= 64, whose 64 lanes then share one block).
-__global__ void __launch_bounds__(256) split_fold_kernel(CrcParams p, uint32_t extra, uint32_t S,
-                                                         uint32_t kshift, const uint32_t* praw,
-                                                         uint32_t* acc) {
+// when kmax >= 64, whose 64 lanes then share one block).  The lanes of one
+// block xor their shifted raws together; with kmax <= 64 one lane then holds
+// the block's raw and finishes it, otherwise each wave xors its part into the
+// block's word acc[i] (zeroed by split_pieces_kernel) and split_finish_kernel
+// follows.  (A last-arriving wave finishing instead measured slower: 2048
+// ordered atomics on one block's words for one 256 MiB block.)
+__global__ void __launch_bounds__(256) split_fold_kernel(CrcParams p, int mode, uint32_t extra,
+                                                         uint32_t S, uint32_t kshift,
+                                                         const uint32_t* praw, uint32_t* acc) {
   const uint64_t slots = p.n_blocks << kshift;
   const uint32_t kmax = 1u << kshift;
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3295,43 +3330,21 @@ __global__ void __launch_bounds__(256) split_fold_kernel(CrcParams p, uint32_t e
     const uint32_t k = split_pieces(split_block_len(p, i, extra), S, kmax);
     if (j < k) c = shift16(p.tab_sh16, (uint64_t)(k - 1 - j) * (S >> 4), praw[s]);
   }
-  // xor over the lanes of one block: all 64 (kmax >= 64) or aligned groups of kmax
   const uint32_t span = kmax < 64 ? kmax : 64u;
   for (uint32_t d = 1; d < span; d <<= 1) c ^= __shfl_xor(c, (int)d);
-  if (s < slots && (j & (span - 1)) == 0 && c) atomicXor(acc + i, c);
+  if (s >= slots || (j & (span - 1)) != 0) return;
+  if (kmax <= 64) {
+    split_finish(p, mode, extra, i, c);
+    return;
+  }
+  if (c) __hip_atomic_fetch_xor(acc + i, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(256) split_finish_kernel(CrcParams p, int mode, uint32_t extra,
                                                            const uint32_t* acc) {
   const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
-  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
-  const uint32_t type = (p.flags >> 8) & 0xffu;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n_blocks; i += nth) {
-    const uint32_t n = split_block_len(p, i, extra);
-    uint32_t crc = acc[i];
-    if (!raw) {
-      uint32_t l = ~(p.init ? p.init[i] : 0u);  // M_n(~init): n & 15 byte steps, then M_{16 (n >> 4)}
-      for (uint32_t r = 0; r < (n & 15u); r++) l = byte_step(l, 0u);
-      crc = ~(shift16(p.tab_sh16, n >> 4, l) ^ crc);
-    }
-    const uint8_t* d = p.base + split_block_off(p, i);
-    if (mode == kVerify) {
-      const uint32_t stored = (uint32_t)d[n] | ((uint32_t)d[n + 1] << 8) |
-                              ((uint32_t)d[n + 2] << 16) | ((uint32_t)d[n + 3] << 24);
-      const bool ok = unmask_crc(stored) == crc;  // table/table.cc:435-437
-      p.ok_out[i] = ok ? 1 : 0;
-      if (!ok && p.n_bad) atomicAdd(p.n_bad, 1u);
-      continue;
-    }
-    if (p.flags & NOVA_CRC32C_APPEND_TYPE) crc = ~byte_step(~crc, type);  // table/table_builder.cc:203
-    if (mode == kTrailer) {
-      store_trailer(const_cast<uint8_t*>(d) + n, type, mask_crc(crc),
-                    (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
-    } else {
-      if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
-      p.out[i] = crc;
-    }
-  }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n_blocks; i += nth)
+    split_finish(p, mode, extra, i, acc[i]);
 }
 
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
@@ -4354,22 +4367,21 @@ int launch_split(int mode, CrcParams& p, bool uniform, uint64_t len, DevTables* 
   uint32_t S = 0, kshift = 0;
   split_shape(p.n_blocks, uniform, len + extra, &S, &kshift);
   const uint64_t slots = p.n_blocks << kshift;
-  // [piece offsets u64][piece lengths u32][piece raws u32][per-block xor u32],
-  // freed in stream order after the finish
+  // [piece offsets u64][piece lengths u32][piece raws u32][per-block xor
+  // word], freed in stream order after the last kernel
   StreamScratch sc;
   if (sc.alloc(slots * 16 + p.n_blocks * 4, stream)) return NOVA_E_NOMEM;
   uint64_t* poff = static_cast<uint64_t*>(sc.p);
   uint32_t* plen = reinterpret_cast<uint32_t*>(poff + slots);
   uint32_t* praw = plen + slots;
   uint32_t* acc = praw + slots;
-  hipError_t e = hipMemsetAsync(acc, 0, p.n_blocks * 4, stream);
-  if (e != hipSuccess) return (int)e;
   p.tab_sh16 = t->sh16;
   const uint64_t cap = (uint64_t)t->cus * 8;
-  uint64_t wgs = (slots + 255) / 256;
+  const uint64_t wgs = (slots + 255) / 256;
   hipLaunchKernelGGL(split_pieces_kernel, dim3(wgs < cap ? wgs : cap), dim3(256), 0, stream, p, extra,
-                     S, kshift, poff, plen);
-  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+                     S, kshift, poff, plen, acc);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
   CrcParams q{};
   q.base = p.base;
   q.offsets = poff;
@@ -4383,11 +4395,12 @@ int launch_split(int mode, CrcParams& p, bool uniform, uint64_t len, DevTables* 
   const int rc = pl.kernel == kRoundsK ? launch_rounds<kStore>(pl.G, q, t, stream, pl.chunk)
                                        : launch_mode<kStore>(pl.G, q, t, stream);
   if (rc) return rc;
-  hipLaunchKernelGGL(split_fold_kernel, dim3((slots + 255) / 256), dim3(256), 0, stream, p, extra, S,
-                     kshift, praw, acc);
+  hipLaunchKernelGGL(split_fold_kernel, dim3(wgs), dim3(256), 0, stream, p, mode, extra, S, kshift,
+                     praw, acc);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-  wgs = (p.n_blocks + 255) / 256;
-  hipLaunchKernelGGL(split_finish_kernel, dim3(wgs < cap ? wgs : cap), dim3(256), 0, stream, p, mode,
+  if (kshift <= 6) return 0;  // kmax <= 64: the fold finished every block
+  const uint64_t fwgs = (p.n_blocks + 255) / 256;
+  hipLaunchKernelGGL(split_finish_kernel, dim3(fwgs < cap ? fwgs : cap), dim3(256), 0, stream, p, mode,
                      extra, acc);
   return (int)hipGetLastError();
 }
