@@ -203,3 +203,32 @@ def test_log_plan_sized_to_the_batch(n, chunk):
     d = C.describe(n, 0, 0, log=True)
     assert d["kernel"].startswith("crc32c_rounds_kernel<8, 3>"), d
     assert d["chunk_blocks"] == chunk
+
+
+@pytest.mark.parametrize("n,length,variable,large,piece,slots", [
+    (1, 256 << 20, False, False, 4096, 65536),      # one big buffer: ~64K pieces of 4 KiB
+    (16, 64 << 20, False, False, 16384, 4096),      # 1 GiB in 16 blocks: 16 KiB pieces
+    (4096, 256 << 10, False, False, 16384, 16),
+    (8192, 1 << 20, False, False, 65536, 16),       # 8 GiB: pieces capped at 64 KiB
+    (8193, 1 << 20, False, False, None, None),      # enough blocks: stream kernel
+    (4096, 64 << 10, False, False, None, None),     # <= 64 KiB blocks: burst kernel
+    (1, 0, True, True, 16384, 65536),               # hinted variable: room for 1 GiB
+    (1024, 0, True, True, 16384, 64),
+    (1025, 0, True, True, None, None),              # more blocks: burst / units
+    (16, 0, True, False, None, None)])              # no hint: lengths unknown, no split
+def test_split_plan(n, length, variable, large, piece, slots):
+    """Host-side dispatch of the split-and-combine path: few
+    large fixed-stride blocks, or <= 1024 hinted variable blocks, are cut into
+    pieces (describe() reports the piece size and slots per block; plan()
+    returns 5 with the piece size)."""
+    d = C.describe(n, length, length, variable=variable, large=large)
+    if piece is None:
+        assert d["kernel"] != "split", d
+        return
+    assert d["kernel"] == "split", d
+    assert (d["piece_bytes"], d["slots_per_block"]) == (piece, slots)
+    if not variable:
+        assert C.plan(n, length)[1] == piece
+        lanes = ctypes.c_int(-1)
+        seg = ctypes.c_uint32(0)
+        assert C.load().nova_crc32c_plan(n, length, ctypes.byref(lanes), ctypes.byref(seg)) == 5
