@@ -130,6 +130,12 @@ int nova_sstable_write_trailers(void* buf, const uint64_t* offsets, const uint32
 int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
                                size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
                                void* stream);
+/* The same with flags: only NOVA_CRC32C_HINT_LARGE_BLOCKS is read (a table of
+ * >= 16 KiB blocks: 32 KiB segments, or pieces over the whole device for at
+ * most 1024 blocks); results are identical. */
+int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
+                                  size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
+                                  uint32_t flags, void* stream);
 
 /* ---- MANIFEST / write-ahead log records ----------
  * buf holds buf_len bytes of a log file image starting at a 32 KiB log-block

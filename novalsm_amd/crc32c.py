@@ -57,6 +57,7 @@ _SIG = {
     "nova_crc32c_batch_strided": (_i32, [_vp, _u64, _u32, _sz, _vp, _vp, _u32, _vp]),
     "nova_sstable_write_trailers": (_i32, [_vp, _vp, _vp, _sz, _u32, _vp]),
     "nova_sstable_verify_blocks": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "nova_sstable_verify_blocks_ex": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _u32, _vp]),
     "nova_crc32c_stream_host": (_i32, [_vp, _u64, _u32, _sz, _vp, _u32, _sz, _i32]),
     "nova_crc32c_batch_host": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _sz, _i32]),
     "nova_sstable_write_trailers_host": (_i32, [_vp, _vp, _vp, _sz, _u32, _sz, _i32]),
@@ -332,9 +333,10 @@ def write_trailers(buf, offsets, sizes, type_byte: int = 0, tb_quirk: bool = Fal
     return buf
 
 
-def verify_blocks(buf, offsets, sizes, stream=None, ok=None, bad=None):
+def verify_blocks(buf, offsets, sizes, stream=None, ok=None, bad=None, hint_large: bool = False):
     """Returns (ok uint8 tensor, n_bad int32 tensor[1]).  A caller-supplied
-    `bad` accumulates (zero it first)."""
+    `bad` accumulates (zero it first).  hint_large: NOVA_CRC32C_HINT_LARGE_BLOCKS
+    (nova_sstable_verify_blocks_ex)."""
     import torch
     _require_gpu()
     n = int(offsets.numel())
@@ -345,10 +347,13 @@ def verify_blocks(buf, offsets, sizes, stream=None, ok=None, bad=None):
     if bad is None:
         bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
     dv = buf.device
-    rc = _L().nova_sstable_verify_blocks(_data(buf, "buf"), _arg(offsets, "offsets", _u64_dtypes(), dv),
-                                         _arg(sizes, "sizes", _u32_dtypes(), dv), n,
-                                         _arg(ok, "ok", (torch.uint8,), dv, n),
-                                         _arg(bad, "bad", _u32_dtypes(), dv, 1), _stream_ptr(stream))
+    args = (_data(buf, "buf"), _arg(offsets, "offsets", _u64_dtypes(), dv),
+            _arg(sizes, "sizes", _u32_dtypes(), dv), n, _arg(ok, "ok", (torch.uint8,), dv, n),
+            _arg(bad, "bad", _u32_dtypes(), dv, 1))
+    if hint_large:
+        rc = _L().nova_sstable_verify_blocks_ex(*args, HINT_LARGE_BLOCKS, _stream_ptr(stream))
+    else:
+        rc = _L().nova_sstable_verify_blocks(*args, _stream_ptr(stream))
     _check(rc, "nova_sstable_verify_blocks")
     return ok, bad
 

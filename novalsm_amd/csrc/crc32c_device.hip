@@ -4323,8 +4323,8 @@ int launch_logstream(CrcParams& p, DevTables* t, hipStream_t stream) {
 // Few large blocks -> the split-and-combine path (split_*_kernel): uniform
 // blocks over kBurstMaxLen in a batch of at most kSplitMaxBlocks, or a batch of
 // at most kSplitMaxHinted blocks the caller marks HINT_LARGE_BLOCKS (the host
-// does not see variable lengths).  Read-verify carries no flags: it splits only
-// when tuning forces it.  tools/big_blocks.py measures both sides.
+// does not see variable lengths; read-verify takes the hint through
+// nova_sstable_verify_blocks_ex).  tools/big_blocks.py measures both sides.
 thread_local std::atomic<int> g_tune_split{0};  // 0 auto, 1 force, -1 off
 constexpr uint64_t kBurstMaxLen = 65536;
 constexpr uint64_t kSplitMaxBlocks = 8192, kSplitMaxHinted = 1024;
@@ -4333,7 +4333,6 @@ bool split_wanted(int mode, const CrcParams& p, bool uniform, uint64_t len) {
   if (mode != kStore && mode != kTrailer && mode != kVerify) return false;
   const int ts = g_tune_split.load();
   if (ts) return ts > 0;
-  if (mode == kVerify) return false;
   if (g_tune_g.load() || g_tune_seg.load() || g_tune_kernel.load() || g_tune_burst.load()) return false;
   if (p.n_blocks > kSplitMaxBlocks) return false;
   if (uniform) return len > kBurstMaxLen;
@@ -4666,9 +4665,9 @@ int nova_sstable_write_trailers(void* buf, const uint64_t* offsets, const uint32
   return run(kTrailer, p, false, 0, (hipStream_t)stream);
 }
 
-int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
-                               size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
-                               void* stream) {
+int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
+                                  size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
+                                  uint32_t flags, void* stream) {
   if (n_blocks && (!buf || !offsets || !sizes || !ok_out)) return NOVA_E_INVAL;
   CrcParams p{};
   p.base = (const uint8_t*)buf;
@@ -4677,7 +4676,14 @@ int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const u
   p.ok_out = ok_out;
   p.n_bad = n_bad_out;
   p.n_blocks = n_blocks;
+  p.flags = flags & NOVA_CRC32C_HINT_LARGE_BLOCKS;
   return run(kVerify, p, false, 0, (hipStream_t)stream);
+}
+
+int nova_sstable_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
+                               size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
+                               void* stream) {
+  return nova_sstable_verify_blocks_ex(buf, offsets, sizes, n_blocks, ok_out, n_bad_out, 0u, stream);
 }
 
 int nova_log_write_crcs(void* buf, size_t buf_len, const uint64_t* record_offsets,

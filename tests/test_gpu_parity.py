@@ -1085,6 +1085,9 @@ def test_large_blocks_hint_same_results(torch_gpu, oracle, mode):
             assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
             assert int(bad.item()) == len(victims)
         C.set_tuning(0, 0)
+        ok, bad = C.verify_blocks(buf, do, dl, hint_large=True)  # units kernel via the hint
+        assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
+        assert int(bad.item()) == len(victims)
 
 
 @pytest.mark.parametrize("n", [1, 5, 6144, 6145, 49152, 98303, 98304, 196608])
@@ -1319,8 +1322,9 @@ def test_split_few_large_blocks(torch_gpu, oracle, flags):
 def test_split_trailers_and_verify(torch_gpu, oracle, n):
     """Trailers (HINT_LARGE_BLOCKS, <= 1024 blocks: the split path) written
     byte-for-byte as table/table_builder.cc:202-206 with the quirk, nothing
-    else in the image touched; read-verify through the split path (forced:
-    verify carries no hint) flags exactly the corrupted blocks."""
+    else in the image touched; read-verify through the split path (the hint via
+    nova_sstable_verify_blocks_ex, and forced) flags exactly the corrupted
+    blocks."""
     torch = torch_gpu
     rng = np.random.default_rng(n)
     lens = rng.choice([3, 4096, 70000, 300000, 1 << 20], n).astype(np.uint32)
@@ -1344,6 +1348,9 @@ def test_split_trailers_and_verify(torch_gpu, oracle, n):
     victims = rng.choice(n, min(n, 3), replace=False)
     for v in victims:
         buf[int(offs[v]) + int(lens[v]) // 2] ^= 0x40
+    ok, bad = C.verify_blocks(buf, do, dl, hint_large=True)
+    assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
+    assert int(bad.item()) == len(victims)
     with C.diagnostics() as D:
         D.nova_diag_set_split(1)
         ok, bad = C.verify_blocks(buf, do, dl)

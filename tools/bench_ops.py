@@ -161,7 +161,7 @@ def main() -> int:
 
             def vf():
                 bad.zero_()
-                C.verify_blocks(buf, offs, lens, stream=stream, ok=okb, bad=bad)
+                C.verify_blocks(buf, offs, lens, stream=stream, ok=okb, bad=bad, hint_large=large)
             sec = timed(torch, vf, args.steps, args.warmup, stream)
             ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
             emit("verify", wl, sum_len + 6 * n, sec, ok, {"image": image})
