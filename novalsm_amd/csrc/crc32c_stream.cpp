@@ -289,18 +289,22 @@ int host_batch(HostOp op, const void* host_base, const uint64_t* offsets, const 
     if (e != hipSuccess) { rc = (int)e; break; }
     const uint64_t* doffs = static_cast<const uint64_t*>(s.offs.p);
     const uint32_t* dlens = static_cast<const uint32_t*>(s.lens.p);
+    // the host sees the lengths: a chunk of >= 16 KiB blocks on average gets the
+    // large-blocks hint (segments; a few big blocks: pieces over the device)
+    const uint32_t hint = (c.hi - c.lo) / m >= 16384 ? NOVA_CRC32C_HINT_LARGE_BLOCKS : 0u;
     if (op == kHostVerify) {
-      rc = nova_sstable_verify_blocks(s.data.p, doffs, dlens, m, static_cast<uint8_t*>(s.out.p),
-                                      nullptr, hs);
+      rc = nova_sstable_verify_blocks_ex(s.data.p, doffs, dlens, m, static_cast<uint8_t*>(s.out.p),
+                                         nullptr, hint, hs);
       if (!rc) rc = (int)hipMemcpyAsync(static_cast<uint8_t*>(pres.p) + c.b0, s.out.p, m,
                                         hipMemcpyDeviceToHost, hs);
     } else {
       // trailers: CRCs (type byte appended, masked) come back; the host writes
       // the 5 trailer bytes into its own image
-      const uint32_t f = op == kHostTrailers
-                             ? ((flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT |
-                                (flags & NOVA_CRC32C_HINT_LARGE_BLOCKS))
-                             : flags;
+      const uint32_t f = (op == kHostTrailers
+                              ? ((flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT |
+                                 (flags & NOVA_CRC32C_HINT_LARGE_BLOCKS))
+                              : flags) |
+                         hint;
       rc = nova_crc32c_batch(s.data.p, doffs, dlens,
                              init ? static_cast<const uint32_t*>(s.init.p) : nullptr,
                              static_cast<uint32_t*>(s.out.p), m, f, hs);
