@@ -38,6 +38,7 @@ def main():
             C.batch_strided(buf, Lb, Lb, n, out=out)
         torch.cuda.synchronize()
         a = st.cpu().numpy().reshape(-1, 3)
+        a = a[a[:, 0] != 0]  # rows of the waves the launch had (8 or 16 per workgroup)
         L.nova_diag_set_variant(0)
         C.set_tuning(0, 0)
         t0 = a[:, 0].min()
