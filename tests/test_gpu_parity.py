@@ -86,6 +86,26 @@ def test_golden_cases_device(torch_gpu, golden, lanes):
     assert bad.size == 0, [(cases[i], hex(got[i])) for i in bad[:5]]
 
 
+def test_golden_cases_split_path(torch_gpu, golden):
+    """The reference-generated golden cases (every misalignment 0..15, lengths
+    0..160 and edge lengths up to 64 KiB+63, random inits) through the
+    split-and-combine path (forced): 16 KiB pieces in 128 slots per block,
+    folded, then finished by the finish kernel."""
+    torch = torch_gpu
+    cases = golden["cases"]
+    buf, offs = pack_cases(cases)
+    lens = np.array([c["length"] for c in cases], np.uint32)
+    init = np.array([c["init"] for c in cases], np.uint32)
+    with C.diagnostics() as D:
+        D.nova_diag_set_split(1)
+        out = C.batch(dev(torch, buf), dev(torch, offs, torch.int64), dev(torch, lens, torch.int32),
+                      init=dev(torch, init.view(np.int32)))
+    got = u32(out)
+    want = np.array([c["crc"] for c in cases], np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(cases[i], hex(got[i])) for i in bad[:5]]
+
+
 def test_config1_fixture_strided(torch_gpu, golden):
     torch = torch_gpu
     c1 = golden["config1"]
@@ -1286,8 +1306,11 @@ def test_split_few_large_blocks(torch_gpu, oracle, flags):
     off (diagnostics) give the same words."""
     torch = torch_gpu
     rng = np.random.default_rng(314)
-    # fixed stride: 1 x (5 MiB + 13) at offset 3; 7 x (300 KiB + 5), stride + 11
-    for n, L, pad, base in ((1, (5 << 20) + 13, 0, 3), (7, (300 << 10) + 5, 11, 1)):
+    # fixed stride: 1 x (5 MiB + 13) at offset 3; 7 x (300 KiB + 5), stride + 11 (both
+    # > 64 piece slots per block: finish kernel); 2000 x (96 KiB + 16): 32 slots, the
+    # fold finishes each block itself
+    for n, L, pad, base in ((1, (5 << 20) + 13, 0, 3), (7, (300 << 10) + 5, 11, 1),
+                            (2000, (96 << 10) + 16, 0, 0)):
         stride = L + pad
         host = splitmix64_bytes(n + 40, base + n * stride + 16).copy()
         init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
@@ -1327,7 +1350,7 @@ def test_split_few_large_blocks(torch_gpu, oracle, flags):
     assert np.array_equal(u32(out), want)
 
 
-@pytest.mark.parametrize("n", [1, 3, 64, 1000])
+@pytest.mark.parametrize("n", [1, 3, 64, 1024])
 def test_split_trailers_and_verify(torch_gpu, oracle, n):
     """Trailers (HINT_LARGE_BLOCKS, <= 1024 blocks: the split path) written
     byte-for-byte as table/table_builder.cc:202-206 with the quirk, nothing
