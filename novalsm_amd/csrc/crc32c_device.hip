@@ -427,6 +427,40 @@ __device__ __forceinline__ uint4 lds_u128(uint32_t a) {
 }
 __device__ __forceinline__ int32_t clamp16(int32_t x) { return x < 0 ? 0 : (x > 16 ? 16 : x); }
 
+// v of lane (lane ^ K), K a power of two known at compile time.  Within a
+// 16-lane row without an LDS round trip (__shfl_xor is a ds_bpermute): DPP for
+// k <= 8 (quad_perm; xor 4 = row_half_mirror after quad_perm [3,2,1,0]; xor 8 =
+// row_mirror after row_half_mirror); 16 and 32 cross rows (ds_bpermute).
+template <int K>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+  if constexpr (K == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  } else if constexpr (K == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  } else if constexpr (K == 4) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false),
+                                              0x141, 0xF, 0xF, false);
+  } else if constexpr (K == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false),
+                                              0x140, 0xF, 0xF, false);
+  } else {
+    // 16, 32: ds_bpermute.  With the gfx950 permlane swaps here the burst
+    // kernel's trailer launch took 2.4 us longer at 16 blocks and one
+    // log-stream experiment case (diagnostics build) failed, so they are not used.
+    static_assert(K == 16 || K == 32, "lane_xor: 1, 2, 4, 8, 16 or 32");
+    return (uint32_t)__shfl_xor((int)v, K);
+  }
+}
+// max over the wave's 64 lanes (every lane gets it)
+__device__ __forceinline__ uint32_t wave_max(uint32_t m) {
+  m = max(m, lane_xor<32>(m));
+  m = max(m, lane_xor<16>(m));
+  m = max(m, lane_xor<8>(m));
+  m = max(m, lane_xor<4>(m));
+  m = max(m, lane_xor<2>(m));
+  return max(m, lane_xor<1>(m));
+}
+
 // Fold the 4G pending stream words of a lane group (4 per lane, lane q holds
 // the words at byte offsets 16q+0,4,8,12 of each 16G-byte swath) into the
 // pending word V of the group's last word: in-lane M4, M8, then cross-lane
@@ -435,14 +469,16 @@ template <int G>
 __device__ __forceinline__ uint32_t group_fold(const uint8_t* lds, uint32_t c0, uint32_t c1,
                                                uint32_t c2, uint32_t c3, int q) {
   uint32_t v = tapply(lds, 1, tapply(lds, 0, c0) ^ c1) ^ (tapply(lds, 0, c2) ^ c3);
-#pragma unroll
-  for (int k = 0; (1 << k) < G; ++k) {
-    const uint32_t o = __shfl_xor(v, 1 << k);
+  auto level = [&](int k, uint32_t o) {  // o: v of lane q ^ 2^k
     const bool right = (q >> k) & 1;
-    const uint32_t left_v = right ? o : v;
-    const uint32_t right_v = right ? v : o;
-    v = tapply(lds, 2 + k, left_v) ^ right_v;
-  }
+    v = tapply(lds, 2 + k, right ? o : v) ^ (right ? v : o);
+  };
+  if constexpr (G > 1) level(0, lane_xor<1>(v));
+  if constexpr (G > 2) level(1, lane_xor<2>(v));
+  if constexpr (G > 4) level(2, lane_xor<4>(v));
+  if constexpr (G > 8) level(3, lane_xor<8>(v));
+  if constexpr (G > 16) level(4, lane_xor<16>(v));
+  if constexpr (G > 32) level(5, lane_xor<32>(v));
   return v;
 }
 
@@ -1974,8 +2010,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       uint64_t S = (g_le - (a & ~(kLine - 1)) + kStep - 1) / kStep;
       if (S == 0) S = 1;
       uint32_t m = ok ? (uint32_t)S : 0u;
-#pragma unroll
-      for (int k = 32; k >= 1; k >>= 1) m = max(m, (uint32_t)__shfl_xor(m, k));
+      m = wave_max(m);
       r_S = m;
       if (r_S != 0) break;  // an empty round (past the batch's end): next one
     }
@@ -2445,11 +2480,8 @@ __global__ void __launch_bounds__(BurstCfg<V>::kWaves * 64) crc32c_burst_kernel(
     A0 = u0 & ~15ull;
     const uint64_t K = E > A0 ? (E - A0 + kS - 1) / kS : 0;
     uint64_t km = valid ? K : 0;  // the wave's largest block (groups end-aligned)
-#pragma unroll
-    for (int k = G; k < 64; k <<= 1) {
-      const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(km >> 32), k) << 32) |
-                         (uint32_t)__shfl_xor((int)(uint32_t)km, k);
-      km = o > km ? o : km;
+    if constexpr (G < 64) {  // per-block step counts fit 32 bits (a block is < 4 GiB)
+      km = wave_max((uint32_t)km);
     }
     Kw = km;
     first = E - Kw * kS + 16ull * q;
@@ -2515,12 +2547,16 @@ __global__ void __launch_bounds__(BurstCfg<V>::kWaves * 64) crc32c_burst_kernel(
     }
     // fold the group's stream words: in-lane M4/M8, then M16 .. across the group
     uint32_t v = lapply(tree + kTreeBytes, lapply(tree, c0) ^ c1) ^ (lapply(tree, c2) ^ c3);
-#pragma unroll
-    for (int k = 0; (1 << k) < G; ++k) {
-      const uint32_t o = __shfl_xor(v, 1 << k);
+    auto level = [&](int k, uint32_t o) {  // o: v of lane q ^ 2^k
       const bool right = (q >> k) & 1;
       v = lapply(tree + (2 + k) * kTreeBytes, right ? o : v) ^ (right ? v : o);
-    }
+    };
+    if constexpr (G > 1) level(0, lane_xor<1>(v));
+    if constexpr (G > 2) level(1, lane_xor<2>(v));
+    if constexpr (G > 4) level(2, lane_xor<4>(v));
+    if constexpr (G > 8) level(3, lane_xor<8>(v));
+    if constexpr (G > 16) level(4, lane_xor<16>(v));
+    if constexpr (G > 32) level(5, lane_xor<32>(v));
     uint64_t wb_a = 0;
     uint32_t wb_v = 0;
 #ifdef NOVA_DIAG
