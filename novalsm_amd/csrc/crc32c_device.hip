@@ -4065,7 +4065,10 @@ struct StreamScratch {
   hipStream_t s = nullptr;
   int alloc(size_t bytes, hipStream_t stream) {
     s = stream;
-    return hipMallocAsync(&p, bytes, stream) == hipSuccess ? 0 : NOVA_E_NOMEM;
+    if (hipMallocAsync(&p, bytes, stream) == hipSuccess) return 0;
+    p = nullptr;
+    (void)hipGetLastError();  // not sticky for the caller's next launch check
+    return NOVA_E_NOMEM;
   }
   ~StreamScratch() {
     if (p) (void)hipFreeAsync(p, s);
@@ -4445,8 +4448,11 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   DevTables* t = tables(&err);
   if (!t) return err;
   if (p.n_blocks == 0) return 0;
-  if (split_wanted(mode, p, uniform, bytes_per_block))
-    return launch_split(mode, p, uniform, bytes_per_block, t, stream);
+  if (split_wanted(mode, p, uniform, bytes_per_block)) {
+    // no scratch for the pieces (nothing launched yet): the one-pass kernels below
+    const int rc = launch_split(mode, p, uniform, bytes_per_block, t, stream);
+    if (rc != NOVA_E_NOMEM) return rc;
+  }
   if (const int bg = burst_lanes(mode, p.n_blocks, (uint32_t)t->cus)) {
     switch (mode) {
       case kStore: return launch_burst_g<kStore>(bg, p, t, stream);
