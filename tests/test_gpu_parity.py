@@ -787,6 +787,51 @@ def test_concurrent_host_threads(torch_gpu, oracle):
             assert np.array_equal(r, want)
 
 
+def test_concurrent_split_path(torch_gpu, oracle):
+    """The split-and-combine path from several host threads at once, each on its
+    own stream and on the shared default stream: every call owns its
+    stream-ordered scratch, so results never mix."""
+    torch = torch_gpu
+    import threading
+    n, length = 3, (3 << 20) + 5  # 3 blocks of 3 MiB: fixed stride > 64 KiB -> split
+    bufs = []
+    for t in range(4):
+        b = torch.empty(n * length, dtype=torch.uint8, device="cuda")
+        C.fill_splitmix64(b, 300 + t)
+        bufs.append(b)
+    torch.cuda.synchronize()
+    assert C.describe(n, length, length)["kernel"] == "split"
+    results = [None] * 8
+    errors = []
+
+    def work(i):
+        try:
+            t = i % 4
+            s = torch.cuda.Stream() if i < 4 else None
+            outs = []
+            for _ in range(6):
+                outs.append(C.batch_strided(bufs[t], length, length, n, stream=s))
+            if s is not None:
+                s.synchronize()
+            else:
+                torch.cuda.synchronize()
+            results[i] = [u32(o) for o in outs]
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    for i in range(8):
+        t = i % 4
+        want = oracle.batch_strided(bufs[t].cpu().numpy(), length, length, n)
+        for r in results[i]:
+            assert np.array_equal(r, want), i
+
+
 @pytest.mark.parametrize("kernel", ["default", "logstream"])
 def test_log_records_write_verify(torch_gpu, golden, oracle, kernel):
     """MANIFEST/WAL record CRCs (db/log_writer.cc:99-114,
