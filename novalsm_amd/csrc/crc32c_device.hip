@@ -110,8 +110,6 @@ struct CrcParams {
   // trailer; null or nonzero: byte stores
   const uint32_t* tr_flag;
   uint32_t wvar;  // diagnostics (timing): 1 = whole-piece stores non-temporal, 2 = no result writes
-                  // 4 = whole pieces into wpieces (128 B per block), copied by a second pass
-  uint8_t* wpieces;
 };
 
 // ---- log records: bounds and status (db/log_reader.cc:228-262) ------------
@@ -162,6 +160,7 @@ constexpr int kVarNarrow = 16;  // flat/rounds/units: one word's lookups in flig
 constexpr int kVarWide = 32;    // stream kernel: a swath's 16 lookups in flight (fold4w, A/B)
 [[maybe_unused]] constexpr int kVarLsFast = 64;  // log-stream kernel: every swath on the fast path (ablation: WRONG CRCs)
 constexpr int kVarInit = 128;   // rounds kernel, store mode: per-block init values (general head masking)
+[[maybe_unused]] constexpr int kVarNoTail = 256;  // rounds kernel ablation: no tail-line loads (WRONG CRCs)
 
 // 16-byte load through the global (not flat) address space.  Block bytes are
 // read exactly once, so production loads carry the nt policy: on gfx950 it
@@ -2084,7 +2083,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       X.d2 = gload16<VAR>((vz && w + 2 >= g_w0) ? pa + 32 * G : zl);
       X.d3 = gload16<VAR>((vz && w + 3 >= g_w0 && (!last || g_l3)) ? pa + 48 * G : zl);
       const bool vl = v && last;
-      if constexpr (kTail2) {
+      if constexpr ((VAR & kVarNoTail) != 0) {  // timing ablation (diagnostics)
+        X.t = make_uint4(0, 0, 0, 0);
+        if constexpr (kTail2) X.t2 = make_uint4(0, 0, 0, 0);
+      } else if constexpr (kTail2) {
         const uint64_t ta = vl ? g_end : zl;  // holds the stored CRC's first byte
         X.t = gload16<VAR>(ta);
         X.t2 = gload16<VAR>((vl && g_u1 + 4 > g_end + 16) ? g_end + 16 : ta);
@@ -2237,9 +2239,6 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
           const uint64_t tv = (uint64_t)((p.flags >> 8) & 0xffu) | ((uint64_t)m << 8);
           wb_a = (Y.u1 & ~63ull) + 16u * (uint32_t)q;
           wb_w = patch_trailer(piece, wb_a, Y.u1, tv);
-#ifdef NOVA_DIAG
-          if (p.wvar == 4) wb_a = (uint64_t)p.wpieces + 128ull * Y.rec + 16u * (uint32_t)q;
-#endif
         }
       }
       if constexpr (MODE == kLogWrite) {
@@ -2808,30 +2807,6 @@ __global__ void __launch_bounds__(256) trailer_rmw_kernel(uint8_t* base, const u
       }
     } else if (k == 0) {
       store_trailer(t, type, m, quirk);
-    }
-  }
-}
-
-// Whole-piece trailer form, second pass: the rounds kernel left block i's
-// patched window pieces at wpieces + 128 i (eligible blocks; the others stored
-// their bytes in place); copy them into the image after every read of it.
-__global__ void __launch_bounds__(256) trailer_piece_copy_kernel(uint8_t* base, const uint64_t* offsets,
-                                                                 uint64_t omask, const uint32_t* lengths,
-                                                                 uint64_t lmask, uint64_t stride,
-                                                                 uint32_t len, const uint8_t* wpieces,
-                                                                 const uint32_t* elig,
-                                                                 const uint32_t* flag, uint64_t n) {
-  const uint64_t nth = ((uint64_t)gridDim.x * blockDim.x) >> 3;
-  const uint32_t k = threadIdx.x & 7u;
-  if (*flag != 0) return;  // byte stores by the CRC kernel
-  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3; i < n; i += nth) {
-    if (!elig[i]) continue;
-    const uint64_t u1 = (uint64_t)(base + offsets[i & omask] + i * stride + lengths[i & lmask] + len);
-    const uint64_t s0 = u1 & ~63ull;
-    const uint32_t np = ((u1 + 4) & ~63ull) != s0 ? 8u : 4u;
-    if (k < np) {
-      const u32x4 w = *(const __attribute__((address_space(1))) u32x4*)(wpieces + 128 * i + 16 * k);
-      *(__attribute__((address_space(1))) u32x4*)(s0 + 16u * k) = w;
     }
   }
 }
@@ -4186,6 +4161,8 @@ int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_
     return launch_rounds_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
   if (MODE == kStore && g_tune_var.load() == kVarNarrow)
     return launch_rounds_g<kStore, kVarNarrow>(G, dim3(wgs), block, lds, stream, p);
+  if ((MODE == kVerify || MODE == kLogVerify) && g_tune_var.load() == kVarNoTail)
+    return launch_rounds_g<MODE, kVarNoTail>(G, dim3(wgs), block, lds, stream, p);
 #endif
   if (MODE == kStore && p.imask != 0)
     return launch_rounds_g<kStore, kVarInit>(G, dim3(wgs), block, lds, stream, p);
@@ -4489,18 +4466,14 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // writes; 6 = no result writes (timing ablations: 5 and 6 write nothing)
   const int tkn = g_tune_trailer_1pass.load();
   p.wvar = tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : tkn == 7 ? 3u : 0u;
-  const bool tk_piece = tkn == 3 || tkn == 4 || tkn == 5 || tkn == 9;
-  if (tkn == 9) p.wvar = 4;
+  const bool tk_piece = tkn == 3 || tkn == 4 || tkn == 5;
   if (pl.kernel == kRoundsK && mode == kTrailer && tk_piece && !small) {
     // whole-64-B-piece trailer stores where the layout allows it
     // (trailer_layout_kernel)
-    // (form 9: + the patched pieces, 128 B per block, copied by a second pass)
     StreamScratch sc;  // flag + eligibility, freed in stream order after the CRC kernel
-    const size_t eb = (sizeof(uint32_t) * (p.n_blocks + 1) + 127) & ~size_t(127);
-    if (sc.alloc(eb + (tkn == 9 ? 128 * p.n_blocks : 0), stream)) return NOVA_E_NOMEM;
+    if (sc.alloc(sizeof(uint32_t) * (p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
     uint32_t* flag = static_cast<uint32_t*>(sc.p);
     uint32_t* elig = flag + 1;
-    p.wpieces = static_cast<uint8_t*>(sc.p) + eb;
     hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return (int)e;
     uint64_t wgs = (p.n_blocks + 255) / 256;
@@ -4516,15 +4489,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     CrcParams q = p;
     q.tr_flag = flag;
     q.init = elig;  // trailer mode reads each block's eligibility in place of an init
-    const int e2 = launch_rounds<kTrailer>(G, q, t, stream, pl.chunk);
-    if (e2 || tkn != 9) return e2;
-    uint64_t wgs8 = (p.n_blocks * 8 + 255) / 256;
-    if (wgs8 > cap) wgs8 = cap;
-    hipLaunchKernelGGL(trailer_piece_copy_kernel, dim3(wgs8), dim3(256), 0, stream,
-                       const_cast<uint8_t*>(p.base), lo, p.offsets ? ~0ull : 0ull, ll,
-                       p.lengths ? ~0ull : 0ull, p.offsets ? 0ull : p.stride, p.lengths ? 0u : p.len,
-                       p.wpieces, elig, flag, p.n_blocks);
-    return (int)hipGetLastError();
+    return launch_rounds<kTrailer>(G, q, t, stream, pl.chunk);
   }
   if (pl.kernel == kRoundsK && mode == kLogWrite && tk_piece &&
       p.n_blocks >= kLogWindowMin && p.offsets) {

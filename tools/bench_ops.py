@@ -173,6 +173,15 @@ def main() -> int:
             gbs1 = (sum_len + 6 * n) / sec1 / 1e9
             print(json.dumps({"sweep": "verify_no_writes", "image": image, "GBps": round(gbs1, 1),
                               "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
+            with C.diagnostics() as D:  # timing ablation: no tail-line loads, no writes (vs verify_no_writes)
+                D.nova_diag_set_variant(256)
+                D.nova_diag_set_trailer_single_pass(6)
+                sec1 = timed(torch, vf, args.steps, args.warmup, stream)
+                D.nova_diag_set_trailer_single_pass(0)
+                D.nova_diag_set_variant(0)
+            gbs1 = (sum_len + 6 * n) / sec1 / 1e9
+            print(json.dumps({"sweep": "verify_no_tail_loads_no_writes", "image": image, "GBps": round(gbs1, 1),
+                              "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
         del buf
         torch.cuda.empty_cache()
 
@@ -223,6 +232,16 @@ def main() -> int:
             sec = timed(torch, lv, args.steps, args.warmup, stream)
             ok = int(bad.item()) == 0 and bool((okb.cpu().numpy() == C.LOG_OK).all())
             emit("log_verify", wl, sum_rec + n, sec, ok)
+            for var, name in ((0, "log_verify_no_writes"), (256, "log_verify_no_tail_loads_no_writes")):
+                with C.diagnostics() as D:  # timing ablations (no result writes; 256: WRONG CRCs)
+                    D.nova_diag_set_variant(var)
+                    D.nova_diag_set_trailer_single_pass(6)
+                    sec1 = timed(torch, lv, args.steps, args.warmup, stream)
+                    D.nova_diag_set_trailer_single_pass(0)
+                    D.nova_diag_set_variant(0)
+                gbs1 = (sum_rec + n) / sec1 / 1e9
+                print(json.dumps({"sweep": name, "GBps": round(gbs1, 1),
+                                  "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
             sweep("log_verify", lv, sum_rec + n)
         del buf
         torch.cuda.empty_cache()
