@@ -2087,9 +2087,13 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         X.t = make_uint4(0, 0, 0, 0);
         if constexpr (kTail2) X.t2 = make_uint4(0, 0, 0, 0);
       } else if constexpr (kTail2) {
+        // tail lines: default (cached) policy -- on every step but a block's
+        // last they all read the zero line, an L1 hit instead of an L2 request
+        // (read-verify +0.4 points, log write +0.4; the trailer writer, which
+        // stores into that line, -3: it keeps nt loads; profiles/r02_ab_tail_cached.log)
         const uint64_t ta = vl ? g_end : zl;  // holds the stored CRC's first byte
-        X.t = gload16<VAR>(ta);
-        X.t2 = gload16<VAR>((vl && g_u1 + 4 > g_end + 16) ? g_end + 16 : ta);
+        X.t = gload16<VAR | kVarCached>(ta);
+        X.t2 = gload16<VAR | kVarCached>((vl && g_u1 + 4 > g_end + 16) ? g_end + 16 : ta);
       } else {
         uint64_t ta = (vl && vz && (g_u1 & 15)) ? g_end : zl;
         if constexpr (MODE == kTrailer) {
@@ -2111,7 +2115,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
           if (w) ta = ((g_u0 - 6) & ~63ull) + 16 * q;
           X.wsec = w;
         }
-        X.t = gload16<VAR>(ta);
+        constexpr int kTailVar = (MODE == kTrailer || MODE == kStore) ? VAR : (VAR | kVarCached);
+        X.t = gload16<kTailVar>(ta);  // (policy: see the verify branch above)
       }
       X.head = vz && g_hneed && (r_step == g_hs || r_step == g_hs2);
       X.l3 = g_l3;  // (fold runs after the next round may have started)
