@@ -1,0 +1,26 @@
+#!/bin/bash
+# Same-box A/B of two builds of the libraries (one gpurun call): the working
+# tree's novalsm_amd/lib ("new") against a previous build copied into ab_old/
+# ("old", e.g. built from the parent commit), alternating new/old/new/old.
+# Runs the GPU tests on "new" first; each leg times the composite ops of
+# tools/bench_ops.py (OPS, default log_write,log_verify,trailers,verify on the
+# SSTable-like image) and appends them to gpurun_out/ab_ops.log.  Every step has
+# its own time limit and the script stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OPS=${OPS:-log_write,log_verify,trailers,verify}
+mkdir -p gpurun_out ab_new
+export TMPDIR=/tmp
+[ -f ab_old/libnova_crc32c.so ] || { echo "ab_old/ holds no build"; exit 1; }
+cp novalsm_amd/lib/libnova_crc32c.so novalsm_amd/lib/libnova_crc32c_diag.so ab_new/
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+  > gpurun_out/pytest_gpu.log 2>&1 || { tail -n 30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -n 2 gpurun_out/pytest_gpu.log
+for leg in new old new old; do
+  cp ab_$leg/libnova_crc32c.so ab_$leg/libnova_crc32c_diag.so novalsm_amd/lib/
+  echo "== $leg"
+  timeout -k 10 300 python -u tools/bench_ops.py --ops "$OPS" --images sst4k > gpurun_out/ops_$leg.log 2>&1 || exit 3
+  grep '"op"' gpurun_out/ops_$leg.log | sed "s/^/$leg /" >> gpurun_out/ab_ops.log
+done
+cp ab_new/libnova_crc32c.so ab_new/libnova_crc32c_diag.so novalsm_amd/lib/
+exit 0
