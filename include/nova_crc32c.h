@@ -91,7 +91,11 @@ uint32_t nova_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
  *     per calling thread), checksummed by the HIP kernels and folded on the
  *     host; ANY device failure (no device, allocation beyond
  *     NOVA_HOOK_MAX_STAGING, a HIP error) falls back to the host Extend.
- * `buf` is HOST memory.  nova_port_stats counts the three outcomes. */
+ * `buf` is HOST memory.  nova_port_stats counts the three outcomes.
+ * Per-thread device footprint: a thread keeps its staging (the call's size
+ * plus 1 B per KiB) between calls only while it is at most
+ * NOVA_HOOK_KEEP_STAGING (env, default 64 MiB); a larger call frees it when it
+ * returns.  nova_host_staging_release() frees the calling thread's staging. */
 uint32_t nova_port_accelerated_crc32c(uint32_t crc, const char* buf, size_t size);
 void nova_port_stats(uint64_t* host_calls, uint64_t* device_calls, uint64_t* fallback_calls);
 
@@ -143,8 +147,11 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
  * buf) points at a physical record header [LE32 masked crc][LE16 length][type]
  * (db/log_format.h:27-30) followed by `length` payload bytes.
  * Bounds, as log::Reader::ReadPhysicalRecord checks them (db/log_reader.cc:
- * 228-247): a record whose header or payload runs past its 32 KiB block (or
- * past buf_len) is never read.
+ * 196-247): a record whose header or payload runs past its 32 KiB block (or
+ * past buf_len) is never read.  A header that does not fit (fewer than 7
+ * bytes left) is the block's trailer, skipped silently (:198-203), or, in the
+ * file's last partial block or at/past buf_len, the end of the file (:204-211);
+ * only a PAYLOAD past a full block is a "bad record length" (:230-235).
  * Write: header crc = Mask(Extend(type_crc[type], payload, length)) --
  * db/log_writer.cc:99-114 (type_crc[t] = Value(&t, 1), :16-21), computed as
  * Value(header+6, 1+length).  Out-of-bounds records are skipped (nothing is
@@ -154,9 +161,10 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
  * corruption (CHECKSUM_MISMATCH, BAD_LENGTH). */
 #define NOVA_LOG_CHECKSUM_MISMATCH 0 /* :251-262 "checksum mismatch" */
 #define NOVA_LOG_OK 1                /* Unmask(stored) == Value(header+6, 1+length) */
-#define NOVA_LOG_BAD_LENGTH 2        /* :228-235 "bad record length" (not read) */
+#define NOVA_LOG_BAD_LENGTH 2        /* :228-235 "bad record length": payload past a full block (not read) */
 #define NOVA_LOG_ZERO_RECORD 3       /* :241-247 type 0, length 0: skipped, not reported */
-#define NOVA_LOG_TRUNCATED 4         /* :236-239 cut by the end of the file: EOF, not reported */
+#define NOVA_LOG_TRUNCATED 4         /* :204-211, :236-239 cut by the end of the file: EOF, not reported */
+#define NOVA_LOG_BLOCK_TRAILER 5     /* :198-203 < 7 bytes left in a full block: a trailer, skipped, not reported */
 int nova_log_write_crcs(void* buf, size_t buf_len, const uint64_t* record_offsets,
                         size_t n_records, void* stream);
 int nova_log_verify_records(const void* buf, size_t buf_len, const uint64_t* record_offsets,
@@ -204,7 +212,8 @@ int nova_sstable_verify_blocks_host(const void* host_buf, const uint64_t* offset
                                     const uint32_t* sizes, size_t n_blocks, uint8_t* ok_out,
                                     uint32_t* n_bad_out, size_t chunk_bytes, int n_streams);
 /* The three calls above keep the calling thread's device staging (n_streams x
- * the largest chunk) and pinned result buffer between calls; this frees them.
+ * the largest chunk) and pinned result buffer between calls; this frees them,
+ * and the port hook's staging of the calling thread.
  * chunk_bytes 0 sizes chunks to the image (about two per stream, 4-64 MiB). */
 void nova_host_staging_release(void);
 

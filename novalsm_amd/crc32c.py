@@ -100,6 +100,7 @@ LOG_OK = 1
 LOG_BAD_LENGTH = 2
 LOG_ZERO_RECORD = 3
 LOG_TRUNCATED = 4
+LOG_BLOCK_TRAILER = 5  # < 7 bytes left in a full block: skipped, not reported
 
 
 def lib_path() -> str:
@@ -375,8 +376,10 @@ def log_write_crcs(buf, record_offsets, stream=None, buf_len: Optional[int] = No
 
 def log_verify_records(buf, record_offsets, stream=None, ok=None, bad=None,
                        buf_len: Optional[int] = None):
-    """db/log_reader.cc:228-262 per record -> (status uint8 tensor of LOG_*,
-    n_bad int32 tensor[1] counting CHECKSUM_MISMATCH and BAD_LENGTH)."""
+    """db/log_reader.cc:196-262 per record -> (status uint8 tensor of LOG_*,
+    n_bad int32 tensor[1] counting CHECKSUM_MISMATCH and BAD_LENGTH; a header
+    in a full block's last 1-6 bytes is LOG_BLOCK_TRAILER, one at/past the end
+    of the file or cut by its last partial block LOG_TRUNCATED, neither counted)."""
     import torch
     _require_gpu()
     n = int(record_offsets.numel())

@@ -141,6 +141,15 @@ __device__ __forceinline__ uint32_t log_status(uint64_t o, uint32_t length, uint
 __device__ __forceinline__ bool log_header_fits(uint64_t o, uint64_t buf_len) {
   return o + 7 <= log_block_end(o, buf_len);
 }
+// Status of a record whose header does not fit (fewer than 7 bytes left,
+// :196-220): at or past the end of the file, or in its last partial block, the
+// read ends (EOF, :204-211); in a full block the bytes are the block's
+// trailer, skipped silently (:198-203).  Neither is reported.
+__device__ __forceinline__ uint32_t log_nohdr_status(uint64_t o, uint64_t buf_len) {
+  if (o >= buf_len) return NOVA_LOG_TRUNCATED;
+  const uint64_t be = log_block_end(o, buf_len);
+  return (be == buf_len && (buf_len % kLogBlock) != 0) ? NOVA_LOG_TRUNCATED : NOVA_LOG_BLOCK_TRAILER;
+}
 
 // ---- device helpers --------------------------------------------------------
 
@@ -725,7 +734,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
           lstat = log_status(o, length, MODE == kLogVerify ? h[6] : 1u, p.buf_len);
           n = lstat == NOVA_LOG_OK ? 1u + length : 0u;
         } else {
-          lstat = log_cut_status(o, p.buf_len);
+          lstat = log_nohdr_status(o, p.buf_len);
         }
         a += 6;  // CRC input starts at the type byte
       } else {
@@ -1466,7 +1475,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) 
       const uint32_t length = h4 | (h5 << 8);  // type byte + payload (db/log_format.h:27-30)
       const uint32_t ls = log_header_fits(o, p.buf_len)
                               ? log_status(o, length, MODE == kLogVerify ? h6 : 1u, p.buf_len)
-                              : log_cut_status(o, p.buf_len);
+                              : log_nohdr_status(o, p.buf_len);
       t_len = ls == NOVA_LOG_OK ? 1u + length : 0u;  // 0: not read, t_aux = status
       t_aux = ls == NOVA_LOG_OK ? (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)) : ls;
     } else {
@@ -1932,7 +1941,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       const uint32_t length = h4 | (h5 << 8);  // db/log_format.h:27-30
       const uint32_t ls = log_header_fits(o, p.buf_len)
                               ? log_status(o, length, MODE == kLogVerify ? h6 : 1u, p.buf_len)
-                              : log_cut_status(o, p.buf_len);
+                              : log_nohdr_status(o, p.buf_len);
       n_n = ls == NOVA_LOG_OK ? 1u + length : 0u;  // 0: not read, n_aux = status
       n_rec = t_rec;
       n_aux = ls == NOVA_LOG_OK ? (MODE == kLogWrite ? t_aux : (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)))
@@ -2999,7 +3008,7 @@ __global__ void __launch_bounds__(kLsWaves * 64) crc32c_logstream_kernel(CrcPara
       const uint32_t length = w1 & 0xffffu;
       const uint32_t st = fits ? log_status(o[m], length, kVerifyMode ? ((w1 >> 16) & 0xffu) : 1u,
                                             p.buf_len)
-                               : NOVA_LOG_BAD_LENGTH;
+                               : (valid ? log_nohdr_status(o[m], p.buf_len) : NOVA_LOG_TRUNCATED);
       const bool elig = st == NOVA_LOG_OK && 1u + length >= kLsMinN;
       const uint64_t hrel = o[m] - bk * kLogBlock;
       wd[m] = elig ? ((uint32_t)hrel + 7u + length) | ((1u + length) << 16) : 0u;
@@ -4382,6 +4391,11 @@ void split_shape(uint64_t n, bool uniform, uint64_t len_in, uint32_t* S, uint32_
   }
 }
 
+// launch_split's "nothing launched" return: its scratch (or the stream's
+// claim slot) could not be had before any kernel was queued, so the caller may
+// still run the one-pass kernels.  Every later failure is the caller's error.
+constexpr int kSplitNoScratch = -1000;
+
 int launch_split(int mode, CrcParams& p, bool uniform, uint64_t len, DevTables* t, hipStream_t stream) {
   const uint32_t extra = mode == kVerify ? 1u : 0u;
   uint32_t S = 0, kshift = 0;
@@ -4390,7 +4404,8 @@ int launch_split(int mode, CrcParams& p, bool uniform, uint64_t len, DevTables* 
   // [piece offsets u64][piece lengths u32][piece raws u32][per-block xor
   // word], freed in stream order after the last kernel
   StreamScratch sc;
-  if (sc.alloc(slots * 16 + p.n_blocks * 4, stream)) return NOVA_E_NOMEM;
+  if (sc.alloc(slots * 16 + p.n_blocks * 4, stream)) return kSplitNoScratch;
+  if (!sched_slot(t, stream)) return kSplitNoScratch;  // the pieces' launch needs it
   uint64_t* poff = static_cast<uint64_t*>(sc.p);
   uint32_t* plen = reinterpret_cast<uint32_t*>(poff + slots);
   uint32_t* praw = plen + slots;
@@ -4431,9 +4446,10 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   if (!t) return err;
   if (p.n_blocks == 0) return 0;
   if (split_wanted(mode, p, uniform, bytes_per_block)) {
-    // no scratch for the pieces (nothing launched yet): the one-pass kernels below
+    // no scratch for the pieces (nothing launched yet): the one-pass kernels
+    // below; any failure after the first launch is returned as is
     const int rc = launch_split(mode, p, uniform, bytes_per_block, t, stream);
-    if (rc != NOVA_E_NOMEM) return rc;
+    if (rc != kSplitNoScratch) return rc;
   }
   if (const int bg = burst_lanes(mode, p.n_blocks, (uint32_t)t->cus)) {
     switch (mode) {

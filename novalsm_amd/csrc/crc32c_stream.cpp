@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -164,20 +165,69 @@ struct Streams {
   }
 };
 
-// Registers pageable host memory for the duration of a call (no-op if pinned).
+// Registers pageable host memory for the duration of a call (no-op if the
+// caller pinned it).  Registrations are shared between concurrent calls and
+// reference-counted by range: a call whose range lies inside one
+// this library registered takes a reference to it, so the registering call's
+// end cannot unregister memory another call's DMA still reads; a call whose
+// range partly overlaps a live registration waits until that one is released
+// (hipHostRegister rejects overlapping ranges), then registers its own.
+struct RegEntry {
+  uintptr_t lo, hi;
+  int refs;
+};
+struct RegTable {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<RegEntry> live;
+};
+RegTable& reg_table() {
+  static RegTable* t = new RegTable;  // never destroyed (exit order)
+  return *t;
+}
+
 struct HostReg {
-  void* p = nullptr;
+  uintptr_t key = 0;  // lo of the entry this call holds a reference to (0: none)
   int reg(const void* base, size_t len) {
-    if (!len || is_pinned(base)) return 0;
+    if (!len) return 0;
+    const uintptr_t lo = (uintptr_t)base, hi = lo + len;
+    RegTable& t = reg_table();
+    std::unique_lock<std::mutex> lk(t.mu);
+    for (;;) {
+      bool overlap = false;
+      for (RegEntry& e : t.live) {
+        if (e.lo <= lo && hi <= e.hi) {  // inside a live registration: share it
+          e.refs++;
+          key = e.lo;
+          return 0;
+        }
+        overlap |= e.lo < hi && lo < e.hi;
+      }
+      if (!overlap) break;
+      t.cv.wait(lk);  // a partly overlapping registration is still in use
+    }
+    if (is_pinned(base) && is_pinned((const uint8_t*)base + len - 1)) return 0;  // caller-pinned
     if (hipHostRegister(const_cast<void*>(base), len, hipHostRegisterDefault) != hipSuccess) {
       (void)hipGetLastError();
       return NOVA_E_NOMEM;
     }
-    p = const_cast<void*>(base);
+    t.live.push_back({lo, hi, 1});
+    key = lo;
     return 0;
   }
   ~HostReg() {
-    if (p) (void)hipHostUnregister(p);
+    if (!key) return;
+    RegTable& t = reg_table();
+    std::lock_guard<std::mutex> lk(t.mu);
+    for (size_t i = 0; i < t.live.size(); i++) {
+      if (t.live[i].lo != key) continue;
+      if (--t.live[i].refs == 0) {
+        (void)hipHostUnregister(reinterpret_cast<void*>(key));
+        t.live.erase(t.live.begin() + (long)i);
+        t.cv.notify_all();
+      }
+      break;
+    }
   }
 };
 
@@ -359,6 +409,14 @@ size_t hook_max_staging() {
   return v;
 }
 
+// Staging a thread keeps between hook calls; a larger call's staging is freed
+// when the call ends, so many threads that occasionally Extend() a big buffer
+// do not each pin up to NOVA_HOOK_MAX_STAGING of HBM.
+size_t hook_keep_staging() {
+  static const size_t v = env_size("NOVA_HOOK_KEEP_STAGING", 64u << 20);
+  return v;
+}
+
 // Per-thread device state of the hook: one pooled stream, staging buffers.
 struct HookState {
   hipStream_t s = nullptr;
@@ -371,6 +429,10 @@ struct HookState {
     }
   }
 };
+HookState& hook_state() {
+  thread_local HookState hs;
+  return hs;
+}
 
 // Extend(crc, buf, size) on the GPU: the buffer is cut into 4 KiB sub-blocks
 // whose linear ("raw") CRCs the kernels compute; the host folds them with the
@@ -378,7 +440,7 @@ struct HookState {
 int device_extend(uint32_t crc, const char* buf, size_t size, uint32_t* out) {
   if (size > hook_max_staging()) return NOVA_E_NOMEM;
   if (nova_device_init() != 0) return NOVA_E_NODEV;
-  thread_local HookState hs;
+  HookState& hs = hook_state();
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
     (void)hipGetLastError();
@@ -408,6 +470,10 @@ int device_extend(uint32_t crc, const char* buf, size_t size, uint32_t* out) {
   if (!rc) rc = (int)hipMemcpyAsync(raw.data(), hs.dout.p, nsub * 4, hipMemcpyDeviceToHost, hs.s);
   const hipError_t se = hipStreamSynchronize(hs.s);
   if (!rc && se != hipSuccess) rc = (int)se;
+  if (hs.dbuf.n > hook_keep_staging()) {  // (the stream is idle: synchronized above)
+    hs.dbuf.reset();
+    hs.dout.reset();
+  }
   if (rc) {
     (void)hipGetLastError();
     return rc;
@@ -523,6 +589,10 @@ void nova_host_staging_release(void) {
   HostStaging& h = host_staging();
   h.stage.clear();
   h.pres.reset();
+  HookState& hs = hook_state();  // the port hook's staging too
+  if (hs.s) (void)hipStreamSynchronize(hs.s);
+  hs.dbuf.reset();
+  hs.dout.reset();
 }
 
 void nova_port_stats(uint64_t* host_calls, uint64_t* device_calls, uint64_t* fallback_calls) {

@@ -229,9 +229,13 @@ int oracle_log_verify(const uint8_t *rec) {
  * bytes that begins on a 32 KiB log-block boundary (db/log_format.h:27,
  * kBlockSize).  The reader holds the rest of the current block in buffer_
  * (a short read, i.e. the file's last partial block, sets eof_):
- *   - header or payload past the block (:197-221, :228-239): with eof_ the
- *     record was cut by the end of the file -> 4, reported as EOF, not as a
- *     corruption; otherwise "bad record length" -> 2;
+ *   - fewer than 7 bytes left for the header (:198-220): at or past the end
+ *     of the file, or in the last partial block (eof_), the read ends -> 4
+ *     (EOF, not reported); in a full block they are its trailer, skipped
+ *     silently -> 5;
+ *   - payload past the block (:228-239): with eof_ the record was cut by the
+ *     end of the file -> 4, reported as EOF, not as a corruption; otherwise
+ *     "bad record length" -> 2;
  *   - a kZeroType record of length 0 is skipped unreported (:241-247) -> 3;
  *   - else the CRC is checked (:249-262): 1 ok, 0 "checksum mismatch".
  * (The NOVA_LOG_* codes of include/nova_crc32c.h.) */
@@ -239,8 +243,10 @@ int oracle_log_check(const uint8_t *buf, uint64_t buf_len, uint64_t off) {
   const uint64_t kBlock = 32768, kHeader = 7;
   uint64_t end = (off / kBlock + 1) * kBlock;
   if (end > buf_len) end = buf_len;
-  const int cut = (end == buf_len && buf_len % kBlock != 0) ? 4 : 2;  /* eof_ : bad length */
-  if (off + kHeader > end) return cut;
+  const int eof = end == buf_len && buf_len % kBlock != 0;  /* the block is the short last read */
+  const int cut = eof ? 4 : 2;                                /* eof_ : bad length */
+  if (off >= buf_len) return 4;                               /* :204-211: no bytes left */
+  if (off + kHeader > end) return eof ? 4 : 5;                /* :204-211 : :198-203 trailer */
   const uint8_t *h = buf + off;
   uint32_t len = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
   if (off + kHeader + len > end) return cut;

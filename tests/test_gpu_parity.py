@@ -892,8 +892,12 @@ def test_log_record_bounds(torch_gpu, golden, oracle, kernel):
             host[o + 8] ^= 0x80  # payload / CRC mismatch (or a 1-byte record's crc field)
     want_img = host.copy()
     cut = host.size - 3  # the image ends inside the last record: EOF for it
-    # plus descriptors past the image: header not read
-    offs_x = np.concatenate([offs, np.array([cut - 2, cut + 100], np.uint64)])
+    # plus descriptors past the image (EOF) and in the last 1-6 bytes of the
+    # full block 0 (its trailer: skipped, not reported -- ADVICE r02)
+    from novalsm_amd.synth import LOG_BLOCK
+    assert cut > LOG_BLOCK
+    offs_x = np.concatenate([offs, np.array([cut - 2, cut + 100], np.uint64),
+                             np.array([LOG_BLOCK - k for k in range(1, 7)], np.uint64)])
     buf = dev(torch, np.concatenate([host, np.zeros(256, np.uint8)]))
     doffs = dev(torch, offs_x, torch.int64)
     ctx = C.diagnostics() if kernel != "default" else None
@@ -908,7 +912,15 @@ def test_log_record_bounds(torch_gpu, golden, oracle, kernel):
         want = oracle.log_check(host, offs_x, buf_len=cut)
         assert np.array_equal(st.cpu().numpy(), want)
         assert int(bad.item()) == int(((want == 0) | (want == 2)).sum())
-        assert {0, 1, 2, 3, 4} <= set(want.tolist())
+        assert {0, 1, 2, 3, 4, 5} <= set(want.tolist())
+        assert (want[-6:] == C.LOG_BLOCK_TRAILER).all()
+        # an image of whole blocks: past its end is EOF, a full block's last
+        # bytes are its trailer
+        st2, bad2 = C.log_verify_records(buf, doffs[-6:], buf_len=LOG_BLOCK)
+        assert (st2.cpu().numpy() == C.LOG_BLOCK_TRAILER).all() and int(bad2.item()) == 0
+        d3 = dev(torch, np.array([LOG_BLOCK, LOG_BLOCK + 5], np.uint64), torch.int64)
+        st3, bad3 = C.log_verify_records(buf, d3, buf_len=LOG_BLOCK)
+        assert (st3.cpu().numpy() == C.LOG_TRUNCATED).all() and int(bad3.item()) == 0
         # write: recompute every readable record; the rest are left untouched
         before = buf.cpu().numpy().copy()
         C.log_write_crcs(buf, doffs, buf_len=cut)

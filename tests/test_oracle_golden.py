@@ -187,6 +187,17 @@ def test_log_check_statuses(oracle, golden):
     room = LOG_BLOCK - oj - 7
     buf[oj + 4], buf[oj + 5] = (room + 1) & 0xFF, (room + 1) >> 8
     assert oracle.log_check(buf, offs[j:j + 1])[0] == 2
+    # fewer than 7 bytes left in a FULL block are its trailer,
+    # skipped silently (:198-203) -> 5, never "bad record length"; in the last
+    # partial block, or at/past the end of the file, the read ends (EOF) -> 4
+    assert buf.size > LOG_BLOCK
+    tail = np.array([LOG_BLOCK - k for k in range(1, 7)], np.uint64)
+    assert (oracle.log_check(buf, tail) == 5).all()
+    assert (oracle.log_check(buf, tail, buf_len=LOG_BLOCK) == 5).all()  # the final block is full
+    last = buf.size - buf.size % LOG_BLOCK
+    assert (oracle.log_check(buf, np.array([buf.size - 3, buf.size, buf.size + 9], np.uint64)) == 4).all()
+    past = np.array([LOG_BLOCK, LOG_BLOCK + 100, last + 1], np.uint64)
+    assert (oracle.log_check(buf, past, buf_len=LOG_BLOCK) == 4).all()
 
 
 def test_xor_parity_oracle():
