@@ -1,12 +1,15 @@
 """Build the in-tree native libraries for gfx950.
 
-Sources: novalsm_amd/csrc/{crc32c_device.hip, crc32c_stream.cpp, crc32c_host.cpp}.
+Sources: novalsm_amd/csrc/{crc32c_device.hip, crc32c_stream.cpp, crc32c_host.cpp}
+(+ crc32c_kernels.hpp, crc32c_internal.hpp) and, for the diagnostics library
+only, crc32c_diag.hip.
 Outputs (git-ignored, travel to the GPU box):
   novalsm_amd/lib/libnova_crc32c.so       the product: production kernels only
-  novalsm_amd/lib/libnova_crc32c_diag.so  the same sources with -DNOVA_DIAG: timing
-      ablations (some compute WRONG CRCs on purpose), the flat kernel, the sort
-      pre-pass, read-ceiling probes and the nova_diag_* knobs -- for tools/ and
-      the tuning-variant tests, never for callers
+  novalsm_amd/lib/libnova_crc32c_diag.so  the SAME product objects plus
+      crc32c_diag.o: timing ablations (some compute WRONG CRCs on purpose), the
+      flat kernel, the sort pre-pass, the log-stream experiment, read-ceiling
+      probes and the nova_diag_* knobs -- for tools/ and the tuning-variant
+      tests, never for callers
 hipcc cross-compiles gfx950 code objects without a GPU; the objects compile in
 parallel.
 """
@@ -26,7 +29,9 @@ DIAG_LIB = os.path.join(LIB_DIR, "libnova_crc32c_diag.so")
 ARCH = os.environ.get("NOVA_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["crc32c_device.hip", "crc32c_stream.cpp", "crc32c_host.cpp"]
-HEADERS = ["gf2_crc32c.hpp", os.path.join("..", "..", "include", "nova_crc32c.h"),
+DIAG_SOURCE = "crc32c_diag.hip"
+HEADERS = ["gf2_crc32c.hpp", "crc32c_kernels.hpp", "crc32c_internal.hpp",
+           os.path.join("..", "..", "include", "nova_crc32c.h"),
            os.path.join("..", "..", "include", "nova_crc32c.hpp")]
 
 
@@ -41,7 +46,8 @@ def _stale(lib: str) -> bool:
     if not os.path.exists(lib):
         return True
     t = os.path.getmtime(lib)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [__file__]
+    extra = [DIAG_SOURCE] if lib == DIAG_LIB else []
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS + extra] + [__file__]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
@@ -70,9 +76,9 @@ def build(force: bool = False, verbose: bool = False, extra: list[str] | None = 
         shared.append(obj)
     dev_obj = os.path.join(LIB_DIR, "crc32c_device.o")
     jobs[dev_obj] = _compile_cmd(cc, SOURCES[0], dev_obj, [], extra)
-    diag_obj = os.path.join(LIB_DIR, "crc32c_device_diag.o")
+    diag_obj = os.path.join(LIB_DIR, "crc32c_diag.o")
     if diag:
-        jobs[diag_obj] = _compile_cmd(cc, SOURCES[0], diag_obj, ["-DNOVA_DIAG"], extra)
+        jobs[diag_obj] = _compile_cmd(cc, DIAG_SOURCE, diag_obj, [], extra)
     procs = []
     for obj, cmd in jobs.items():
         if verbose:
@@ -81,7 +87,7 @@ def build(force: bool = False, verbose: bool = False, extra: list[str] | None = 
     failed = [cmd for cmd, p in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
-    links = [(LIB, [dev_obj] + shared)] + ([(DIAG_LIB, [diag_obj] + shared)] if diag else [])
+    links = [(LIB, [dev_obj] + shared)] + ([(DIAG_LIB, [dev_obj, diag_obj] + shared)] if diag else [])
     for lib, objs in links:
         tmp = lib + ".tmp"
         subprocess.run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +

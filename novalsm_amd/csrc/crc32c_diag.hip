@@ -1,0 +1,1661 @@
+// MI355X (gfx950) batched CRC-32C -- the diagnostics translation unit
+// (libnova_crc32c_diag.so only; never linked into libnova_crc32c.so):
+//   * experiment kernels measured slower than the product's and kept with
+//     their tests: the flat kernel, the whole-batch sort
+//     pre-pass (3.5a), the trailer / log CRC-field store forms (3.5b), the
+//     log-stream kernel (3.5e);
+//   * timing ablations that compute WRONG CRCs on purpose (no lookups, no
+//     tail loads, no writes, no epilogue) and per-wave s_memrealtime stamps,
+//     as instantiations of the product kernel templates (crc32c_kernels.hpp)
+//     with diagnostics VAR bits;
+//   * read-ceiling probes;
+//   * the nova_diag_* knobs.
+// The product's dispatcher reaches all of it through the hook table g_diag,
+// which this TU fills at load time.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "crc32c_kernels.hpp"
+#include "gf2_crc32c.hpp"
+
+namespace {
+using namespace nova_dev;
+
+// ---- crc32c_flat_kernel<G, MODE> -------------------------------------------
+// Variable-length batches (any alignment and length; per-block init; all
+// modes).  Every lane group walks its own sequence of WHOLE blocks, one
+// 4-swath step (64G bytes) at a time, and the wave streams all its groups'
+// steps as one flat sequence with the next step's loads in flight while the
+// current one folds -- across block boundaries, like the stream kernel.  The
+// groups of a wave change blocks independently, so a wave never waits for its
+// longest block (the units kernel's rounds did) and no block is split.
+//
+//   * Region of a block [u0,u1): its steps end at E = u1 & ~15 (16-B aligned)
+//     and start at E - S*64G <= u0 & ~15.  Pieces before u0 read as zero (a
+//     zero register ignores leading zeros; they are not loaded), ~init is
+//     xor-ed into the bytes [u0,u0+4).  After the group fold the register at E
+//     is M4(V); the 0..15 tail bytes [E,u1) (loaded with the last step) finish
+//     it with <= 3 word steps (M4 in LDS) and <= 3 byte steps (M1 in LDS).
+//   * Blocks reach the groups through per-wave chunks of C consecutive block
+//     descriptors held one per lane, in two banks (current and next).  The
+//     groups whose block ended take the next positions of the chunk sequence
+//     (ballot + popcount), reading the descriptor from its lane (bpermute).
+//     A bank is refilled as soon as it is used up, so its loads are at least
+//     one step old when first read and never drain the data prefetch.
+//   * Chunks are claimed like the units kernel's (per-workgroup counters,
+//     bounded stealing), one claim ahead, the claim issued from inline asm
+//     with EXEC = lane 0 and collected after >= one step of loads.
+//   * Log modes: descriptors are record headers; the refill loads the offsets,
+//     the next step loads the header bytes, the one after packs them.
+
+// Issue one 4-swath step of a block region for this lane (pieces before the
+// block's first line, or of an invalid group, read the zero line) plus, on the
+// block's last step, its tail line(s).
+//
+// kLines (rounds kernel): the step grid is aligned to 16G-byte lines, so each
+// swath of a group is one aligned 16G-byte line (an unaligned grid splits
+// every group-swath over two cache lines: measured 61.5% vs 71.5% of HBM peak
+// on 4 KiB blocks).  The region then ends at Le = roundup(E, 16G) >= E; the
+// last step's last swath holds the pieces at or after E, which read the zero
+// line here and leave their lane's registers unchanged in fold_step.
+template <int G, int VAR, bool kTail2, bool kLines = false>
+__device__ __forceinline__ void load_step(FlatSet& X, uint64_t lp, uint64_t u0, uint64_t u1,
+                                          uint64_t end, bool v, bool last, uint64_t zl, int q) {
+  const uint64_t A0 = u0 & ~15ull;
+  const bool nz = v && u1 > u0;
+  const uint64_t pa = lp + 16 * q;
+  const uint64_t a0 = pa, a1 = pa + 16 * G, a2 = pa + 32 * G, a3 = pa + 48 * G;
+  const bool in3 = !kLines || !last || a3 < end;
+  X.d0 = gload16<VAR>((nz && a0 >= A0) ? a0 : zl);
+  X.d1 = gload16<VAR>((nz && a1 >= A0) ? a1 : zl);
+  X.d2 = gload16<VAR>((nz && a2 >= A0) ? a2 : zl);
+  X.d3 = gload16<VAR>((nz && a3 >= A0 && in3) ? a3 : zl);
+  if constexpr (kTail2) {
+    const uint64_t ta = last ? end : zl;  // holds the stored CRC's first byte
+    X.t = gload16<VAR>(ta);
+    X.t2 = gload16<VAR>((last && u1 + 4 > end + 16) ? end + 16 : ta);
+  } else {
+    X.t = gload16<VAR>((last && nz && (u1 & 15)) ? end : zl);
+  }
+}
+
+// Mask the head piece(s) of a step (bytes before u0, ~init at u0) and run it
+// through the lane's four stream registers.  A piece needs it only if it holds
+// a byte of [u0, u0+4): pieces wholly before u0 were loaded from the zero line
+// (load_step) and are zero already.  No region piece holds a byte at or after
+// u1 (regions end at E = u1 & ~15; the tail bytes come from the tail line).
+template <int G, int VAR, bool kTail2, bool kLines = false>
+__device__ __forceinline__ void fold_step(const uint8_t* lds, const FlatSet& Y, int q, uint32_t& c0,
+                                          uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t lo0,
+                                          uint32_t lo1, uint32_t lo2, uint32_t lo3) {
+  const int32_t h = rel32(Y.u0, Y.pa + 16 * q, 48 * G + 16);
+  uint4 d0 = Y.d0, d1 = Y.d1, d2 = Y.d2, d3 = Y.d3;
+  if (is_head(h)) d0 = head_piece(d0, h, Y.ninit);
+  if (is_head(h - 16 * G)) d1 = head_piece(d1, h - 16 * G, Y.ninit);
+  if (is_head(h - 32 * G)) d2 = head_piece(d2, h - 32 * G, Y.ninit);
+  if (is_head(h - 48 * G)) d3 = head_piece(d3, h - 48 * G, Y.ninit);
+  if (kLines && Y.last) {  // wave-uniform: the region's last line may end past E
+    swath4<VAR>(lds, c0, c1, c2, c3, d0, lo0, lo1, lo2, lo3);
+    swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);
+    swath4<VAR>(lds, c0, c1, c2, c3, d2, lo0, lo1, lo2, lo3);
+    const uint32_t k0 = c0, k1 = c1, k2 = c2, k3 = c3;
+    swath4<VAR>(lds, c0, c1, c2, c3, d3, lo0, lo1, lo2, lo3);
+    if (Y.pa + 16 * q + 48 * G >= (Y.u1 & ~15ull)) {  // piece at or after E: not in the region
+      c0 = k0;
+      c1 = k1;
+      c2 = k2;
+      c3 = k3;
+    }
+  } else if constexpr ((VAR & kVarNarrow) != 0) {
+    fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+  } else {
+    fold4w<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
+  }
+  // the tail line(s) are used only on a block's last step: consume anyway, so
+  // the compiler resolves their loads here with an exact count
+  asm volatile("" ::"v"(Y.t.x), "v"(Y.t.y), "v"(Y.t.z), "v"(Y.t.w));
+  if constexpr (kTail2) asm volatile("" ::"v"(Y.t2.x), "v"(Y.t2.y), "v"(Y.t2.z), "v"(Y.t2.w));
+}
+
+
+// The flat kernel is measured slower than the rounds kernel on every workload
+// (DESIGN.md 3.5): diagnostics build only.
+template <int G, int MODE, int VAR = 0>
+__global__ void __launch_bounds__(kFlatThreads) crc32c_flat_kernel(CrcParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
+  constexpr uint32_t kByteTab = kMainBytes + kLevels * kTreeBytes;
+  constexpr bool kLog = MODE == kLogWrite || MODE == kLogVerify;
+  constexpr bool kTail2 = MODE == kVerify;  // stored CRC follows the CRC input
+  constexpr uint64_t kStep = 64 * G;
+  static_assert(kByteTab == kMainBytes + kLevels * kTreeBytes, "byte table follows the tree");
+  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, p.tab_byte, 64);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane & (G - 1);
+  const int grp = lane / G;
+  const uint32_t rep = (uint32_t)(lane & 31) << 2;
+  const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
+  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
+  const uint32_t extra = (MODE == kVerify) ? 1u : 0u;  // verify covers block + type byte
+  const uint64_t zl = (uint64_t)p.zline;
+  const uint64_t base = (uint64_t)p.base;
+  const uint32_t C = p.chunk;  // kGroups <= C <= 64
+  const uint32_t nwg = gridDim.x;
+  const uint32_t nwaves = blockDim.x >> 6;
+
+  // ---- chunk claims (wave-uniform) ------------------------------------------
+  // A compiler-visible atomic by lane 0.  (Issued from inline asm, as the
+  // stream kernel does, the compiler copied the result register before the
+  // atomic had returned.)  The claim for the next switch is issued in the
+  // loop body's second take and read at the next switch, a step or more later.
+  uint32_t victim = blockIdx.x, tried = 0, req = 0;
+  bool claim_due = false;  // the next switch's claim is still to be issued
+  auto claim = [&](uint32_t v) {
+    uint32_t r = 0;
+    if (lane == 0)
+      r = __hip_atomic_fetch_add(p.sched + v * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    req = r;
+  };
+  auto chunk_of = [&](uint32_t v, uint32_t idx) -> uint64_t {
+    const uint64_t c = ((uint64_t)idx + nwaves) * nwg + v;  // first nwaves chunks implicit
+    return c < p.n_chunks ? c : kNoChunk;
+  };
+  // The chunk of the claim in req (issued in the second take since the last
+  // switch, or just before in the prologue); steal if exhausted.
+  auto collect = [&]() -> uint64_t {
+    uint64_t c = chunk_of(victim, __builtin_amdgcn_readfirstlane(req));
+    while (c == kNoChunk && ++tried < p.steal_limit + 1) {
+      victim = (victim + 1) % nwg;
+      claim(victim);
+      c = chunk_of(victim, __builtin_amdgcn_readfirstlane(req));
+    }
+    return c;
+  };
+
+  // ---- descriptor banks (LDS): bank k, slot i = block chunk_k*C + i -------------
+  // A refill loads the chunk's descriptors into registers (t_*); the next take,
+  // at least one step later, writes them to the wave's LDS bank, so neither
+  // the write nor any read waits on fresh loads.  (Registers as banks made
+  // the compiler copy fresh load results between registers at once, which
+  // drained the data prefetch at every refill.)  Log modes: the next take
+  // loads the header bytes, the one after packs and writes them.
+  const uint32_t desc_base = kByteTab + 1024u + (uint32_t)wave * 2u * C * 16u;
+  auto desc_at = [&](uint32_t bank, uint32_t i) -> uint4* {
+    return reinterpret_cast<uint4*>(lds + desc_base + (bank * C + i) * 16u);
+  };
+  uint32_t t_olo = 0, t_ohi = 0, t_len = 0, t_aux = 0;      // descriptor words in flight
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0, h6 = 0;  // log: header bytes in flight
+  int pend = 0;            // 1: LDS write due (log: header loads due), 2: log pack + write due
+  uint32_t pend_bank = 0;
+  uint64_t ch0 = kNoChunk, ch1 = kNoChunk;  // chunk held by bank 0 / 1
+  const uint32_t my = (uint32_t)lane < C ? (uint32_t)lane : C - 1;
+  auto refill = [&](uint64_t chunk, uint32_t bank) {
+    uint64_t rec = (chunk == kNoChunk ? 0 : chunk * C) + my;
+    if (rec >= p.n_blocks) rec = p.n_blocks - 1;
+    const uint64_t o = p.offsets[rec & p.omask];
+    t_olo = (uint32_t)o;
+    t_ohi = (uint32_t)(o >> 32);
+    if constexpr (!kLog) {
+      t_len = p.lengths[rec & p.lmask];
+      t_aux = p.init[rec & p.imask];
+    }
+    if (bank) ch1 = chunk;
+    else ch0 = chunk;
+    pend = 1;
+    pend_bank = bank;
+  };
+  // The descriptor pipeline runs at fixed points of the two-step loop body, so
+  // every value in it has one producer and one consumer (no register copies,
+  // which would wait on the loads): refill in the first take, LDS write in
+  // the second (log: header loads in the second, pack + write in the next
+  // first).
+  auto step_pending = [&](bool first) {
+    if constexpr (kLog) {
+      const uint64_t o = ((uint64_t)t_ohi << 32) | t_olo;
+      if (pend == 1 && !first) {
+        const uint8_t* h = log_header_fits(o, p.buf_len) ? (const uint8_t*)(base + o) : p.zline;
+        h4 = h[4];
+        h5 = h[5];
+        if constexpr (MODE == kLogVerify) {
+          h0 = h[0];
+          h1 = h[1];
+          h2 = h[2];
+          h3 = h[3];
+          h6 = h[6];
+        }
+        pend = 2;
+        return;
+      }
+      if (pend != 2 || !first) return;
+      const uint32_t length = h4 | (h5 << 8);  // type byte + payload (db/log_format.h:27-30)
+      const uint32_t ls = log_header_fits(o, p.buf_len)
+                              ? log_status(o, length, MODE == kLogVerify ? h6 : 1u, p.buf_len)
+                              : log_nohdr_status(o, p.buf_len);
+      t_len = ls == NOVA_LOG_OK ? 1u + length : 0u;  // 0: not read, t_aux = status
+      t_aux = ls == NOVA_LOG_OK ? (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)) : ls;
+    } else {
+      if (pend != 1 || first) return;
+    }
+    if ((uint32_t)lane < C) *desc_at(pend_bank, lane) = make_uint4(t_olo, t_ohi, t_len, t_aux);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    pend = 0;
+  };
+  auto complete_pending = [&]() {  // out of order (drains); only when C is small
+    step_pending(false);
+    step_pending(true);
+  };
+
+  // ---- per-group block state (load side; group-uniform values) ---------------
+  uint64_t g_u0 = 0, g_u1 = 0, g_lp = 0, g_end = 0, g_rec = 0;
+  uint32_t g_ninit = 0, g_st = 0;
+  bool g_valid = false, g_need = true;
+  uint32_t pos = 0;     // next position in the current bank
+  uint32_t cb = 0;      // current bank
+  bool dry = false;     // no more chunks for this wave
+
+  // first: the loop body's first take (the only one that switches banks and
+  // refills; positions may run past the current bank into the other one
+  // meanwhile: C >= 2 groups keeps them below 2C).
+  // Values loaded in one take and used only conditionally later are consumed
+  // here unconditionally (an empty asm reading them), so the compiler
+  // resolves their loads at a fixed point with an exact count instead of
+  // waiting for all loads wherever its paths merge.
+  auto take = [&](bool first) {
+    if (first) {
+      asm volatile("" ::"v"(req));
+      if constexpr (kLog)
+        asm volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(h4), "v"(h5), "v"(h6));
+    } else {
+      asm volatile("" ::"v"(t_olo), "v"(t_ohi), "v"(t_len), "v"(t_aux));
+    }
+    step_pending(first);
+    if (!first && claim_due) {
+      claim(victim);
+      claim_due = false;
+    }
+    const uint64_t needm = __ballot(g_need && q == 0);
+    const uint32_t cnt = (uint32_t)__popcll(needm);
+    if (pend && pos + cnt > C) complete_pending();  // reads the refilled bank (small C only)
+    const uint32_t rank = (uint32_t)__popcll(needm & ((1ull << (grp * G)) - 1));
+    const uint32_t s = pos + rank;
+    const bool oth = s >= C;  // past the current bank: the other one
+    const uint32_t idx = oth ? s - C : s;
+    const uint32_t bank = oth ? cb ^ 1u : cb;
+    if (g_need) {  // (no group needing a block: only the switch check below)
+      const uint4 d = *desc_at(bank, idx);
+      const uint64_t cid = bank ? ch1 : ch0;
+      const uint64_t rec = cid * C + idx;
+      const bool ok = cid != kNoChunk && rec < p.n_blocks;
+      uint64_t a = base + (((uint64_t)d.y << 32) | d.x) + rec * p.stride;
+      if (kLog) a += 6;  // CRC input starts at the type byte (db/log_writer.cc:112)
+      const uint32_t n = d.z + p.len + extra;
+      const uint32_t aux = d.w;
+      g_valid = ok;
+      g_need = false;
+      g_u0 = a;
+      g_u1 = a + n;
+      g_rec = rec;
+      // ~init goes into the data's first 4 bytes; a block shorter than 4 bytes
+      // gets it at the end instead (R ^= M_n(~init), see fold).
+      g_ninit = (raw || n < 4) ? 0u : ~((kLog || MODE == kTrailer) ? 0u : aux);  // log records: Value(), init 0
+      g_st = aux;
+      const uint64_t E = g_u1 & ~15ull;
+      const uint64_t A0 = a & ~15ull;
+      uint64_t S = (E - A0 + kStep - 1) / kStep;
+      if (S == 0) S = 1;
+      g_end = E;
+      g_lp = E - S * kStep;
+    }
+    pos += cnt;
+    // Checked in every first take, even with no block taken: the second take
+    // may then run past the current bank by < 1 group count, never past the
+    // other one (positions < C + 2 * groups <= 2C).
+    if (first && pos >= C) {  // the current bank is used up: switch, refill it
+      pos -= C;
+      cb ^= 1u;
+      uint64_t nc = kNoChunk;
+      if (!dry) {
+        nc = collect();
+        if (nc == kNoChunk) dry = true;
+        else claim_due = true;
+      }
+      refill(nc, cb ^ 1u);
+    }
+  };
+
+  auto issue = [&](FlatSet& X) -> bool {
+    const bool v = g_valid;
+    const bool last = v && (g_lp + kStep == g_end);
+    load_step<G, VAR, kTail2>(X, g_lp, g_u0, g_u1, g_end, v, last, zl, q);
+    X.pa = g_lp;
+    X.u0 = g_u0;
+    X.u1 = g_u1;
+    X.rec = g_rec;
+    X.ninit = v ? g_ninit : 0u;
+    X.st = g_st;
+    X.valid = v;
+    X.last = last;
+    if (v) g_lp += kStep;
+    if (last) g_need = true;
+    return __ballot(v) != 0;
+  };
+
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  bool wb_on = false;  // a finished block's write is pending (lane q == 0)
+  uint64_t wb_a = 0;
+  uint32_t wb_v = 0;
+  auto fold = [&](FlatSet& Y) {
+    fold_step<G, VAR, kTail2>(lds, Y, q, c0, c1, c2, c3, lo0, lo1, lo2, lo3);
+    if (Y.last) {  // group-uniform
+      const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
+      c0 = c1 = c2 = c3 = 0;
+      // The memory write waits until after the next step's loads are issued
+      // (writeback): a store here would make the compiler drain the prefetch
+      // before the store's address registers are reused.
+      finish_block<MODE>(lds, kByteTab, p, raw, v, Y, wb_a, wb_v);
+      wb_on = q == 0;
+    }
+  };
+  auto writeback = [&]() {
+    if (wb_on) {
+      write_result<MODE>(p, wb_a, wb_v);
+      wb_on = false;
+    }
+  };
+
+  // ---- prologue: wave k's first chunk is implicit, the second is claimed ------
+  {
+    uint64_t c0 = (uint64_t)wave * nwg + blockIdx.x;
+    if (c0 >= p.n_chunks) {
+      claim(victim);
+      c0 = collect();
+    }
+    if (c0 == kNoChunk) dry = true;
+    refill(c0, 0);
+    complete_pending();
+    uint64_t c1 = kNoChunk;
+    if (!dry) {
+      claim(victim);
+      c1 = collect();
+      if (c1 == kNoChunk) dry = true;
+      else claim_due = true;
+    }
+    refill(c1, 1);
+    complete_pending();
+  }
+  // The loop starts by folding an empty set A (zeros, not valid): no data
+  // load is in flight when the loop is entered, so the compiler's wait
+  // counts at the loop head follow the steady state (an A issued before the
+  // loop made it wait for everything there, every iteration).
+  FlatSet A, B;
+  A.d0 = A.d1 = A.d2 = A.d3 = A.t = A.t2 = make_uint4(0, 0, 0, 0);
+  A.pa = A.u0 = A.u1 = A.rec = 0;
+  A.ninit = A.st = 0;
+  A.valid = A.last = A.head = A.l3 = A.wsec = false;
+  for (;;) {
+    take(true);
+    issue(B);
+    writeback();
+    fold(A);
+    // No exit here: a mid-body exit makes the CFG structurizer add a path
+    // that enters the loop head with B's loads outstanding, and the head then
+    // waits for all loads every iteration.  A B without valid groups costs
+    // one more (empty) half.
+    take(false);
+    const bool a_live = issue(A);
+    writeback();
+    fold(B);
+    if (!a_live) break;
+  }
+  writeback();
+  // The last claim (if any) must have returned before this workgroup counts
+  // itself finished: the last workgroup then zeroes the counters.
+  __builtin_amdgcn_s_waitcnt(0);
+  sched_release(p.sched);
+}
+
+// The whole-batch sort was measured slower than sorting each claimed chunk
+// (DESIGN.md 3.5a): diagnostics build only.
+constexpr int kBins = 256;
+
+__device__ __forceinline__ uint32_t steps_class(uint64_t S) {
+  if (S < 128) return (uint32_t)S;
+  const uint32_t lg = 63u - (uint32_t)__builtin_clzll(S);  // >= 7
+  const uint32_t c = 128u + (lg - 7u) * 16u + (uint32_t)((S >> (lg - 4)) & 15u);
+  return c > 255u ? 255u : c;
+}
+
+// Step count of block b (region [A0, E) in kStep-byte steps), as the rounds
+// kernel computes it; rank = 255 - class orders the largest first.
+template <int MODE>
+__device__ __forceinline__ uint32_t block_rank(const CrcParams& p, uint64_t b, uint64_t kStep) {
+  constexpr bool kLog = MODE == kLogWrite || MODE == kLogVerify;
+  uint64_t a = (uint64_t)p.base + p.offsets[b & p.omask] + b * p.stride;
+  uint32_t n;
+  if constexpr (kLog) {
+    const uint8_t* h = (const uint8_t*)a;
+    n = 1u + ((uint32_t)h[4] | ((uint32_t)h[5] << 8));
+    a += 6;
+  } else {
+    n = p.lengths[b & p.lmask] + p.len + (MODE == kVerify ? 1u : 0u);
+  }
+  const uint64_t E = (a + n) & ~15ull, A0 = a & ~15ull;
+  uint64_t S = (E - A0 + kStep - 1) / kStep;
+  if (S == 0) S = 1;
+  return 255u - steps_class(S);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) bin_count_kernel(CrcParams p, uint64_t kStep, uint32_t* hist) {
+  __shared__ uint32_t h[kBins];
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < p.n_blocks; b += nth)
+    atomicAdd(&h[block_rank<MODE>(p, b, kStep)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// hist -> cursor: exclusive prefix over the ranks (one workgroup of kBins threads).
+__global__ void __launch_bounds__(kBins) bin_scan_kernel(const uint32_t* hist, uint32_t* cursor) {
+  __shared__ uint32_t t[kBins];
+  const int i = threadIdx.x;
+  t[i] = hist[i];
+  __syncthreads();
+  for (int d = 1; d < kBins; d <<= 1) {
+    const uint32_t v = i >= d ? t[i - d] : 0u;
+    __syncthreads();
+    t[i] += v;
+    __syncthreads();
+  }
+  cursor[i] = t[i] - hist[i];
+}
+
+// Same grid-stride assignment as bin_count_kernel: each workgroup reserves its
+// ranges per class with one atomic, then places its blocks.
+template <int MODE>
+__global__ void __launch_bounds__(256) bin_scatter_kernel(CrcParams p, uint64_t kStep, uint32_t* cursor,
+                                                          uint32_t* perm) {
+  __shared__ uint32_t h[kBins];
+  __shared__ uint32_t base[kBins];
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < p.n_blocks; b += nth)
+    atomicAdd(&h[block_rank<MODE>(p, b, kStep)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) {
+    base[i] = h[i] ? atomicAdd(&cursor[i], h[i]) : 0u;
+    h[i] = 0;
+  }
+  __syncthreads();
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < p.n_blocks; b += nth) {
+    const uint32_t r = block_rank<MODE>(p, b, kStep);
+    perm[base[r] + atomicAdd(&h[r], 1u)] = (uint32_t)b;
+  }
+}
+
+// Trailer writer, second pass: crc[i] = Mask(Extend(Value(block i), type))
+// from the first pass (the rounds kernel in store mode); write the 5-byte
+// trailer [type][LE32] at base + offsets[i] + sizes[i], with '!' over its last
+// byte for TableBuilder's ordering (table/table_builder.cc:202-206,
+// ltc/stoc_file_client_impl.cpp:713-719).  Inside the streaming kernel the
+// trailer stores per block cost ~12 points of HBM throughput.
+// Store-form experiments for the trailer writer and log CRC fields (DESIGN.md
+// 3.5b): measured, not faster than the CRC kernel's own byte stores.
+
+// Trailer writer pre-pass.  HBM writes whole 64-B pieces; a store that
+// covers only part of one (a 5-B trailer) costs a read-modify-write at the
+// memory, so the rounds kernel rewrites the whole aligned
+// 64-B piece(s) holding a trailer -- its "window", one piece or two when the
+// trailer crosses a piece boundary -- patched with the trailer bytes.  The
+// window's other bytes are stored back unchanged, which is safe when no other
+// block's trailer lies in it: then nobody else writes those bytes (block data
+// is only read) and no two windows share a piece (every window piece holds a
+// byte of its own trailer).
+//   *flag |= 1 unless the blocks are ascending and disjoint, trailer
+//   included (offset[i+1] >= offset[i] + size[i] + 5): then only the
+//   neighbours' trailers can reach a window, and
+//   elig[i] = 1 iff block i's window holds neither neighbour's trailer, lies
+//   above the first block's start (i == 0) and is not the last block's (its
+//   window may run past the image).  Window bytes outside every block (gaps)
+//   lie between two blocks of the image, so inside the caller's allocation.
+//   Windows are aligned in absolute addresses (ba = the image base), as the
+//   kernels that store them see them.
+__global__ void __launch_bounds__(256) trailer_layout_kernel(uint64_t ba, const uint64_t* offsets,
+                                                             uint64_t omask, const uint32_t* lengths,
+                                                             uint64_t lmask, uint64_t stride,
+                                                             uint32_t len, uint64_t n, uint32_t* elig,
+                                                             uint32_t* flag) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  auto u0_of = [&](uint64_t i) { return ba + offsets[i & omask] + i * stride; };
+  auto u1_of = [&](uint64_t i) { return u0_of(i) + lengths[i & lmask] + len; };
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
+    const uint64_t u0 = u0_of(i), u1 = u1_of(i);
+    const uint64_t ws = u1 & ~63ull, we = ((u1 + 4) & ~63ull) + 64;
+    bool e = i + 1 < n;
+    if (i + 1 < n) {
+      bad = bad || u0_of(i + 1) < u1 + 5;
+      e = e && u1_of(i + 1) >= we;
+    }
+    e = e && (i == 0 ? ws >= u0 : u1_of(i - 1) + 5 <= ws);
+    elig[i] = e ? 1u : 0u;
+  }
+  if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+// Log write pre-pass (same reasoning as trailer_layout_kernel): the rounds
+// kernel rewrites the whole 64-B piece holding a record's 4-byte CRC field
+// [o, o+4) (db/log_writer.cc:113) instead of storing 4 bytes into it.
+//   *flag |= 1 unless the record offsets are non-decreasing (then only the
+//   neighbours' CRC fields can reach a piece);
+//   elig[i] = 1 iff the field lies in one piece, the piece lies inside the
+//   image (buf_len) and holds neither neighbour's CRC field.  Every other byte
+//   of the piece (payloads, length and type bytes, block padding) is only read
+//   and is stored back unchanged.
+__global__ void __launch_bounds__(256) log_window_kernel(const uint64_t* offs, uint64_t n,
+                                                         uint64_t buf_len, uint32_t* elig,
+                                                         uint32_t* flag) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
+    const uint64_t o = offs[i], ws = o & ~63ull;
+    bool e = (o & 63) <= 60 && ws + 64 <= buf_len;
+    if (i + 1 < n) {
+      const uint64_t on = offs[i + 1];
+      bad = bad || on < o;
+      e = e && on >= ws + 64;
+    }
+    if (i > 0) e = e && offs[i - 1] + 4 <= ws;
+    elig[i] = e ? 1u : 0u;
+  }
+  if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+// Two-pass trailer writer with whole-piece stores, second pass: the CRC pass
+// left crc[i] = Mask(crc) (type appended); block i's trailer [u1, u1+5) is
+// patched into the aligned 64-B piece(s) holding it, which are read and
+// stored whole when trailer_layout_kernel found them private to the block
+// (*flag == 0, elig[i]); other blocks store their five bytes.  Eight lanes per
+// block: lane k owns the piece line s0 + 16k (k < 4, or < 8 when the trailer
+// crosses a piece).  The stores run after every read of the image, in their
+// own launch.
+__global__ void __launch_bounds__(256) trailer_rmw_kernel(uint8_t* base, const uint64_t* offsets,
+                                                          uint64_t omask, const uint32_t* lengths,
+                                                          uint64_t lmask, uint64_t stride, uint32_t len,
+                                                          const uint32_t* crc, const uint32_t* elig,
+                                                          const uint32_t* flag, uint64_t n,
+                                                          uint32_t flags) {
+  const uint64_t nth = ((uint64_t)gridDim.x * blockDim.x) >> 3;
+  const uint32_t k = threadIdx.x & 7u;
+  const bool layout_ok = *flag == 0;
+  const bool quirk = (flags & NOVA_TRAILER_TB_QUIRK) != 0;
+  const uint32_t type = (flags >> 8) & 0xffu;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3; i < n; i += nth) {
+    uint8_t* t = base + offsets[i & omask] + i * stride + lengths[i & lmask] + len;
+    const uint32_t m = crc[i];
+    if (layout_ok && elig[i]) {
+      const uint64_t u1 = (uint64_t)t, s0 = u1 & ~63ull;
+      const uint32_t np = ((u1 + 4) & ~63ull) != s0 ? 8u : 4u;
+      if (k < np) {
+        const uint32_t mq = quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m;
+        const uint64_t tv = (uint64_t)type | ((uint64_t)mq << 8);
+        const uint64_t a = s0 + 16u * k;
+        auto* pa = (__attribute__((address_space(1))) u32x4*)a;
+        u32x4 w = *pa;
+        const uint4 d = patch_trailer(make_uint4(w.x, w.y, w.z, w.w), a, u1, tv);
+        w.x = d.x;
+        w.y = d.y;
+        w.z = d.z;
+        w.w = d.w;
+        *pa = w;
+      }
+    } else if (k == 0) {
+      store_trailer(t, type, m, quirk);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) trailer_scatter_kernel(uint8_t* base, const uint64_t* offsets,
+                                                              const uint32_t* sizes,
+                                                              const uint32_t* crc, uint64_t n,
+                                                              uint32_t flags) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
+    store_trailer(base + offsets[i] + sizes[i], (flags >> 8) & 0xffu, crc[i],
+                  (flags & NOVA_TRAILER_TB_QUIRK) != 0);
+  }
+}
+
+
+// ---- crc32c_logstream_kernel<MODE>: a whole log image, record CRCs ----------
+// MANIFEST / write-ahead-log record CRCs for a log image
+// whose record offsets are in file order.  Each lane group of 8 lanes streams
+// one 32 KiB log block (db/log_format.h:27, kBlockSize) with the stream
+// kernel's uniform schedule -- 4-swath steps of one 128-B line per swath,
+// identical for every group of the wave, no per-record regions and no round
+// padding -- and resolves the block's records on the fly:
+//
+//   * A record's CRC input is [a, b) = [header+6, header+7+length) (type byte +
+//     payload, db/log_writer.cc:99-114).  The group's four stream registers per
+//     lane hold the CURRENT record only.  A swath holding a, a byte of the init
+//     window [a, a+4), or b takes the slow path: each lane masks its 16-B piece
+//     to [a, b) with two 16-B prefix masks from LDS and xors ~0 into [a, a+4)
+//     (Extend's init, as the units kernel); a record that starts in the swath
+//     starts from zero.  Between records (headers, block trailers, records
+//     left to the follow-up) the registers run on unmasked data: the next
+//     record's first swath resets them.
+//   * Only records of >= kLsMinN CRC bytes are streamed, so a group meets at
+//     most one record end and one record start per 128-B swath and the slow
+//     path is straight-line code (no loop, no global memory access -- either
+//     would make the compiler drain the step's prefetch).  Shorter records,
+//     records the reader would not read (bounds / zero records: status only)
+//     and whole blocks of more than 64 records go to a leftover list that the
+//     gated rounds kernel processes right after (crc32c_rounds_kernel, gate).
+//   * At b the group spills its 32 stream words to a per-wave LDS slot
+//     ("snapshot").  Streams whose word of the last swath lies entirely at or
+//     after b keep their value from the swath before (the rounds kernel's
+//     rotation), so the snapshot is a virtual 128-B message ending at the
+//     4-byte word holding b-1: pad = 0..3 bytes.
+//   * Snapshots are folded after the swath once a wave holds kLsFlush of them
+//     (the fold phase): four lanes per record run one Horner chain each (M16
+//     over every 4th word), a 3-step merge (M4) gives the pending word V,
+//     register = M4(V), and `pad` inverse zero-byte steps (bitwise) give the
+//     register at b.  Write: Mask(crc) into the header; verify: compare with
+//     the stored CRC (one status byte per record, mismatches counted).
+//   * Descriptors: a 64-record window per group (8 per lane), decoded at the
+//     start of each block from the offsets and the 7-byte record headers.
+//   * Preconditions (else the follow-up reruns the whole batch): offsets
+//     ascending (pre-pass, flag bit 0) and no streamed record starting before
+//     the previous one ended (flag bit 1).
+// Fast swaths cost what the stream kernel's do; the per-record work runs
+// wave-wide on the swaths that hold a record boundary.
+constexpr int kLsG = 8;                      // lanes per group (one 128-B line per swath)
+constexpr int kLsWaves = 8;                  // waves per workgroup
+constexpr uint32_t kLsSlots = 16;            // snapshot slots per wave
+constexpr uint32_t kLsFlush = kLsSlots - 8;  // fold after a swath leaving this many (<= 8 per swath)
+constexpr uint32_t kLsSlotBytes = 144;       // 32 stream words + 16 B of meta (bank spread)
+constexpr uint32_t kLsM4 = kMainBytes;       // LDS: M4 byte tables (4 KiB)
+constexpr uint32_t kLsM16 = kMainBytes + 4096;
+constexpr uint32_t kLsLM = kMainBytes + 8192;  // 17 x 16-B prefix masks: LM[n] = bytes [0, n)
+constexpr uint32_t kLsTabBytes = 8192 + 17 * 16;
+constexpr uint32_t kLsSlot0 = kMainBytes + kLsTabBytes;
+constexpr uint32_t kLsLds = kLsSlot0 + kLsWaves * kLsSlots * kLsSlotBytes;
+static_assert(kLsLds <= 160 * 1024, "log-stream LDS exceeds the CU");
+static_assert(kLsSlot0 % 16 == 0, "slots are 16-B aligned");
+constexpr int kLsWin = 8;                    // decoded descriptors per lane (64 per group)
+constexpr uint32_t kLsMinN = 128;            // CRC bytes of a streamed record (>= one swath)
+constexpr int32_t kLsFar = 1 << 28;          // "no record": past every swath
+
+
+typedef __attribute__((address_space(1))) const u32_unaligned gcu32u;
+
+// Pre-pass: first[k] = first record of log block k (record i belongs to block
+// min(off_i / 32 KiB, nb - 1): a record past the image lands in the last block,
+// whose status logic rejects it), first[nb] = n.  Unsorted offsets set bit 0
+// of *flag (the log-stream kernel then leaves the batch to the follow-up).
+__global__ void __launch_bounds__(256) log_first_kernel(const uint64_t* __restrict__ offs, uint64_t n,
+                                                        uint64_t nb, uint32_t* __restrict__ first,
+                                                        uint32_t* flag) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += nth) {
+    const uint64_t o = i < n ? offs[i] : 0;
+    const uint64_t k = i < n ? ((o >> 15) < nb - 1 ? (o >> 15) : nb - 1) : nb;
+    uint64_t k_lo = 0;
+    if (i > 0) {
+      const uint64_t op = offs[i - 1];
+      if (i < n && o < op) atomicOr(flag, 1u);
+      k_lo = ((op >> 15) < nb - 1 ? (op >> 15) : nb - 1) + 1;
+    }
+    for (uint64_t kk = k_lo; kk <= k; kk++) first[kk] = (uint32_t)i;
+  }
+}
+
+template <int MODE, int VAR = 0>
+__global__ void __launch_bounds__(kLsWaves * 64) crc32c_logstream_kernel(CrcParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  static_assert(MODE == kLogWrite || MODE == kLogVerify, "log modes only");
+  constexpr bool kVerifyMode = MODE == kLogVerify;
+  if (*(volatile const uint32_t*)p.ls_flag & 1u) return;  // unsorted: the follow-up takes it
+  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLsTabBytes / 16, nullptr, 0);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane & 7;
+  const int grp = lane >> 3;
+  const uint32_t rep = (uint32_t)(lane & 31) << 2;
+  const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
+  const uint64_t base = (uint64_t)p.base;
+  const uint64_t nb = p.n_lblocks;
+  const uint64_t R = (nb + 7) / 8;                     // rounds: 8 log blocks (one per group)
+  const int32_t off0 = (int32_t)(base & 127u);         // every block starts off0 into its line
+  const uint32_t KG = ((uint32_t)off0 + kLogBlock + 511u) / 512u;  // 4-line steps per block
+  const uint64_t zl = (uint64_t)p.zline;
+  const uint64_t lo_ok = base & ~15ull, hi_ok = (base + p.buf_len + 15) & ~15ull;
+  const uint32_t slots = kLsSlot0 + (uint32_t)wave * kLsSlots * kLsSlotBytes;
+  const uint32_t nwaves = blockDim.x >> 6;
+  const uint32_t nwg = gridDim.x;
+  const uint4 zero4 = make_uint4(0, 0, 0, 0);
+
+  // ---- round claims (per-workgroup counters, bounded stealing)
+  uint32_t victim = blockIdx.x, tried = 0, req = 0;
+  auto claim = [&](uint32_t v) {
+    uint32_t r = 0;
+    if (lane == 0)
+      r = __hip_atomic_fetch_add(p.sched + v * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    req = r;
+  };
+  auto round_of = [&](uint32_t v, uint32_t idx) -> uint64_t {
+    const uint64_t r = ((uint64_t)idx + nwaves) * nwg + v;
+    return r < R ? r : ~0ull;
+  };
+  auto collect = [&]() -> uint64_t {
+    uint64_t r = round_of(victim, __builtin_amdgcn_readfirstlane(req));
+    while (r == ~0ull && ++tried < p.steal_limit + 1) {
+      victim = (victim + 1) % nwg;
+      claim(victim);
+      r = round_of(victim, __builtin_amdgcn_readfirstlane(req));
+    }
+    return r;
+  };
+
+  // ---- per-group block state (group-uniform values, in every lane of it)
+  uint64_t k = 0;                      // log block of the group
+  uint32_t r_lo = 0, nrec = 0;         // its records [r_lo, r_lo + nrec)
+  uint32_t nwin = 0;                   // records in the window (0: dense block, all leftover)
+  uint32_t j = 0;                      // current window position
+  int32_t a_c = kLsFar, b_c = kLsFar;  // current record's CRC range, region-relative
+  uint32_t n_c = 0, ax_c = 0;          // its CRC length, aux (stored CRC)
+  int32_t prev_b = 0;                  // end of the previous streamed record (overlap check)
+  uint32_t wd[kLsWin], wa[kLsWin];     // window: desc = b_rel | n << 16 (n = 0: not streamed), aux
+  uint32_t np = 0;                     // pending snapshots of the wave (wave-uniform)
+  uint32_t ovl = 0;                    // this lane saw overlapping records
+  uint32_t nbad = 0;                   // this lane's mismatches (verify)
+  uint32_t* const left = p.ls_left;    // leftover record list, count at ls_flag[2]
+
+  // Decode the block's records (synchronous; once per block): offsets, then
+  // the 7-byte headers (a header past its block or the image is not read).
+  // Records not streamed here are appended to the leftover list.
+  auto decode_block = [&](uint64_t bk) {
+    const bool dense = nrec > 8u * kLsWin;
+    nwin = dense ? 0u : nrec;
+    uint64_t o[kLsWin];
+#pragma unroll
+    for (int m = 0; m < kLsWin; m++) {
+      const uint32_t jj = 8u * m + (uint32_t)q;
+      o[m] = jj < nwin ? p.offsets[r_lo + jj] : 0;
+    }
+    uint32_t nl = 0;  // this lane's leftovers
+#pragma unroll
+    for (int m = 0; m < kLsWin; m++) {
+      const uint32_t jj = 8u * m + (uint32_t)q;
+      const bool valid = jj < nwin;
+      const bool fits = valid && log_header_fits(o[m], p.buf_len);
+      const uint64_t h = fits ? base + o[m] : zl;
+      const uint32_t w0 = kVerifyMode ? *(gcu32u*)h : 0u;  // stored masked CRC
+      const uint32_t w1 = *(gcu32u*)(fits ? h + 4 : zl);    // length, type
+      const uint32_t length = w1 & 0xffffu;
+      const uint32_t st = fits ? log_status(o[m], length, kVerifyMode ? ((w1 >> 16) & 0xffu) : 1u,
+                                            p.buf_len)
+                               : (valid ? log_nohdr_status(o[m], p.buf_len) : NOVA_LOG_TRUNCATED);
+      const bool elig = st == NOVA_LOG_OK && 1u + length >= kLsMinN;
+      const uint64_t hrel = o[m] - bk * kLogBlock;
+      wd[m] = elig ? ((uint32_t)hrel + 7u + length) | ((1u + length) << 16) : 0u;
+      wa[m] = kVerifyMode ? w0 : 0u;
+      nl += (valid && !elig) ? 1u : 0u;
+    }
+    // leftover list: the whole block if dense, else the records not streamed
+    uint32_t cnt = dense ? (nrec > (uint32_t)q ? (nrec - 1u - (uint32_t)q) / 8u + 1u : 0u) : nl;
+    uint32_t incl = cnt;  // inclusive prefix over the group's 8 lanes
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, (unsigned)d, 8);
+      if (q >= d) incl += y;
+    }
+    const uint32_t total = __shfl(incl, (grp << 3) | 7);
+    uint32_t at = 0;
+    if (q == 0 && total) at = atomicAdd(p.ls_flag + 2, total);
+    at = __shfl(at, grp << 3);
+    if (dense) {
+      for (uint32_t i = (uint32_t)q; i < nrec; i += 8) left[at + i] = r_lo + i;
+    } else {
+      uint32_t pos = at + incl - cnt;
+#pragma unroll
+      for (int m = 0; m < kLsWin; m++) {
+        const uint32_t jj = 8u * m + (uint32_t)q;
+        if (jj < nwin && (wd[m] >> 16) == 0) left[pos++] = r_lo + jj;
+      }
+    }
+  };
+  // Current record := the first streamed record at window position >= j.
+  auto fetch = [&]() {
+    for (;;) {
+      if (j >= nwin) {
+        a_c = b_c = kLsFar;
+        n_c = 0;
+        return;
+      }
+      const uint32_t m = j >> 3;
+      uint32_t dsel = wd[0], asel = wa[0];
+#pragma unroll
+      for (int mm = 1; mm < kLsWin; mm++) {
+        if (m == (uint32_t)mm) {
+          dsel = wd[mm];
+          asel = wa[mm];
+        }
+      }
+      const int src = (grp << 3) | (int)(j & 7u);
+      const uint32_t d = __shfl(dsel, src);
+      if ((d >> 16) != 0) {
+        n_c = d >> 16;
+        b_c = off0 + (int32_t)(d & 0xffffu);
+        a_c = b_c - (int32_t)n_c;
+        ax_c = kVerifyMode ? __shfl(asel, src) : 0u;
+        if (a_c - 6 < prev_b) ovl = 1;  // starts inside the previous streamed record
+        prev_b = b_c;
+        return;
+      }
+      j++;
+    }
+  };
+
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+
+  // ---- fold phase: four lanes per pending snapshot ----------------------------
+  // A wave's LDS operations execute in order, so other lanes' snapshot stores
+  // are visible to the reads below once the compiler keeps the order (memory
+  // clobber); a wavefront-scope fence would also drain the step's data loads.
+  auto lds_order = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  auto fold_phase = [&]() {
+    lds_order();
+    const uint32_t rec = (uint32_t)lane >> 2, sub = (uint32_t)lane & 3u;
+    const bool act = rec < np;
+    const uint32_t sa = slots + (act ? rec : 0u) * kLsSlotBytes;
+    const uint4 meta = lds_u128(sa + 128);
+    const uint32_t info = meta.w;
+    const uint32_t kb = (info >> 16) & 31u, pad = (info >> 21) & 3u;
+    // chain `sub`: words kb+1+jj (mod 32) of the rotated message, jj = sub, sub+4, ...
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t jj = 0; jj < 32; jj += 4)
+      v = lds_apply(kLsM16, v) ^ lds_u32(nullptr, sa + (((kb + 1u + jj + sub) & 31u) << 2));
+    const int b4 = lane & ~3;
+    const uint32_t u0 = __shfl(v, b4), u1 = __shfl(v, b4 + 1), u2 = __shfl(v, b4 + 2);
+    const uint32_t u3 = __shfl(v, b4 + 3);
+    const uint32_t V = lds_apply(kLsM4, lds_apply(kLsM4, lds_apply(kLsM4, u0) ^ u1) ^ u2) ^ u3;
+    uint32_t reg = lds_apply(kLsM4, V);
+    if (pad >= 1) reg = unstep_byte(reg);
+    if (pad >= 2) reg = unstep_byte(reg);
+    if (pad >= 3) reg = unstep_byte(reg);
+    const uint32_t crc = ~reg;
+    if (act && sub == 0) {
+      if constexpr (MODE == kLogWrite) {
+        const uint64_t h = base + (uint64_t)meta.z * kLogBlock + (info & 0xffffu);
+        store_u32_unaligned((uint8_t*)h, mask_crc(crc));
+      } else {
+        const bool ok = unmask_crc(meta.y) == crc;
+        *(__attribute__((address_space(1))) uint8_t*)(p.ok_out + meta.x) =
+            (uint8_t)(ok ? NOVA_LOG_OK : NOVA_LOG_CHECKSUM_MISMATCH);
+        nbad += ok ? 0u : 1u;
+      }
+    }
+    np = 0;
+    lds_order();
+  };
+
+  // ---- one swath: line L0 (region-relative byte) of the group's block --------
+  auto swath = [&](const uint4 d, int32_t L0) {
+    const bool st = (a_c + 4 > L0) && (a_c < L0 + 128);
+    const bool en = b_c <= L0 + 128;
+    if ((VAR & kVarLsFast) != 0 || __builtin_amdgcn_ballot_w64(st || en) == 0) {
+      swath4(lds, c0, c1, c2, c3, d, lo0, lo1, lo2, lo3);
+      return;
+    }
+    // slow path: a record of some group starts or ends in this swath
+    const int32_t P = L0 + 16 * q;
+    const uint32_t o0 = c0, o1 = c1, o2 = c2, o3 = c3;
+    uint32_t t0 = c0, t1 = c1, t2 = c2, t3 = c3;
+    swath4(lds, t0, t1, t2, t3, zero4, lo0, lo1, lo2, lo3);  // T(c): the record goes on
+    const bool cont = a_c < L0;  // the current record began in an earlier swath
+    const uint32_t km = cont ? ~0u : 0u;
+    uint32_t r0, r1, r2, r3;
+    {  // r = (cont ? T(c) : 0) ^ (((d & LM[hi]) ^ LM[lo4]) & ~LM[lo])
+      const int32_t lo = clamp16(a_c - P), hi = clamp16(b_c - P), lo4 = clamp16(a_c + 4 - P);
+      const uint4 A = lds_u128(kLsLM + 16u * (uint32_t)hi);
+      const uint4 B = lds_u128(kLsLM + 16u * (uint32_t)lo);
+      const uint4 Cm = lds_u128(kLsLM + 16u * (uint32_t)lo4);
+      r0 = (t0 & km) ^ (((d.x & A.x) ^ Cm.x) & ~B.x);
+      r1 = (t1 & km) ^ (((d.y & A.y) ^ Cm.y) & ~B.y);
+      r2 = (t2 & km) ^ (((d.z & A.z) ^ Cm.z) & ~B.z);
+      r3 = (t3 & km) ^ (((d.w & A.w) ^ Cm.w) & ~B.w);
+    }
+    const uint64_t eb = __builtin_amdgcn_ballot_w64(en);
+    if (eb == 0) {  // starts only
+      c0 = r0;
+      c1 = r1;
+      c2 = r2;
+      c3 = r3;
+      return;
+    }
+    const uint64_t leaders = eb & 0x0101010101010101ull;
+    if (en) {  // snapshot the ending record, then take the group's next one
+      const int32_t kb = (b_c - 1 - L0) >> 2;  // stream holding byte b-1 (b > L0: n >= 128)
+      const uint32_t pad = (uint32_t)(4 * (kb + 1) - (b_c - L0));
+      const int k0 = 4 * q;
+      uint4 sn;
+      sn.x = (k0 + 0 > kb) ? (o0 & km) : r0;
+      sn.y = (k0 + 1 > kb) ? (o1 & km) : r1;
+      sn.z = (k0 + 2 > kb) ? (o2 & km) : r2;
+      sn.w = (k0 + 3 > kb) ? (o3 & km) : r3;
+      const uint64_t below = leaders & ((1ull << (grp * 8)) - 1ull);
+      const uint32_t sa = slots + (np + (uint32_t)__popcll(below)) * kLsSlotBytes;
+      lds_st128(sa + 16u * (uint32_t)q, sn);
+      if (q == 0) {
+        const uint32_t hrel = (uint32_t)(a_c - off0) - 6u;  // the record's header
+        lds_st128(sa + 128, make_uint4(r_lo + j, ax_c, (uint32_t)k,
+                                       hrel | ((uint32_t)kb << 16) | (pad << 21)));
+      }
+      j++;
+      fetch();
+    }
+    np += (uint32_t)__popcll(leaders);
+    // the ending groups' next record starts from zero (it may start in this swath;
+    // it cannot also end in it)
+    const int32_t lo = clamp16(a_c - P), hi = clamp16(b_c - P), lo4 = clamp16(a_c + 4 - P);
+    const uint4 A = lds_u128(kLsLM + 16u * (uint32_t)hi);
+    const uint4 B = lds_u128(kLsLM + 16u * (uint32_t)lo);
+    const uint4 Cm = lds_u128(kLsLM + 16u * (uint32_t)lo4);
+    c0 = en ? (((d.x & A.x) ^ Cm.x) & ~B.x) : r0;
+    c1 = en ? (((d.y & A.y) ^ Cm.y) & ~B.y) : r1;
+    c2 = en ? (((d.z & A.z) ^ Cm.z) & ~B.z) : r2;
+    c3 = en ? (((d.w & A.w) ^ Cm.w) & ~B.w) : r3;
+  };
+
+  // ---- rounds ---------------------------------------------------------------
+  uint64_t r = (uint64_t)wave * nwg + blockIdx.x;  // implicit first round
+  if (r >= R) {
+    claim(victim);
+    r = collect();
+  }
+  while (r != ~0ull) {
+    claim(victim);  // the next round (collected after this one)
+    k = r * 8 + (uint64_t)grp;
+    const bool act = k < nb;
+    r_lo = act ? p.first[k] : 0u;
+    nrec = act ? p.first[k + 1] - r_lo : 0u;
+    const uint64_t bstart = k * kLogBlock;
+    const uint32_t blen =
+        act ? (uint32_t)(p.buf_len - bstart < kLogBlock ? p.buf_len - bstart : kLogBlock) : 0u;
+    const uint64_t RS = base + bstart - (uint64_t)off0;  // region start: 128-B aligned
+    const uint32_t lines = act ? ((uint32_t)off0 + blen + 127u) / 128u : 0u;
+    decode_block(k);
+    j = 0;
+    prev_b = 0;
+    fetch();
+    c0 = c1 = c2 = c3 = 0;
+    auto piece = [&](uint32_t line) -> uint64_t {
+      const uint64_t a = RS + 128ull * line + 16u * (uint32_t)q;
+      return (line < lines && a >= lo_ok && a < hi_ok) ? a : zl;
+    };
+    uint4 b0 = gload16(piece(0)), b1 = gload16(piece(1));
+    uint4 b2 = gload16(piece(2)), b3 = gload16(piece(3));
+    for (uint32_t s = 0; s < KG; s++) {
+      const uint4 x0 = b0, x1 = b1, x2 = b2, x3 = b3;
+      const uint32_t ln = 4 * s + 4;
+      b0 = gload16(piece(ln));
+      b1 = gload16(piece(ln + 1));
+      b2 = gload16(piece(ln + 2));
+      b3 = gload16(piece(ln + 3));
+      const int32_t L = (int32_t)(512 * s);
+      swath(x0, L);
+      if (np >= kLsFlush) fold_phase();
+      swath(x1, L + 128);
+      if (np >= kLsFlush) fold_phase();
+      swath(x2, L + 256);
+      if (np >= kLsFlush) fold_phase();
+      swath(x3, L + 384);
+      if (np >= kLsFlush) fold_phase();
+    }
+    r = collect();
+  }
+  if (np) fold_phase();
+  if constexpr ((VAR & kVarLsFast) != 0)  // keep the ablation's stream live
+    if ((c0 ^ c1 ^ c2 ^ c3) == 0x9e3779b9u) atomicOr(p.ls_flag, 4u);
+  if (__builtin_amdgcn_ballot_w64(ovl != 0) && lane == 0) atomicOr(p.ls_flag, 2u);
+  if constexpr (kVerifyMode) {
+    if (__builtin_amdgcn_ballot_w64(nbad != 0)) {
+      uint32_t v = nbad;
+      for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) atomicAdd(p.ls_bad, v);
+    }
+  }
+  sched_release(p.sched);
+}
+
+
+// Diagnostic: plain coalesced streaming read (grid-stride, 4 x 16 B per lane
+// in flight), the chip's read ceiling for comparison with the CRC kernels.
+__global__ void __launch_bounds__(256) read_stream_kernel(const uint8_t* base, uint64_t n16,
+                                                          uint32_t* out) {
+  const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t nth = (uint64_t)gridDim.x * 256;
+  uint32_t acc = 0;
+  uint64_t i = tid;
+  const uint64_t b = (uint64_t)base;
+  for (; i + 3 * nth < n16; i += 4 * nth) {
+    const uint4 a0 = gload16(b + 16 * i), a1 = gload16(b + 16 * (i + nth));
+    const uint4 a2 = gload16(b + 16 * (i + 2 * nth)), a3 = gload16(b + 16 * (i + 3 * nth));
+    acc ^= a0.x ^ a0.y ^ a0.z ^ a0.w ^ a1.x ^ a1.y ^ a1.z ^ a1.w;
+    acc ^= a2.x ^ a2.y ^ a2.z ^ a2.w ^ a3.x ^ a3.y ^ a3.z ^ a3.w;
+  }
+  for (; i < n16; i += nth) {
+    const uint4 a = gload16(b + 16 * i);
+    acc ^= a.x ^ a.y ^ a.z ^ a.w;
+  }
+  out[tid] = acc;
+}
+
+// Diagnostic: read-ceiling probe.  U 16-byte loads per lane issued before any
+// use, default or nt policy, for measuring how much memory-level parallelism
+// the chip needs to approach its read peak.
+template <int U, int NT>
+__global__ void __launch_bounds__(1024) read_ceiling_kernel(const uint8_t* base, uint64_t n16,
+                                                            uint32_t* out) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  uint64_t i = tid;
+  const uint64_t b = (uint64_t)base;
+  for (; i + (U - 1) * nth < n16; i += U * nth) {
+    uint4 a[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) a[k] = gload16<NT ? 0 : kVarCached>(b + 16 * (i + k * nth));
+#pragma unroll
+    for (int k = 0; k < U; k++) acc ^= a[k].x ^ a[k].y ^ a[k].z ^ a[k].w;
+  }
+  for (; i < n16; i += nth) {
+    const uint4 a = gload16(b + 16 * i);
+    acc ^= a.x ^ a.y ^ a.z ^ a.w;
+  }
+  out[tid] = acc;
+}
+
+
+// ---- host ----------------------------------------------------------------------
+constexpr uint64_t kLogWindowMin = 1u << 15;  // log records: whole-piece CRC-field stores from here
+constexpr int kNotTaken = -999;               // a hook found nothing to do
+
+// g_tune_trailer_1pass: 2 = trailers in two passes; 3 = whole-64-B-piece
+// stores; 4 = the same non-temporal; 5 = whole-piece form without result
+// writes; 6 = no result writes; 7 = no per-block epilogue and no writes
+// (timing ablations: 5, 6 and 7 write nothing) -> CrcParams::wvar.
+uint32_t wvar_of(int tkn) {
+  return tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : tkn == 7 ? 3u : 0u;
+}
+
+template <int G, int MODE, int VAR = 0>
+int set_lds_attr_flat() {
+  return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_flat_kernel<G, MODE, VAR>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+}
+
+template <int MODE, int VAR = 0>
+int set_lds_attrs_flat() {
+  int e = 0;
+  if ((e = set_lds_attr_flat<1, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_flat<2, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_flat<4, MODE, VAR>())) return e;
+  if ((e = set_lds_attr_flat<8, MODE, VAR>())) return e;
+  return set_lds_attr_flat<16, MODE, VAR>();
+}
+
+// Blocks per claimed chunk of the flat kernel: one per lane group (the bank
+// refill is one step old when read), four per group for log records (the
+// header bytes need two more steps); at most 64 (one per lane).
+uint32_t flat_chunk(int G, int mode) {
+  const uint32_t groups = 64u / (uint32_t)G;
+  const bool log = mode == kLogWrite || mode == kLogVerify;
+  const int tc = g_tune_chunk.load();
+  uint32_t c = tc > 0 ? (uint32_t)tc : (log ? 4 * groups : 2 * groups);
+  // the descriptor banks must fit next to the tables
+  const uint64_t room = (kLdsMax - flat_lds_g(G)) / (flat_waves() * 2 * 16);
+  if (c > room) c = (uint32_t)room;
+  if (c > 64) c = 64;
+  if (c < 2 * groups) c = 2 * groups;  // the kernel relies on it (positions < 2C)
+  return c;
+}
+
+template <int MODE, int VAR>
+int launch_flat_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
+  switch (G) {
+    case 1: hipLaunchKernelGGL((crc32c_flat_kernel<1, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 2: hipLaunchKernelGGL((crc32c_flat_kernel<2, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 4: hipLaunchKernelGGL((crc32c_flat_kernel<4, MODE, VAR>), grid, block, lds, stream, p); break;
+    case 8: hipLaunchKernelGGL((crc32c_flat_kernel<8, MODE, VAR>), grid, block, lds, stream, p); break;
+    default: hipLaunchKernelGGL((crc32c_flat_kernel<16, MODE, VAR>), grid, block, lds, stream, p); break;
+  }
+  return (int)hipGetLastError();
+}
+
+template <int MODE>
+int launch_flat(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
+  p.tab_main = t->main[gindex(G)];
+  p.tab_tree = t->tree;
+  p.tab_byte = t->byte8;
+  p.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
+  p.omask = p.lmask = p.imask = ~0ull;
+  if (p.offsets) {
+    p.stride = 0;
+  } else {  // fixed stride: offset i * stride
+    p.offsets = reinterpret_cast<const uint64_t*>(t->zero_word);
+    p.omask = 0;
+  }
+  if (p.lengths) {
+    p.len = 0;
+  } else {  // fixed length p.len (log modes read the header instead)
+    p.lengths = t->zero_word;
+    p.lmask = 0;
+  }
+  if (!p.init) {
+    p.init = t->zero_word;
+    p.imask = 0;
+  }
+  p.chunk = flat_chunk(G, MODE);
+  p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
+  uint64_t nwaves = flat_waves();
+  while (nwaves > 1 && flat_lds_g(G) + nwaves * 2 * p.chunk * 16 > kLdsMax) nwaves--;  // G = 2
+  uint64_t wgs = (p.n_chunks + nwaves - 1) / nwaves;
+  if (wgs > (uint64_t)t->cus) wgs = t->cus;
+  if (wgs > 256) wgs = 256;
+  if (wgs == 0) return 0;
+  {
+    const int sl = g_tune_static_pct.load();
+    p.steal_limit = sl < 0 ? 8u : (uint32_t)sl;
+    // The first nwaves x wgs chunks are implicit (one per wave): when they cover
+    // the batch, a claim or a steal can only come back empty, and each of the
+    // 8 probes is a serial device-scope atomic (~1.5 us) on the launch's tail.
+    if (sl < 0 && p.n_chunks <= wgs * (uint64_t)nwaves) p.steal_limit = 0;
+  }
+  p.sched = sched_slot(t, stream);
+  if (!p.sched) return NOVA_E_NOMEM;
+  const dim3 block(64 * nwaves);
+  const size_t lds = flat_lds_g(G) + nwaves * 2 * p.chunk * 16;
+  if (lds > kLdsMax) return NOVA_E_INVAL;
+  const int var = g_tune_var.load();
+  if (MODE == kStore && var == kVarNoLookup) return launch_flat_g<kStore, kVarNoLookup>(G, dim3(wgs), block, lds, stream, p);
+  if (MODE == kStore && var == kVarCached) return launch_flat_g<kStore, kVarCached>(G, dim3(wgs), block, lds, stream, p);
+  return launch_flat_g<MODE, 0>(G, dim3(wgs), block, lds, stream, p);
+}
+
+template <int MODE>
+int launch_sort(CrcParams& p, DevTables* t, hipStream_t stream, uint64_t kStep, StreamScratch& sc) {
+  const size_t hist_bytes = 2 * kBins * sizeof(uint32_t);
+  if (sc.alloc(hist_bytes + p.n_blocks * sizeof(uint32_t), stream)) return NOVA_E_NOMEM;
+  uint32_t* hist = static_cast<uint32_t*>(sc.p);
+  uint32_t* perm = hist + 2 * kBins;
+  hipError_t e = hipMemsetAsync(hist, 0, kBins * sizeof(uint32_t), stream);
+  if (e != hipSuccess) return (int)e;
+  uint64_t wgs = (p.n_blocks + 255) / 256;
+  const uint64_t cap = (uint64_t)t->cus * 4;
+  if (wgs > cap) wgs = cap;
+  hipLaunchKernelGGL(bin_count_kernel<MODE>, dim3(wgs), dim3(256), 0, stream, p, kStep, hist);
+  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(kBins), 0, stream, hist, hist + kBins);
+  hipLaunchKernelGGL(bin_scatter_kernel<MODE>, dim3(wgs), dim3(256), 0, stream, p, kStep,
+                     hist + kBins, perm);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  p.perm = perm;
+  return 0;
+}
+
+// Log-stream experiment (nova_diag_set_variable_kernel(4)):
+// a pre-pass finds each 32 KiB block's first record, the log-stream kernel
+// streams the image, and the rounds kernel follows, gated: the leftover list,
+// or the whole batch if a precondition failed.  Measured slower than the
+// rounds kernel on 2 KiB-average records, so the product does not use it.
+template <int MODE>
+int launch_logstream(CrcParams& p, DevTables* t, hipStream_t stream) {
+  const uint64_t nb = (p.buf_len + kLogBlock - 1) / kLogBlock;
+  // [flag, mismatches, leftovers, -, first[0..nb], leftover list[n]], freed in stream order
+  StreamScratch sc;
+  const uint64_t left_at = (4 + nb + 1 + 3) & ~3ull;
+  if (sc.alloc((left_at + p.n_blocks) * sizeof(uint32_t), stream)) return NOVA_E_NOMEM;
+  uint32_t* w = static_cast<uint32_t*>(sc.p);
+  hipError_t e = hipMemsetAsync(w, 0, 16, stream);
+  if (e != hipSuccess) return (int)e;
+  uint32_t* first = w + 4;
+  uint64_t fwgs = (p.n_blocks + 1 + 255) / 256;
+  if (fwgs > (uint64_t)t->cus * 8) fwgs = (uint64_t)t->cus * 8;
+  hipLaunchKernelGGL(log_first_kernel, dim3(fwgs), dim3(256), 0, stream, p.offsets, p.n_blocks, nb,
+                     first, w);
+  CrcParams s = p;
+  s.first = first;
+  s.n_lblocks = nb;
+  s.ls_flag = w;
+  s.ls_bad = w + 1;
+  s.ls_left = w + left_at;
+  s.tab_main = t->main[gindex(kLsG)];
+  s.tab_tree = t->ls_tabs;
+  s.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
+  const uint64_t R = (nb + 7) / 8;
+  uint64_t wgs = (R + kLsWaves - 1) / kLsWaves;
+  if (wgs > (uint64_t)t->cus) wgs = t->cus;
+  if (wgs > 256) wgs = 256;
+  s.steal_limit = R <= wgs * kLsWaves ? 0u : 8u;
+  s.sched = sched_slot(t, stream);
+  if (!s.sched) return NOVA_E_NOMEM;
+  if (MODE == kLogWrite && g_tune_var.load() == kVarLsFast)
+    hipLaunchKernelGGL((crc32c_logstream_kernel<kLogWrite, kVarLsFast>), dim3(wgs), dim3(64 * kLsWaves),
+                       kLsLds, stream, s);
+  else
+    hipLaunchKernelGGL(crc32c_logstream_kernel<MODE>, dim3(wgs), dim3(64 * kLsWaves), kLsLds, stream, s);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  CrcParams f = p;  // follow-up: the leftover list, or the whole batch if flagged
+  f.gate = w;
+  f.ls_bad = w + 1;
+  f.perm = w + left_at;
+  const Plan pl = plan(p.n_blocks, 0, false, MODE, false, (uint32_t)t->cus);
+  f.wvar = 0;
+  return launch_rounds_v<MODE, kVarDiag>(pl.G, f, t, stream, pl.chunk);
+}
+
+// Trailer / log-write store forms and timing ablations.
+int store_forms(int mode, CrcParams& p, const Plan& pl, DevTables* t, hipStream_t stream) {
+  const int G = pl.G;
+  const bool small = p.n_blocks <= 2ull * t->cus * flat_waves();
+  // g_tune_trailer_1pass: 2 = trailers in two passes; 3 = whole-64-B-piece
+  // stores; 4 = the same non-temporal; 5 = whole-piece form without result
+  // writes; 6 = no result writes (timing ablations: 5 and 6 write nothing)
+  const int tkn = g_tune_trailer_1pass.load();
+  p.wvar = wvar_of(tkn);
+  const bool tk_piece = tkn == 3 || tkn == 4 || tkn == 5;
+  if (pl.kernel == kRoundsK && mode == kTrailer && tk_piece && !small) {
+    // whole-64-B-piece trailer stores where the layout allows it
+    // (trailer_layout_kernel)
+    StreamScratch sc;  // flag + eligibility, freed in stream order after the CRC kernel
+    if (sc.alloc(sizeof(uint32_t) * (p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
+    uint32_t* flag = static_cast<uint32_t*>(sc.p);
+    uint32_t* elig = flag + 1;
+    hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return (int)e;
+    uint64_t wgs = (p.n_blocks + 255) / 256;
+    const uint64_t cap = (uint64_t)t->cus * 8;
+    if (wgs > cap) wgs = cap;
+    // descriptors as launch_rounds normalises them (absent arrays: stride / len)
+    const uint64_t* lo = p.offsets ? p.offsets : reinterpret_cast<const uint64_t*>(t->zero_word);
+    const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
+    hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, lo,
+                       p.offsets ? ~0ull : 0ull, ll, p.lengths ? ~0ull : 0ull,
+                       p.offsets ? 0ull : p.stride, p.lengths ? 0u : p.len, p.n_blocks, elig, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    CrcParams q = p;
+    q.tr_flag = flag;
+    q.init = elig;  // trailer mode reads each block's eligibility in place of an init
+    return launch_rounds_v<kTrailer, kVarDiag>(G, q, t, stream, pl.chunk);
+  }
+  if (pl.kernel == kRoundsK && mode == kLogWrite && tk_piece &&
+      p.n_blocks >= kLogWindowMin && p.offsets) {
+    // whole-64-B-piece CRC-field stores where the layout allows it
+    // (log_window_kernel)
+    StreamScratch sc;  // flag + eligibility, freed in stream order after the CRC kernel
+    if (sc.alloc(sizeof(uint32_t) * (p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
+    uint32_t* flag = static_cast<uint32_t*>(sc.p);
+    uint32_t* elig = flag + 1;
+    hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return (int)e;
+    uint64_t wgs = (p.n_blocks + 255) / 256;
+    const uint64_t cap = (uint64_t)t->cus * 8;
+    if (wgs > cap) wgs = cap;
+    hipLaunchKernelGGL(log_window_kernel, dim3(wgs), dim3(256), 0, stream, p.offsets, p.n_blocks,
+                       p.buf_len, elig, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    CrcParams q = p;
+    q.tr_flag = flag;
+    q.init = elig;  // log write reads each record's eligibility in place of an init
+    return launch_rounds_v<kLogWrite, kVarDiag>(G, q, t, stream, pl.chunk);
+  }
+  if (pl.kernel == kRoundsK && mode == kTrailer && tkn == 8 && !small) {
+    // Two passes: CRCs into this call's own stream-ordered array (with the
+    // layout pre-pass's flag and eligibility), then trailer_rmw_kernel
+    StreamScratch sc;  // flag, eligibility, CRCs; freed in stream order after the second pass
+    if (sc.alloc(sizeof(uint32_t) * (2 * p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
+    uint32_t* flag = static_cast<uint32_t*>(sc.p);
+    uint32_t* elig = flag + 1;
+    uint32_t* tmp = elig + p.n_blocks;
+    hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return (int)e;
+    uint64_t wgs = (p.n_blocks + 255) / 256;
+    const uint64_t cap = (uint64_t)t->cus * 8;
+    if (wgs > cap) wgs = cap;
+    const uint64_t* lo = p.offsets ? p.offsets : reinterpret_cast<const uint64_t*>(t->zero_word);
+    const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
+    const uint64_t om = p.offsets ? ~0ull : 0ull, lm = p.lengths ? ~0ull : 0ull;
+    const uint64_t st = p.offsets ? 0ull : p.stride;
+    const uint32_t ln = p.lengths ? 0u : p.len;
+    hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, lo,
+                       om, ll, lm, st, ln, p.n_blocks, elig, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    CrcParams q = p;
+    q.out = tmp;
+    q.flags = (p.flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT;
+    const int e2 = launch_rounds_v<kStore, 0>(G, q, t, stream, pl.chunk);
+    if (e2) return e2;
+    uint64_t wgs8 = (p.n_blocks * 8 + 255) / 256;
+    if (wgs8 > cap) wgs8 = cap;
+    hipLaunchKernelGGL(trailer_rmw_kernel, dim3(wgs8), dim3(256), 0, stream,
+                       const_cast<uint8_t*>(p.base), lo, om, ll, lm, st, ln, tmp, elig, flag,
+                       p.n_blocks, p.flags);
+    return (int)hipGetLastError();
+  }
+  if (pl.kernel == kRoundsK && mode == kTrailer && tkn == 2 && !small) {
+    // Two passes: CRCs (type byte appended, masked) into this call's own
+    // stream-ordered array, then the trailer bytes (trailer_scatter_kernel).
+    StreamScratch sc;  // freed in stream order after the scatter
+    if (sc.alloc(p.n_blocks * sizeof(uint32_t), stream)) return NOVA_E_NOMEM;
+    uint32_t* tmp = static_cast<uint32_t*>(sc.p);
+    CrcParams q = p;
+    q.out = tmp;
+    q.flags = (p.flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT;
+    const int e = launch_rounds_v<kStore, 0>(G, q, t, stream, pl.chunk);
+    if (e) return e;
+    uint64_t wgs = (p.n_blocks + 255) / 256;
+    const uint64_t cap = (uint64_t)t->cus * 8;
+    if (wgs > cap) wgs = cap;
+    hipLaunchKernelGGL(trailer_scatter_kernel, dim3(wgs), dim3(256), 0, stream,
+                       const_cast<uint8_t*>(p.base), p.offsets, p.lengths, tmp, p.n_blocks, p.flags);
+    return (int)hipGetLastError();
+  }
+  return kNotTaken;
+}
+
+// ---- hooks (DiagHooks, crc32c_internal.hpp) -----------------------------------
+void push_op(const nova::gf2::Lin& m, std::vector<uint32_t>& v) {
+  uint32_t tb[4][256];
+  nova::gf2::byte_tables(m, tb);
+  for (int k = 0; k < 4; k++) v.insert(v.end(), tb[k], tb[k] + 256);
+}
+
+int hook_init_device(DevTables* t) {
+  using namespace nova::gf2;
+  const Lin m1 = zero_byte();
+  int e = 0;
+  {  // the burst kernel's M_1024 operator, 16-way bank-replicated (V = 65)
+    std::vector<uint32_t> op;
+    push_op(power(m1, (uint32_t)kBurstSw), op);
+    std::vector<uint32_t> rep(16384);  // 4 tables x 256 entries x 16 replicas
+    for (int k = 0; k < 4; k++)
+      for (int idx = 0; idx < 256; idx++)
+        for (int c = 0; c < 16; c++) rep[(k * 256 + idx) * 16 + c] = op[k * 256 + idx];
+    if ((e = upload_u32(&t->op1024r, rep.data(), rep.size()))) return e;
+  }
+  {  // log-stream experiment: M4, M16 and the prefix masks
+    std::vector<uint32_t> ls;
+    push_op(power(m1, 4), ls);
+    push_op(power(m1, 16), ls);
+    for (uint32_t nbytes = 0; nbytes <= 16; nbytes++)
+      for (uint32_t w = 0; w < 4; w++) {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 4; b++)
+          if (4 * w + b < nbytes) v |= 0xffu << (8 * b);
+        ls.push_back(v);
+      }
+    if ((e = upload_u32(&t->ls_tabs, ls.data(), ls.size()))) return e;
+    for (const void* f : {reinterpret_cast<const void*>(&crc32c_logstream_kernel<kLogWrite>),
+                          reinterpret_cast<const void*>(&crc32c_logstream_kernel<kLogVerify>),
+                          reinterpret_cast<const void*>(&crc32c_logstream_kernel<kLogWrite, kVarLsFast>)})
+      if ((e = (int)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLsLds)))
+        return e;
+  }
+  // timing ablations and alternative schedules
+  if ((e = set_lds_attrs_flat<kStore>())) return e;
+  if ((e = set_lds_attrs_flat<kTrailer>())) return e;
+  if ((e = set_lds_attrs_flat<kVerify>())) return e;
+  if ((e = set_lds_attrs_flat<kLogWrite>())) return e;
+  if ((e = set_lds_attrs_flat<kLogVerify>())) return e;
+  if ((e = set_lds_attrs_flat<kStore, kVarNoLookup>())) return e;
+  if ((e = set_lds_attrs_flat<kStore, kVarCached>())) return e;
+  if ((e = set_lds_attrs_rounds<kStore, kVarNoLookup>())) return e;
+  if ((e = set_lds_attrs_rounds<kStore, kVarNarrow>())) return e;
+  if ((e = set_lds_attrs_rounds<kStore, kVarDiag>())) return e;
+  if ((e = set_lds_attrs_rounds<kTrailer, kVarDiag>())) return e;
+  if ((e = set_lds_attrs_rounds<kVerify, kVarDiag>())) return e;
+  if ((e = set_lds_attrs_rounds<kLogWrite, kVarDiag>())) return e;
+  if ((e = set_lds_attrs_rounds<kLogVerify, kVarDiag>())) return e;
+  if ((e = set_lds_attrs_rounds<kVerify, kVarDiag | kVarNoTail>())) return e;
+  if ((e = set_lds_attrs_rounds<kLogVerify, kVarDiag | kVarNoTail>())) return e;
+  if ((e = set_lds_attrs_mode<kStore, kVarNoLookup>())) return e;
+  if ((e = set_lds_attrs_mode<kStore, kVarNarrow>())) return e;
+  if ((e = set_lds_attrs_mode<kStore, kVarCached>())) return e;
+  if ((e = set_lds_attrs_stream<kVarNoLookup>())) return e;
+  if ((e = set_lds_attrs_stream<kVarCached>())) return e;
+  if ((e = set_lds_attrs_stream<kVarWide>())) return e;
+  if ((e = set_lds_attrs_stream<kVarStamps>())) return e;
+  if ((e = set_lds_attrs_stream<kVarStamps | kVarStaticClaims>())) return e;
+  if ((e = set_lds_attr_burst<64, kStore, kVarStamps>()) || (e = set_lds_attr_burst<65, kStore>()) ||
+      (e = set_lds_attr_burst<16, kStore>()))
+    return e;
+  if ((e = set_lds_attr_burst<64, kTrailer, kVarStamps>()) || (e = set_lds_attr_burst<65, kTrailer>()) ||
+      (e = set_lds_attr_burst<16, kTrailer>()))
+    return e;
+  if ((e = set_lds_attr_burst<64, kVerify, kVarStamps>()) || (e = set_lds_attr_burst<65, kVerify>()) ||
+      (e = set_lds_attr_burst<16, kVerify>()))
+    return e;
+  return 0;
+}
+
+bool hook_run_early(int mode, CrcParams& p, DevTables* t, hipStream_t s, int* rc) {
+  if ((mode == kLogWrite || mode == kLogVerify) && p.n_blocks < (1ull << 31) &&
+      g_tune_kernel.load() == kLogStreamK) {
+    *rc = mode == kLogWrite ? launch_logstream<kLogWrite>(p, t, s) : launch_logstream<kLogVerify>(p, t, s);
+    return true;
+  }
+  return false;
+}
+
+bool hook_run_planned(int mode, CrcParams& p, const Plan& pl, DevTables* t, hipStream_t s, int* rc) {
+  const int r = store_forms(mode, p, pl, t, s);
+  if (r != kNotTaken) {
+    *rc = r;
+    return true;
+  }
+  if (pl.kernel == kFlatK) {
+    switch (mode) {
+      case kStore: *rc = launch_flat<kStore>(pl.G, p, t, s); break;
+      case kTrailer: *rc = launch_flat<kTrailer>(pl.G, p, t, s); break;
+      case kLogWrite: *rc = launch_flat<kLogWrite>(pl.G, p, t, s); break;
+      case kLogVerify: *rc = launch_flat<kLogVerify>(pl.G, p, t, s); break;
+      default: *rc = launch_flat<kVerify>(pl.G, p, t, s); break;
+    }
+    return true;
+  }
+  return false;
+}
+
+template <int MODE>
+int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk, int var) {
+  if constexpr (MODE == kStore) {
+    if (var == kVarNoLookup) return launch_rounds_v<kStore, kVarNoLookup>(G, p, t, s, chunk);
+    if (var == kVarNarrow) return launch_rounds_v<kStore, kVarNarrow>(G, p, t, s, chunk);
+  }
+  if constexpr (MODE == kVerify || MODE == kLogVerify) {
+    if (var == kVarNoTail) return launch_rounds_v<MODE, kVarDiag | kVarNoTail>(G, p, t, s, chunk);
+  }
+  if (p.wvar || p.gate || p.tr_flag) return launch_rounds_v<MODE, kVarDiag>(G, p, t, s, chunk);
+  if (p.perm) {  // sorted by the whole-batch pre-pass: the product kernels
+    if (MODE == kStore && p.init) return launch_rounds_v<kStore, kVarInit>(G, p, t, s, chunk);
+    return launch_rounds_v<MODE, 0>(G, p, t, s, chunk);
+  }
+  return kNotTaken;
+}
+
+bool hook_rounds(int mode, int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk, int* rc) {
+  const int var = g_tune_var.load();
+  p.wvar = wvar_of(g_tune_trailer_1pass.load());
+  StreamScratch sort_sc;  // freed in stream order after the launch below
+  if (g_tune_sort.load() == 1 && p.n_blocks >= 1024) {  // whole-batch sort pre-pass
+    const int g = G < 2 ? 2 : G;
+    CrcParams q = p;
+    rounds_params(g, q, t);  // the descriptors as the kernel reads them
+    int e = 0;
+    switch (mode) {
+      case kStore: e = launch_sort<kStore>(q, t, s, 64ull * g, sort_sc); break;
+      case kTrailer: e = launch_sort<kTrailer>(q, t, s, 64ull * g, sort_sc); break;
+      case kLogWrite: e = launch_sort<kLogWrite>(q, t, s, 64ull * g, sort_sc); break;
+      case kLogVerify: e = launch_sort<kLogVerify>(q, t, s, 64ull * g, sort_sc); break;
+      default: e = launch_sort<kVerify>(q, t, s, 64ull * g, sort_sc); break;
+    }
+    if (e) {
+      *rc = e;
+      return true;
+    }
+    p.perm = q.perm;
+  }
+  int r = kNotTaken;
+  switch (mode) {
+    case kStore: r = rounds_diag<kStore>(G, p, t, s, chunk, var); break;
+    case kTrailer: r = rounds_diag<kTrailer>(G, p, t, s, chunk, var); break;
+    case kLogWrite: r = rounds_diag<kLogWrite>(G, p, t, s, chunk, var); break;
+    case kLogVerify: r = rounds_diag<kLogVerify>(G, p, t, s, chunk, var); break;
+    default: r = rounds_diag<kVerify>(G, p, t, s, chunk, var); break;
+  }
+  if (r == kNotTaken) return false;  // the product launch
+  *rc = r;
+  return true;
+}
+
+bool hook_units(int mode, int G, CrcParams& p, DevTables* t, hipStream_t s, int* rc) {
+  if (mode != kStore) return false;
+  switch (g_tune_var.load()) {
+    case kVarNoLookup: *rc = launch_units_v<kStore, kVarNoLookup>(G, p, t, s); return true;
+    case kVarNarrow: *rc = launch_units_v<kStore, kVarNarrow>(G, p, t, s); return true;
+    case kVarCached: *rc = launch_units_v<kStore, kVarCached>(G, p, t, s); return true;
+    default: return false;
+  }
+}
+
+bool hook_stream(int G, CrcParams& p, DevTables* t, hipStream_t s, int* rc) {
+  switch (g_tune_var.load()) {
+    case kVarNoLookup: *rc = launch_stream_v<kVarNoLookup>(G, p, t, s); return true;
+    case kVarCached: *rc = launch_stream_v<kVarCached>(G, p, t, s); return true;
+    case kVarWide: *rc = launch_stream_v<kVarWide>(G, p, t, s); return true;
+    case kVarStamps:
+      p.stamps = g_diag_stamps.load();
+      *rc = launch_stream_v<kVarStamps>(G, p, t, s);
+      return true;
+    case kVarStamps | kVarStaticClaims:
+      p.stamps = g_diag_stamps.load();
+      *rc = launch_stream_v<kVarStamps | kVarStaticClaims>(G, p, t, s);
+      return true;
+    default: return false;
+  }
+}
+
+template <int MODE>
+int burst_diag(int V, CrcParams& p, DevTables* t, hipStream_t s) {
+  // V 65 / 16: measured slower at every batch size (profiles/r02_latency_burst_variants.log)
+  if (V == 65) return launch_burst_v<65, MODE>(p, t, s);
+  if (V == 16) return launch_burst_v<16, MODE>(p, t, s);
+  if (g_tune_var.load() == kVarStamps) {
+    p.stamps = g_diag_stamps.load();
+    return launch_burst_v<64, MODE, kVarStamps>(p, t, s);
+  }
+  return kNotTaken;
+}
+
+bool hook_burst(int V, int mode, CrcParams& p, DevTables* t, hipStream_t s, int* rc) {
+  int r = kNotTaken;
+  switch (mode) {
+    case kStore: r = burst_diag<kStore>(V, p, t, s); break;
+    case kTrailer: r = burst_diag<kTrailer>(V, p, t, s); break;
+    default: r = burst_diag<kVerify>(V, p, t, s); break;
+  }
+  if (r == kNotTaken) return false;
+  *rc = r;
+  return true;
+}
+
+int hook_describe_flat(int G, int mode, char* buf, size_t buflen) {
+  return snprintf(buf, buflen,
+                  "{\"kernel\": \"crc32c_flat_kernel<%d, %d>\", \"lanes_per_block\": %d, "
+                  "\"chunk_blocks\": %u, \"waves_per_wg\": %d}", G, mode, G,
+                  flat_chunk(G, mode), (int)flat_waves());
+}
+
+DiagHooks g_hooks = {hook_init_device, hook_run_early, hook_run_planned, hook_rounds,
+                     hook_units, hook_stream, hook_burst, hook_describe_flat};
+// Installed when the library loads, before any call can initialise a device.
+struct Install {
+  Install() { g_diag = &g_hooks; }
+} g_install;
+
+}  // namespace
+
+using namespace nova_dev;
+
+extern "C" {
+
+void nova_diag_set_variant(int variant) { g_tune_var.store(variant); }
+
+void nova_diag_set_stamps(uint64_t* dev_stamps) { g_diag_stamps.store(dev_stamps); }
+
+void nova_diag_set_static_pct(int pct) { g_tune_static_pct.store(pct); }
+
+void nova_diag_set_blocks_per_group(int bpg) { g_tune_bpg.store(bpg); }
+
+void nova_diag_set_chunk_blocks(int blocks) { g_tune_chunk.store(blocks); }
+
+void nova_diag_set_stream_waves(int waves) { g_tune_waves.store(waves); }
+
+void nova_diag_set_variable_kernel(int kernel) { g_tune_kernel.store(kernel); }
+
+void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
+
+void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
+
+void nova_diag_set_trailer_single_pass(int on) { g_tune_trailer_1pass.store(on); }
+
+void nova_diag_set_burst_lanes(int lanes) { g_tune_burst.store(lanes); }
+void nova_diag_set_split(int on) { g_tune_split.store(on); }
+
+int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
+                          void* stream) {
+  if (!base || !out_dev || wgs <= 0) return NOVA_E_INVAL;
+  hipLaunchKernelGGL(read_stream_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)base, (uint64_t)(bytes / 16), out_dev);
+  return (int)hipGetLastError();
+}
+
+int nova_diag_read_ceiling(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
+                           int variant, void* stream) {
+  if (!base || !out_dev || wgs <= 0) return NOVA_E_INVAL;
+  const int u = variant & 0xff;
+  const bool nt = (variant & 0x100) != 0;
+  const int threads = (variant & 0x200) ? 1024 : 256;
+  const uint8_t* b = (const uint8_t*)base;
+  const uint64_t n16 = bytes / 16;
+  hipStream_t st = (hipStream_t)stream;
+#define NOVA_RC(U)                                                                        \
+  if (u == U) {                                                                           \
+    if (nt) hipLaunchKernelGGL((read_ceiling_kernel<U, 1>), dim3(wgs), dim3(threads), 0, st, b, n16, out_dev); \
+    else hipLaunchKernelGGL((read_ceiling_kernel<U, 0>), dim3(wgs), dim3(threads), 0, st, b, n16, out_dev);   \
+    return (int)hipGetLastError();                                                        \
+  }
+  NOVA_RC(2) NOVA_RC(4) NOVA_RC(8) NOVA_RC(16)
+#undef NOVA_RC
+  return NOVA_E_INVAL;
+}
+
+
+}  // extern "C"
