@@ -86,6 +86,7 @@ _DIAG_SIG = {
     "nova_diag_set_variable_kernel": (None, [_i32]),
     "nova_diag_set_parity_variant": (None, [_i32]),
     "nova_diag_set_rounds_sort": (None, [_i32]),
+    "nova_diag_set_log_window": (None, [_i32]),
     "nova_diag_set_trailer_single_pass": (None, [_i32]),
     "nova_diag_set_burst_lanes": (None, [_i32]),
     "nova_diag_set_split": (None, [_i32]),
@@ -176,6 +177,7 @@ def diagnostics():
         D.nova_diag_set_stream_waves(0)
         D.nova_diag_set_variable_kernel(0)
         D.nova_diag_set_rounds_sort(2)
+        D.nova_diag_set_log_window(0)
         D.nova_diag_set_trailer_single_pass(0)
         D.nova_diag_set_parity_variant(0)
         D.nova_diag_set_burst_lanes(0)

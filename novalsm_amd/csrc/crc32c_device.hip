@@ -254,6 +254,92 @@ __global__ void __launch_bounds__(256) split_finish_kernel(CrcParams p, int mode
     split_finish(p, mode, extra, i, acc[i]);
 }
 
+// ---- log records: windowed sort by step count ---------------
+// The rounds kernel pads a round's kGroups records to the longest; sorting each
+// claimed chunk of 64 records leaves ~21 % of the loaded step capacity as
+// padding on U[1,4096] B records (tools/sim_rounds.py).  This pre-pass sorts
+// windows of kLogSortWin consecutive records (~1 MiB of log, so a chunk's
+// records stay close together in memory) by their step count, largest first,
+// into perm[]; the kernel then takes chunks of that order.  The key comes from
+// the offsets alone -- record i's length is at most the gap to the next
+// record's header or to its 32 KiB block's end -- so the pre-pass reads 8 B
+// per record and no header byte; a wrong estimate (unsorted offsets, a block
+// trailer) only costs padding, never a wrong CRC.  One workgroup per window,
+// counting sort in LDS (order within a step count is arbitrary).
+constexpr uint32_t kLogSortWin = 512;  // records per window (at most; g_tune_logwin)
+constexpr uint32_t kLogSortBins = 128;
+__global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint64_t* __restrict__ offs,
+                                                       uint64_t n, uint64_t buf_len, uint32_t line,
+                                                       uint32_t win, uint32_t* __restrict__ perm) {
+  __shared__ uint32_t cnt[kLogSortBins];
+  const uint64_t w0 = (uint64_t)blockIdx.x * win;
+  for (uint32_t b = threadIdx.x; b < kLogSortBins; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  constexpr int kPer = kLogSortWin / 256;
+  uint32_t key[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint64_t i = w0 + threadIdx.x + 256u * k;
+    key[k] = 0;
+    if (threadIdx.x + 256u * k < win && i < n) {
+      const uint64_t o = offs[i];
+      const uint64_t be = log_block_end(o, buf_len);
+      uint64_t e = i + 1 < n ? offs[i + 1] : be;
+      if (e > be || e < o) e = be;
+      const uint64_t u0 = base + o + 6, u1 = base + (e > o + 7 ? e : o + 7);  // CRC input [u0, u1)
+      const uint64_t E = u1 & ~15ull;
+      const uint64_t first = (u0 & ~15ull) & ~(uint64_t)(line - 1);
+      const uint64_t Le = (E + line - 1) & ~(uint64_t)(line - 1);
+      const uint64_t S = Le > first ? (Le - first + 4ull * line - 1) / (4ull * line) : 1;
+      key[k] = S < kLogSortBins ? (uint32_t)S : kLogSortBins - 1;
+      atomicAdd(&cnt[key[k]], 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive prefix in descending key order
+    uint32_t run = 0;
+    for (int b = kLogSortBins - 1; b >= 0; b--) {
+      const uint32_t c = cnt[b];
+      cnt[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint64_t i = w0 + threadIdx.x + 256u * k;
+    if (threadIdx.x + 256u * k < win && i < n) perm[w0 + atomicAdd(&cnt[key[k]], 1u)] = (uint32_t)i;
+  }
+}
+
+// The sorted records ran position-indexed (kVarOutPos): per window, move each
+// record's result from its position to the record, in record order -- verify:
+// its status byte into status_out[i]; write: Mask(crc) into the header's CRC
+// field when its status is OK (db/log_writer.cc:113).  Storing from the CRC
+// kernel in sorted order scattered a window's stores over time and over 1 MiB
+// of image (log write 52 % vs 63 % without the stores); here a
+// window's stores issue together, in file order, and the status lines are
+// written whole.
+__global__ void __launch_bounds__(256) log_unperm_kernel(uint8_t* base, const uint64_t* __restrict__ offs,
+                                                         uint64_t n, const uint32_t* __restrict__ perm,
+                                                         const uint8_t* __restrict__ st_pos,
+                                                         const uint32_t* __restrict__ crc_pos,
+                                                         uint8_t* __restrict__ status_out, uint32_t win) {
+  __shared__ uint16_t inv[kLogSortWin];
+  const uint64_t w0 = (uint64_t)blockIdx.x * win;
+  const uint32_t m = n - w0 < win ? (uint32_t)(n - w0) : win;
+  for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) inv[perm[w0 + j] - w0] = (uint16_t)j;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+    const uint64_t pos = w0 + inv[j];
+    const uint8_t st = st_pos[pos];
+    if (status_out)
+      status_out[w0 + j] = st;
+    else if (st == NOVA_LOG_OK)
+      store_u32_unaligned(base + offs[w0 + j], crc_pos[pos]);
+  }
+}
+
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
 __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                        uint64_t first_word) {
@@ -292,6 +378,7 @@ thread_local std::atomic<int> g_tune_waves{0};
 thread_local std::atomic<int> g_tune_parity{0};
 thread_local std::atomic<int> g_tune_kernel{0};
 thread_local std::atomic<int> g_tune_sort{2};
+thread_local std::atomic<int> g_tune_logwin{0};
 thread_local std::atomic<int> g_tune_trailer_1pass{0};
 thread_local std::atomic<int> g_tune_burst{0};
 thread_local std::atomic<int> g_tune_split{0};
@@ -396,6 +483,8 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_rounds<kVerify>())) return;
   if ((t->err = set_lds_attrs_rounds<kLogWrite>())) return;
   if ((t->err = set_lds_attrs_rounds<kLogVerify>())) return;
+  if ((t->err = set_lds_attr_rounds<8, kLogWrite, kVarOutPos>())) return;
+  if ((t->err = set_lds_attr_rounds<8, kLogVerify, kVarOutPos>())) return;
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;
@@ -565,11 +654,13 @@ int launch_mode(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   return launch_units_v<MODE, 0>(G, p, t, stream);
 }
 
+// p.perm: null, or the order to take the blocks in (log records: log_sort_kernel).
 template <int MODE>
 int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_t chunk = 0) {
-  p.perm = nullptr;
   int rc = 0;
   if (g_diag && g_diag->rounds(MODE, G, p, t, stream, chunk, &rc)) return rc;
+  if constexpr (MODE == kLogWrite || MODE == kLogVerify)
+    if (p.out_pos) return launch_rounds_v<MODE, kVarOutPos>(G, p, t, stream, chunk);
   if (MODE == kStore && p.init)  // per-block init values: the general head masking
     return launch_rounds_v<kStore, kVarInit>(G, p, t, stream, chunk);
   return launch_rounds_v<MODE, 0>(G, p, t, stream, chunk);
@@ -601,6 +692,8 @@ int launch_burst_g(int V, CrcParams& p, DevTables* t, hipStream_t stream) {
   return launch_burst_v<64, MODE>(p, t, stream);
 }
 
+
+constexpr uint64_t kLogSortMin = 1u << 16;  // records: the log_sort_kernel pre-pass from here
 
 // Few large blocks -> the split-and-combine path (split_*_kernel): uniform
 // blocks over kBurstMaxLen in a batch of at most kSplitMaxBlocks, or a batch of
@@ -729,6 +822,47 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   {
     int rc = 0;
     if (g_diag && g_diag->run_planned(mode, p, pl, t, stream, &rc)) return rc;
+  }
+  // Large logs: records in step-count order (log_sort_kernel), results by
+  // position, then log_unperm_kernel (small logs are latency-bound: two more
+  // launches would add their fixed cost).  Without scratch the records run
+  // unsorted (each claimed chunk still sorts itself).
+  StreamScratch log_sc;  // order + position-indexed results, freed in stream order
+  const int lsort = g_tune_sort.load();  // 2 default; 3-5 diagnostics A/B (crc32c_internal.hpp)
+  // Log write stays in file order: its CRC-field stores cost ~4 points of
+  // HBM throughput in file order, ~10 in sorted order from the CRC kernel and
+  // ~9 as a separate file-order pass (profiles/r03_ops_logsort3.log), more
+  // than the sort gains; the sort is a diagnostics option there.
+  const bool lsort_mode = mode == kLogVerify || (mode == kLogWrite && g_diag && g_tune_logwin.load() < 0);
+  if (pl.kernel == kRoundsK && lsort_mode && G == 8 &&
+      p.n_blocks >= kLogSortMin && p.n_blocks < (1ull << 32) && lsort >= 2 &&
+      !log_sc.alloc(p.n_blocks * (mode == kLogWrite ? 9 : 5), stream)) {
+    const uint64_t n = p.n_blocks;
+    const int tw = g_tune_logwin.load() < 0 ? -g_tune_logwin.load() : g_tune_logwin.load();
+    const uint32_t win = (tw > 0 && tw <= (int)kLogSortWin) ? (uint32_t)tw : kLogSortWin;
+    const bool by_pos = lsort == 2 || lsort == 3;
+    uint32_t* perm = static_cast<uint32_t*>(log_sc.p);
+    uint32_t* crc_pos = perm + n;  // log write only
+    uint8_t* st_pos = reinterpret_cast<uint8_t*>(mode == kLogWrite ? crc_pos + n : perm + n);
+    const uint64_t wgs = (n + win - 1) / win;
+    hipLaunchKernelGGL(log_sort_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, p.offsets, n,
+                       (uint64_t)p.buf_len, 16u * (uint32_t)G, win, perm);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    CrcParams q = p;
+    q.perm = perm;
+    uint8_t* status_out = p.ok_out;  // verify: the caller's status array
+    if (by_pos) {
+      q.out_pos = 1;
+      q.out = crc_pos;
+      q.ok_out = st_pos;
+    }
+    const int rc = mode == kLogWrite ? launch_rounds<kLogWrite>(G, q, t, stream, pl.chunk)
+                                     : launch_rounds<kLogVerify>(G, q, t, stream, pl.chunk);
+    if (rc || !by_pos) return rc;
+    hipLaunchKernelGGL(log_unperm_kernel, dim3(wgs), dim3(256), 0, stream, const_cast<uint8_t*>(p.base),
+                       p.offsets, n, perm, st_pos, crc_pos, mode == kLogWrite ? nullptr : status_out, win);
+    return (int)hipGetLastError();
   }
   if (pl.kernel == kRoundsK) {
     switch (mode) {

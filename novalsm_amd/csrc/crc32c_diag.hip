@@ -1435,6 +1435,9 @@ int hook_init_device(DevTables* t) {
   if ((e = set_lds_attrs_rounds<kLogVerify, kVarDiag>())) return e;
   if ((e = set_lds_attrs_rounds<kVerify, kVarDiag | kVarNoTail>())) return e;
   if ((e = set_lds_attrs_rounds<kLogVerify, kVarDiag | kVarNoTail>())) return e;
+  if ((e = set_lds_attr_rounds<8, kLogWrite, kVarDiag | kVarOutPos>())) return e;
+  if ((e = set_lds_attr_rounds<8, kLogVerify, kVarDiag | kVarOutPos>())) return e;
+  if ((e = set_lds_attr_rounds<8, kLogVerify, kVarDiag | kVarNoTail | kVarOutPos>())) return e;
   if ((e = set_lds_attrs_mode<kStore, kVarNoLookup>())) return e;
   if ((e = set_lds_attrs_mode<kStore, kVarNarrow>())) return e;
   if ((e = set_lds_attrs_mode<kStore, kVarCached>())) return e;
@@ -1488,6 +1491,14 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
   if constexpr (MODE == kStore) {
     if (var == kVarNoLookup) return launch_rounds_v<kStore, kVarNoLookup>(G, p, t, s, chunk);
     if (var == kVarNarrow) return launch_rounds_v<kStore, kVarNarrow>(G, p, t, s, chunk);
+  }
+  if constexpr (MODE == kLogWrite || MODE == kLogVerify) {
+    if (p.out_pos) {  // the product's sorted large-log path (G = 8), with the ablations
+      if (MODE == kLogVerify && var == kVarNoTail)
+        return launch_rounds_v<MODE, kVarDiag | kVarNoTail | kVarOutPos>(G, p, t, s, chunk);
+      if (p.wvar) return launch_rounds_v<MODE, kVarDiag | kVarOutPos>(G, p, t, s, chunk);
+      return kNotTaken;
+    }
   }
   if constexpr (MODE == kVerify || MODE == kLogVerify) {
     if (var == kVarNoTail) return launch_rounds_v<MODE, kVarDiag | kVarNoTail>(G, p, t, s, chunk);
@@ -1623,6 +1634,8 @@ void nova_diag_set_variable_kernel(int kernel) { g_tune_kernel.store(kernel); }
 void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
 
 void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
+
+void nova_diag_set_log_window(int records) { g_tune_logwin.store(records); }
 
 void nova_diag_set_trailer_single_pass(int on) { g_tune_trailer_1pass.store(on); }
 

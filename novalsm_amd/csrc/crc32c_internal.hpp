@@ -79,6 +79,7 @@ struct CrcParams {
   // pre-pass's eligibility array) rewrite the whole 64-B pieces holding its
   // trailer; null or nonzero: byte stores
   const uint32_t* tr_flag;
+  uint32_t out_pos;  // host: launch the kVarOutPos instantiation (log records in p.perm's order)
   uint32_t wvar;  // diagnostics (timing, kVarDiag): 1 = whole-piece stores non-temporal,
                   // 2 = no result writes, 3 = no per-block epilogue and no writes
 };
@@ -98,6 +99,11 @@ constexpr int kVarNoTail = 256;  // rounds kernel ablation: no tail-line loads (
 // timing ablations (CrcParams::gate, tr_flag, wvar) are compiled in.  The
 // product's instantiations (VAR 0, kVarInit) carry none of it.
 constexpr int kVarDiag = 512;
+// Rounds kernel, log modes: results indexed by the record's position in
+// CrcParams::perm's order (dense per chunk) instead of its index; log write
+// stores Mask(crc) to out[pos] and the record's status to ok_out[pos] and
+// leaves the image alone.  log_unperm_kernel finishes the call.
+constexpr int kVarOutPos = 1024;
 
 constexpr size_t kLdsMax = 160 * 1024;  // per CU on MI355X
 constexpr int kMaxDevices = 64;
@@ -144,7 +150,13 @@ extern thread_local std::atomic<int> g_tune_chunk;
 extern thread_local std::atomic<int> g_tune_waves;       // waves per workgroup (0 = per-kernel default)
 extern thread_local std::atomic<int> g_tune_parity;      // XOR parity kernel variant (0 = default)
 extern thread_local std::atomic<int> g_tune_kernel;      // VarKernel (0 = auto)
-extern thread_local std::atomic<int> g_tune_sort;        // rounds kernel: 0 in order, 1 whole batch, 2 per chunk
+// rounds kernel order: 0 blocks in order, 1 whole-batch sort (diagnostics),
+// 2 each chunk sorted + large logs in windows (log_sort_kernel), results by
+// position (default); diagnostics A/B for large logs: 3 windows only, by
+// position; 4 windows + chunks, results in place; 5 windows only, in place
+extern thread_local std::atomic<int> g_tune_sort;
+// log sort window in records (0 = 512); negative: -window, and log write sorts too
+extern thread_local std::atomic<int> g_tune_logwin;
 extern thread_local std::atomic<int> g_tune_trailer_1pass;  // trailer / log-write store forms
 extern thread_local std::atomic<int> g_tune_burst;       // 0 auto, 16/64/65 force, -1 off
 extern thread_local std::atomic<int> g_tune_split;       // 0 auto, 1 force, -1 off

@@ -1384,7 +1384,9 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
                               ? log_status(o, length, MODE == kLogVerify ? h6 : 1u, p.buf_len)
                               : log_nohdr_status(o, p.buf_len);
       n_n = ls == NOVA_LOG_OK ? 1u + length : 0u;  // 0: not read, n_aux = status
-      n_rec = t_rec;
+      // kVarOutPos: results go to the record's position in p.perm's order
+      // (dense per chunk); log_unperm_kernel moves them to the records
+      n_rec = (VAR & kVarOutPos) ? t_chunk * C + my : t_rec;
       n_aux = ls == NOVA_LOG_OK ? (MODE == kLogWrite ? t_aux : (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)))
                                 : ls;
       n_chunk = t_chunk;
@@ -1593,6 +1595,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   uint64_t wb_a = 0;
   uint32_t wb_v = 0;
   uint4 wb_w = make_uint4(0, 0, 0, 0);  // trailer writer: the patched sector piece
+  uint32_t wb_pos = 0, wb_st = 0;       // kVarOutPos log write: position, status
   auto fold = [&](FlatSet& Y) {
     uint4 d0 = Y.d0, d1 = Y.d1, d2 = Y.d2, d3 = Y.d3;
     if (__builtin_amdgcn_ballot_w64(Y.head)) {  // wave-uniform: some group's head step
@@ -1682,6 +1685,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         finish_block<MODE>(lds, kByteTab, p, raw, v, Y, wb_a, wb_v);
       }
       wb_on = q == 0 && Y.valid;  // written after the next step's loads are issued
+      if constexpr ((VAR & kVarOutPos) != 0 && MODE == kLogWrite) {
+        wb_pos = (uint32_t)Y.rec;
+        wb_st = Y.u1 == Y.u0 ? Y.st : (uint32_t)NOVA_LOG_OK;  // (status-only records: Y.st = status)
+      }
       if constexpr (MODE == kTrailer) {
         // lanes holding a sector piece store it patched with the trailer;
         // lane 0's byte stores are not used
@@ -1707,6 +1714,18 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   };
   auto writeback = [&]() {
     if (wb_on) {
+      if constexpr ((VAR & kVarOutPos) != 0 && MODE == kLogWrite) {
+        // position-indexed: Mask(crc) and the record's status (log_unperm_kernel
+        // writes the CRC field of the records whose status is OK)
+        typedef __attribute__((address_space(1))) uint32_t gu32;
+        typedef __attribute__((address_space(1))) uint8_t gu8;
+        if (!kDiag || p.wvar < 2) {
+          *(gu32*)(p.out + wb_pos) = wb_v;
+          *(gu8*)(p.ok_out + wb_pos) = (uint8_t)wb_st;
+        }
+        wb_on = false;
+        return;
+      }
       if ((MODE == kTrailer || MODE == kLogWrite) && wb_sec) {
         u32x4 w;
         w.x = wb_w.x;
@@ -2206,6 +2225,11 @@ int launch_stream_v(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
 // ---- rounds kernel (whole variable-length blocks in lockstep rounds) ----------
 template <int MODE, int VAR>
 int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
+  if constexpr ((VAR & kVarOutPos) != 0) {  // large logs only: G = 8
+    if (G != 8) return NOVA_E_INVAL;
+    hipLaunchKernelGGL((crc32c_rounds_kernel<8, MODE, VAR>), grid, block, lds, stream, p);
+    return (int)hipGetLastError();
+  }
   switch (G) {
     case 2: hipLaunchKernelGGL((crc32c_rounds_kernel<2, MODE, VAR>), grid, block, lds, stream, p); break;
     case 4: hipLaunchKernelGGL((crc32c_rounds_kernel<4, MODE, VAR>), grid, block, lds, stream, p); break;
@@ -2247,7 +2271,10 @@ template <int MODE, int VAR>
 int launch_rounds_v(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_t chunk = 0) {
   if (G < 2) G = 2;
   rounds_params(G, p, t);
-  p.sort_local = g_tune_sort.load() == 2 ? 1u : 0u;  // sort each chunk by step count
+  {
+    const int so = g_tune_sort.load();
+    p.sort_local = (so == 2 || so == 4) ? 1u : 0u;  // sort each chunk by step count
+  }
   {
     // chunk = R rounds of 64/G blocks.  Default (plan() passes 0 only when
     // tuning forces G): log records 64, SSTable blocks 4 rounds, since a chunk

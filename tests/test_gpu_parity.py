@@ -1315,6 +1315,56 @@ def test_logstream_preconditions(torch_gpu, oracle, case):
         assert np.array_equal(fresh.cpu().numpy(), exp)
 
 
+@pytest.mark.parametrize("order", ["file", "shuffled", "windows_only", "in_place", "unsorted"])
+def test_log_sorted_windows(torch_gpu, oracle, order):
+    """Log verify of >= 64K records runs in the order of the windowed
+    step-count sort (log_sort_kernel), keyed from the offsets
+    alone, with results by position moved back by log_unperm_kernel.  The
+    results are the oracle's whatever the key says: offsets in file order,
+    shuffled (the keys are then garbage), the window sort without the
+    per-chunk sort (diagnostics; log write sorted too, by position), results
+    stored in place (window 128), and no sort at all; write is bit-exact over
+    the image, verify finds exactly the corrupted records."""
+    from novalsm_amd.synth import log_image
+    torch = torch_gpu
+    rng = np.random.default_rng(91)
+    n = 150000
+    plen = rng.integers(0, 1400, n)
+    plen[rng.integers(0, n, 300)] = rng.integers(0, 3, 300)
+    plen[rng.integers(0, n, 30)] = rng.integers(20000, 70000, 30)
+    host, offs, _, _ = log_image(29, plen)
+    assert len(offs) >= 1 << 16
+    if order == "shuffled":
+        offs = offs[rng.permutation(len(offs))]
+    buf = dev(torch, host)
+    doffs = dev(torch, offs, torch.int64)
+    want = host.copy()
+    oracle.log_write(want, offs)
+
+    def run():
+        C.log_write_crcs(buf, doffs)
+        assert np.array_equal(buf.cpu().numpy(), want)
+        ok, bad = C.log_verify_records(buf, doffs)
+        assert (ok.cpu().numpy() == C.LOG_OK).all() and int(bad.item()) == 0
+        victims = rng.choice(len(offs), 40, replace=False)
+        for v in victims:
+            buf[int(offs[v]) + 6] ^= 0x02
+        ok, bad = C.log_verify_records(buf, doffs)
+        okh = ok.cpu().numpy()
+        assert sorted(np.nonzero(okh == C.LOG_CHECKSUM_MISMATCH)[0].tolist()) == sorted(victims.tolist())
+        assert int(bad.item()) == len(victims)
+        for v in victims:
+            buf[int(offs[v]) + 6] ^= 0x02
+
+    if order in ("windows_only", "in_place", "unsorted"):
+        with C.diagnostics() as L:
+            L.nova_diag_set_rounds_sort({"windows_only": 3, "in_place": 5, "unsorted": 0}[order])
+            L.nova_diag_set_log_window({"windows_only": -512, "in_place": -128, "unsorted": 0}[order])
+            run()
+    else:
+        run()
+
+
 @pytest.mark.parametrize("kernel", ["default", "logstream"])
 def test_log_96mib(torch_gpu, oracle, kernel):
     """A 96 MiB log::Writer image with U[1,4096] B payloads (the bench_ops log

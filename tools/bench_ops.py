@@ -71,6 +71,10 @@ def main() -> int:
                     help="comma list of nova_diag_set_parity_variant values (tuning)")
     ap.add_argument("--lanes-sweep", action="store_true",
                     help="also time each CRC op at 4/8/16 lanes per unit (tuning)")
+    ap.add_argument("--sort-sweep", default="",
+                    help="log ops: comma list of nova_diag_set_rounds_sort values (0 in order, "
+                         "2 windows + chunks, 3 windows only)")
+    ap.add_argument("--no-ablations", action="store_true", help="skip the diagnostics ablations")
     args = ap.parse_args()
     import torch
     from novalsm_amd import crc32c as C
@@ -82,6 +86,20 @@ def main() -> int:
     stream = torch.cuda.current_stream()
     ops = args.ops.split(",")
     rows = []
+
+    def sort_sweep(op, fn, alg_bytes):
+        # entries "sort" or "sort:window" (nova_diag_set_rounds_sort / _log_window)
+        for v in [x for x in args.sort_sweep.split(",") if x]:
+            so, _, win = v.partition(":")
+            with C.diagnostics() as D:
+                D.nova_diag_set_rounds_sort(int(so))
+                D.nova_diag_set_log_window(int(win or 0))
+                sec = timed(torch, fn, args.steps, args.warmup, stream)
+                D.nova_diag_set_rounds_sort(2)
+                D.nova_diag_set_log_window(0)
+            print(json.dumps({"sweep": op, "rounds_sort": int(so), "log_window": int(win or 0),
+                              "GBps": round(alg_bytes / sec / 1e9, 1),
+                              "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}), flush=True)
 
     def sweep(op, fn, alg_bytes):
         if not args.lanes_sweep:
@@ -210,9 +228,10 @@ def main() -> int:
                 ok &= int.from_bytes(rec[:4].tobytes(), "little") == want
             emit("log_write", wl, sum_rec, sec, ok)
             sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
-            for var, name in ((3, "log_write_pieces"), (4, "log_write_pieces_nt"),
+            sort_sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
+            for var, name in (() if args.no_ablations else ((3, "log_write_pieces"), (4, "log_write_pieces_nt"),
                               (5, "log_write_pieces_no_writes"), (6, "log_write_no_writes"),
-                              (7, "log_write_no_epilogue")):
+                              (7, "log_write_no_epilogue"))):
                 with C.diagnostics() as D:
                     D.nova_diag_set_trailer_single_pass(var)
                     sec1 = timed(torch, lambda: C.log_write_crcs(buf, o, stream=stream), args.steps,
@@ -232,7 +251,9 @@ def main() -> int:
             sec = timed(torch, lv, args.steps, args.warmup, stream)
             ok = int(bad.item()) == 0 and bool((okb.cpu().numpy() == C.LOG_OK).all())
             emit("log_verify", wl, sum_rec + n, sec, ok)
-            for var, name in ((0, "log_verify_no_writes"), (256, "log_verify_no_tail_loads_no_writes")):
+            sort_sweep("log_verify", lv, sum_rec + n)
+            for var, name in (() if args.no_ablations else
+                              ((0, "log_verify_no_writes"), (256, "log_verify_no_tail_loads_no_writes"))):
                 with C.diagnostics() as D:  # timing ablations (no result writes; 256: WRONG CRCs)
                     D.nova_diag_set_variant(var)
                     D.nova_diag_set_trailer_single_pass(6)
