@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Device-resident batched CRC32C throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
-                    [--secondary 3,4|none] [--settle-ms MS]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--config 2|3|4|5|sst4k_trailers|sst4k_verify]
+                    [--secondary 3,4,sst4k_trailers,sst4k_verify|none] [--settle-ms MS]
 
 One step = one pass of the hot path (a nova_crc32c_batch* call through the
 C-ABI) over one batch of synthetic SSTable blocks already resident in HBM.
@@ -14,8 +15,14 @@ Workloads (BASELINE.json configs; per GPU, weak scaling):
   4  1M x 16 KiB (16 GiB; 8M x 16 KiB over 8 GPUs)
   5  host-resident (pinned) 16 KiB blocks streamed H2D -> CRC -> D2H; its own
      line, never the device-resident value
-By default the line carries config 2 as `value` and configs 3 and 4 as
-`secondary` objects measured in the same run, each with its own roofline.
+  sst4k_trailers / sst4k_verify  NovaLSM's live block shape: 1M x (4096+U[0,255])
+     B blocks back to back with 5-B trailers, unaligned -- the trailer writer
+     (nova_sstable_write_trailers, TableBuilder ordering, table/table_builder.cc:
+     192-212) and the read-verify (nova_sstable_verify_blocks, table/table.cc:
+     434-440) over that image
+By default the line carries config 2 as `value` and configs 3, 4 and the two
+SSTable-shape workloads as `secondary` objects measured in the same run, each
+with its own roofline.
 
 Multi-GPU: one process per GPU.  Run under torchrun (WORLD_SIZE set) each rank
 takes its device from LOCAL_RANK; run as `python bench.py --gpus N` without
@@ -68,7 +75,31 @@ def config3_layout(n: int, seed: int = 3):
     return offs, lens, total
 
 
-def workload(cfg: int):
+SST_WORKLOADS = ("sst4k_trailers", "sst4k_verify")
+
+
+def sst4k_layout(n: int, seed: int = 5):
+    """NovaLSM's data blocks: 4096+U[0,255] B (a 4 KiB block_size block closes
+    past 4 KiB, table/block_builder.cc:56-60), back to back with their 5-B
+    trailers, from splitmix64(seed)."""
+    from novalsm_amd.synth import splitmix64_words
+    r = splitmix64_words(seed, 0, n)
+    lens = (np.uint64(4096) + (r % np.uint64(256))).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5))
+    total = int(offs[-1]) + int(lens[-1]) + 5
+    return offs, lens, total
+
+
+def workload(cfg):
+    if cfg == "sst4k_trailers":
+        return {"workload": "sst4k_trailers: 1M x (4096+U[0,255]) B blocks + 5-B trailers per GPU, "
+                            "trailer writer (TableBuilder ordering)",
+                "n_blocks": 1 << 20, "block_bytes": None, "kind": "sst_trailers"}
+    if cfg == "sst4k_verify":
+        return {"workload": "sst4k_verify: 1M x (4096+U[0,255]) B blocks + 5-B trailers per GPU, "
+                            "read-verify",
+                "n_blocks": 1 << 20, "block_bytes": None, "kind": "sst_verify"}
     if cfg == 2:
         return {"workload": "config2: 1M x 4 KiB uniform blocks per GPU (BASELINE configs[1])",
                 "n_blocks": 1 << 20, "block_bytes": 4096, "kind": "strided"}
@@ -174,12 +205,37 @@ def cpu_baseline(seconds: float = 4.0):
         pass
     return {"value": round(allc, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
             "single_core": round(one, 3), "cpu": model, **share,
+            "product_host_extend": product_host_extend(seconds / 4),
             "sample": f"BASELINE config 1: 1024 x 4 KiB splitmix64(seed 1) blocks, "
                       f"{r2} reps on {threads} threads (+{r1} reps on 1 thread), g++ -O2",
             "db_bench_crc32c": {"value": round(db_bytes / db_s / 2**30, 3), "unit": "GiB/s",
                                 "threads": 1, "crc": f"0x{crc:08x}",
                                 "sample": "benchmarks/db_bench.cc:635-652: Value(4 KiB of 'x') "
                                           "until 500 MiB, 1 thread"}}
+
+
+def product_host_extend(seconds: float = 1.0) -> dict:
+    """The product's own scalar drop-in (leveldb::crc32c::Extend in
+    crc32c_host.cpp, what every Extend() of an unmodified NovaLSM runs after
+    INTEGRATION.md level 1), 1 thread, on 4 KiB and 1 MiB buffers; the loop
+    runs natively (nova_diag_host_extend_loop: the same object code)."""
+    from novalsm_amd import crc32c as C
+    from novalsm_amd.synth import splitmix64_bytes
+    fn = C.load_diag().nova_diag_host_extend_loop
+    buf = splitmix64_bytes(9, 1 << 20)
+    res = {"threads": 1, "unit": "GiB/s",
+           "impl": "3 interleaved SSE4.2 crc32 chains joined by GF(2) shifts (crc32c_host.cpp)"}
+    for size, key in ((4096, "4KiB"), (1 << 20, "1MiB")):
+        reps = max(1, int(16 * 2**20 // size))
+        while True:
+            t0 = time.perf_counter()
+            fn(buf.ctypes.data, size, reps)
+            dt = time.perf_counter() - t0
+            if dt >= seconds / 2:
+                break
+            reps *= 2
+        res[key] = round(reps * size / dt / 2**30, 3)
+    return res
 
 
 # ---- launcher -----------------------------------------------------------------
@@ -248,6 +304,31 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
         lens_np = offs_np = None
         bytes_step = total
         dispatch = C.describe(n, L, L, variable=False)
+    elif wl["kind"] in ("sst_trailers", "sst_verify"):
+        offs_np, lens_np, total = sst4k_layout(n, 5)
+        buf = torch.empty(total + 64, dtype=torch.uint8, device=ctx.dev)
+        C.fill_splitmix64(buf, 31, first_word=ctx.rank * (total // 8))
+        offs = torch.from_numpy(offs_np.view(np.int64)).to(ctx.dev)
+        lens = torch.from_numpy(lens_np.view(np.int32)).to(ctx.dev)
+        sum_len = int(lens_np.astype(np.uint64).sum())
+        if wl["kind"] == "sst_trailers":
+            def step():  # TableBuilder's ordering ('!' after the encode)
+                C.write_trailers(buf, offs, lens, 0, True, stream=stream)
+            # algorithmic bytes: the blocks read and the trailers written
+            bytes_step = sum_len + 5 * n
+            out = None
+        else:
+            C.write_trailers(buf, offs, lens, 0, False, stream=stream)  # StoC order: verifiable
+            out = torch.empty(n, dtype=torch.uint8, device=ctx.dev)
+            bad = torch.zeros(1, dtype=torch.int32, device=ctx.dev)
+
+            def step():
+                C.verify_blocks(buf, offs, lens, stream=stream, ok=out, bad=bad)
+            # algorithmic bytes: block + type byte + stored CRC read, one flag written
+            bytes_step = sum_len + 6 * n
+        dispatch = C.describe(n, 4096 + 128, 0, variable=True)
+        dispatch["op"] = "nova_sstable_write_trailers" if wl["kind"] == "sst_trailers" \
+            else "nova_sstable_verify_blocks"
     else:
         offs_np, lens_np, total = config3_layout(n, seed)
         buf = torch.empty(total + 64, dtype=torch.uint8, device=ctx.dev)
@@ -303,16 +384,24 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
     if args.verify:
         from tests.oracle_lib import load_oracle
         orc = load_oracle()
-        got = out.cpu().numpy().view(np.uint32)
         idx = np.linspace(0, n - 1, 257).astype(np.int64)
         ok = True
-        for i in idx:
-            if wl["kind"] == "strided":
-                o, ln = int(i) * L, L
-            else:
+        if wl["kind"] == "sst_trailers":
+            for i in idx:
                 o, ln = int(offs_np[i]), int(lens_np[i])
-            blk = buf[o:o + ln].cpu().numpy().tobytes()
-            ok &= orc.value(blk) == int(got[i])
+                blk = buf[o:o + ln + 5].cpu().numpy().tobytes()
+                ok &= orc.trailer(blk[:ln], 0, True) == blk[ln:]
+        elif wl["kind"] == "sst_verify":
+            ok = bool(out.cpu().numpy().all()) and int(bad.item()) == 0  # every block, every step
+        else:
+            got = out.cpu().numpy().view(np.uint32)
+            for i in idx:
+                if wl["kind"] == "strided":
+                    o, ln = int(i) * L, L
+                else:
+                    o, ln = int(offs_np[i]), int(lens_np[i])
+                blk = buf[o:o + ln].cpu().numpy().tobytes()
+                ok &= orc.value(blk) == int(got[i])
         oks = ctx.all_gather_f64(1.0 if ok else 0.0)  # every rank learns whether any shard failed
         verified = bool(min(oks) > 0)
 
@@ -327,34 +416,59 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
         roof["kernel_ms_avg_per_rank"] = [round(x, 4) for x in rank_kernel_ms]
     del buf, out
     torch.cuda.empty_cache()
+    res_wl = {"workload": wl["workload"], "n_blocks": n, "bytes_per_gpu": bytes_step,
+              "dispatch": dispatch}
+    if wl["kind"] in ("sst_trailers", "sst_verify"):
+        res_wl["algorithmic_bytes"] = ("sum(len) read + 5 B trailer written per block"
+                                       if wl["kind"] == "sst_trailers"
+                                       else "sum(len + 5) read + 1 B flag written per block")
     return {
         "config": cfg,
         "value": round(ctx.world * bytes_step * args.steps / dt_max / 2**30, 2),
         "unit": "GiB/s",
         "ms_per_step": round(dt_max / args.steps * 1e3, 4),
-        "workload": {"workload": wl["workload"], "n_blocks": n, "bytes_per_gpu": bytes_step,
-                     "dispatch": dispatch},
+        "workload": res_wl,
         "settle": {"settle_ms": round(settle_ms, 1), "settle_launches": settle_launches},
         "roofline": roof,
         "verified_sample": verified,
     }
 
 
-def traffic_of(cfg: int, dispatch: dict) -> dict:
+KERNEL_SOURCES = ("crc32c_kernels.hpp", "crc32c_internal.hpp", "crc32c_device.hip")
+
+
+def kernel_src_sha16() -> str:
+    """Hash of the product kernels' sources: a PMC pass taken on other sources
+    (even for a kernel of the same name) does not describe this run."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "novalsm_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def traffic_of(cfg, dispatch: dict) -> dict:
     """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE
     pass (tools/pmc.sh -> profiles/pmc_config<N>.json); PMC counters cannot be
     read from inside the timed run.  Used only when that pass profiled the
-    kernel this run dispatches."""
+    kernel this run dispatches, built from the same kernel sources
+    (src_sha16); otherwise traffic is null and traffic_source says why."""
     path = os.path.join("profiles", f"pmc_config{cfg}.json")
     try:
         with open(os.path.join(ROOT, path)) as f:
             pmc = json.load(f)
     except (OSError, ValueError):
-        return {"traffic": None, "traffic_source": None}
+        return {"traffic": None, "traffic_source": f"no PMC pass ({path})"}
     k = pmc.get("kernel")
     if k and k != dispatch.get("kernel"):
         return {"traffic": None, "traffic_source": f"{path} profiled {k}, not this dispatch"}
-    src = f"{path} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate pass"
+    sha = kernel_src_sha16()
+    if pmc.get("src_sha16") != sha:
+        return {"traffic": None,
+                "traffic_source": f"{path} was taken on kernel sources {pmc.get('src_sha16')}, "
+                                  f"not this tree's {sha}"}
+    src = f"{path} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate pass, kernel sources {sha}"
     if pmc.get("commit"):
         src += f", tree {pmc['commit']}"
     return {"traffic": pmc.get("hbm_bytes_per_launch"), "traffic_source": src + ")"}
@@ -420,7 +534,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", default="2", choices=["2", "3", "4", "5", *SST_WORKLOADS])
     ap.add_argument("--secondary", default="auto",
                     help="configs measured after the primary one in the same run "
                          "(comma list, 'none'; auto: 3,4 when the primary is 2)")
@@ -434,6 +548,7 @@ def main() -> int:
     ap.add_argument("--harness-check", action="store_true",
                     help="CPU-only check of the rank launcher (gloo), no measurement")
     args = ap.parse_args()
+    args.config = int(args.config) if args.config.isdigit() else args.config
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args.gpus, sys.argv[1:])
@@ -473,11 +588,12 @@ def main() -> int:
 
     prim = run_device_config(args.config, args, ctx)
     if args.secondary == "auto":
-        sec_cfgs = [3, 4] if args.config == 2 else []
+        sec_cfgs = [3, 4, *SST_WORKLOADS] if args.config == 2 else []
     elif args.secondary in ("", "none"):
         sec_cfgs = []
     else:
-        sec_cfgs = [int(x) for x in args.secondary.split(",") if int(x) != args.config]
+        sec_cfgs = [int(x) if x.isdigit() else x for x in args.secondary.split(",")]
+        sec_cfgs = [c for c in sec_cfgs if c != args.config]
     secondary = []
     for c in sec_cfgs:
         if c == 5:

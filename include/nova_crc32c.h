@@ -85,8 +85,10 @@ uint32_t nova_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
  * self-test ("TestCRCBuffer" -> 0xdcbc59fa, util/crc32c.cc:477-485), after
  * which the reference sends EVERY Extend() here (util/crc32c.cc:487-491), so
  * the hook never returns a wrong CRC:
- *   - buffers below NOVA_HOOK_MIN_BYTES (env, default 1 MiB) run on the host
- *     (the library's SSE4.2 Extend; one 4 KiB block is ~1 us there);
+ *   - buffers below NOVA_HOOK_MIN_BYTES (env, default 8 MiB) run on the host
+ *     (the library's SSE4.2 Extend, three interleaved crc32 chains: ~30-35
+ *     GiB/s on one EPYC core; the measured crossover with the device path,
+ *     copy included, lies between 4 and 16 MiB: tools/hook_crossover.py);
  *   - larger ones are copied to the GPU (one pooled stream and staging buffer
  *     per calling thread), checksummed by the HIP kernels and folded on the
  *     host; ANY device failure (no device, allocation beyond

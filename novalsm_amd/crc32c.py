@@ -87,6 +87,7 @@ _DIAG_SIG = {
     "nova_diag_set_parity_variant": (None, [_i32]),
     "nova_diag_set_rounds_sort": (None, [_i32]),
     "nova_diag_set_log_window": (None, [_i32]),
+    "nova_diag_host_extend_loop": (_u32, [_vp, _sz, ctypes.c_uint64]),
     "nova_diag_set_trailer_single_pass": (None, [_i32]),
     "nova_diag_set_burst_lanes": (None, [_i32]),
     "nova_diag_set_split": (None, [_i32]),

@@ -340,6 +340,92 @@ __global__ void __launch_bounds__(256) log_unperm_kernel(uint8_t* base, const ui
   }
 }
 
+// ---- trailer writer: CRC pass, then whole-piece trailer stores
+// Trailer writer pre-pass.  HBM writes whole 64-B pieces; a store that
+// covers only part of one (a 5-B trailer) costs a read-modify-write at the
+// memory, so the rounds kernel rewrites the whole aligned
+// 64-B piece(s) holding a trailer -- its "window", one piece or two when the
+// trailer crosses a piece boundary -- patched with the trailer bytes.  The
+// window's other bytes are stored back unchanged, which is safe when no other
+// block's trailer lies in it: then nobody else writes those bytes (block data
+// is only read) and no two windows share a piece (every window piece holds a
+// byte of its own trailer).
+//   *flag |= 1 unless the blocks are ascending and disjoint, trailer
+//   included (offset[i+1] >= offset[i] + size[i] + 5): then only the
+//   neighbours' trailers can reach a window, and
+//   elig[i] = 1 iff block i's window holds neither neighbour's trailer, lies
+//   above the first block's start (i == 0) and is not the last block's (its
+//   window may run past the image).  Window bytes outside every block (gaps)
+//   lie between two blocks of the image, so inside the caller's allocation.
+//   Windows are aligned in absolute addresses (ba = the image base), as the
+//   kernels that store them see them.
+__global__ void __launch_bounds__(256) trailer_layout_kernel(uint64_t ba, const uint64_t* offsets,
+                                                             uint64_t omask, const uint32_t* lengths,
+                                                             uint64_t lmask, uint64_t stride,
+                                                             uint32_t len, uint64_t n, uint32_t* elig,
+                                                             uint32_t* flag) {
+  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  auto u0_of = [&](uint64_t i) { return ba + offsets[i & omask] + i * stride; };
+  auto u1_of = [&](uint64_t i) { return u0_of(i) + lengths[i & lmask] + len; };
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
+    const uint64_t u0 = u0_of(i), u1 = u1_of(i);
+    const uint64_t ws = u1 & ~63ull, we = ((u1 + 4) & ~63ull) + 64;
+    bool e = i + 1 < n;
+    if (i + 1 < n) {
+      bad = bad || u0_of(i + 1) < u1 + 5;
+      e = e && u1_of(i + 1) >= we;
+    }
+    e = e && (i == 0 ? ws >= u0 : u1_of(i - 1) + 5 <= ws);
+    elig[i] = e ? 1u : 0u;
+  }
+  if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+// Two-pass trailer writer with whole-piece stores, second pass: the CRC pass
+// left crc[i] = Mask(crc) (type appended); block i's trailer [u1, u1+5) is
+// patched into the aligned 64-B piece(s) holding it, which are read and
+// stored whole when trailer_layout_kernel found them private to the block
+// (*flag == 0, elig[i]); other blocks store their five bytes.  Eight lanes per
+// block: lane k owns the piece line s0 + 16k (k < 4, or < 8 when the trailer
+// crosses a piece).  The stores run after every read of the image, in their
+// own launch.
+__global__ void __launch_bounds__(256) trailer_rmw_kernel(uint8_t* base, const uint64_t* offsets,
+                                                          uint64_t omask, const uint32_t* lengths,
+                                                          uint64_t lmask, uint64_t stride, uint32_t len,
+                                                          const uint32_t* crc, const uint32_t* elig,
+                                                          const uint32_t* flag, uint64_t n,
+                                                          uint32_t flags) {
+  const uint64_t nth = ((uint64_t)gridDim.x * blockDim.x) >> 3;
+  const uint32_t k = threadIdx.x & 7u;
+  const bool layout_ok = *flag == 0;
+  const bool quirk = (flags & NOVA_TRAILER_TB_QUIRK) != 0;
+  const uint32_t type = (flags >> 8) & 0xffu;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3; i < n; i += nth) {
+    uint8_t* t = base + offsets[i & omask] + i * stride + lengths[i & lmask] + len;
+    const uint32_t m = crc[i];
+    if (layout_ok && elig[i]) {
+      const uint64_t u1 = (uint64_t)t, s0 = u1 & ~63ull;
+      const uint32_t np = ((u1 + 4) & ~63ull) != s0 ? 8u : 4u;
+      if (k < np) {
+        const uint32_t mq = quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m;
+        const uint64_t tv = (uint64_t)type | ((uint64_t)mq << 8);
+        const uint64_t a = s0 + 16u * k;
+        auto* pa = (__attribute__((address_space(1))) u32x4*)a;
+        u32x4 w = *pa;
+        const uint4 d = patch_trailer(make_uint4(w.x, w.y, w.z, w.w), a, u1, tv);
+        w.x = d.x;
+        w.y = d.y;
+        w.z = d.z;
+        w.w = d.w;
+        *pa = w;
+      }
+    } else if (k == 0) {
+      store_trailer(t, type, m, quirk);
+    }
+  }
+}
+
 // Synthetic data: splitmix64 counter stream (novalsm_amd/synth.py).
 __global__ void fill_splitmix64_kernel(uint8_t* dst, uint64_t nbytes, uint64_t seed,
                                        uint64_t first_word) {
@@ -695,6 +781,60 @@ int launch_burst_g(int V, CrcParams& p, DevTables* t, hipStream_t stream) {
 
 constexpr uint64_t kLogSortMin = 1u << 16;  // records: the log_sort_kernel pre-pass from here
 
+}  // namespace
+
+namespace nova_dev {
+
+int trailer_layout(const CrcParams& p, DevTables* t, hipStream_t stream, uint32_t* elig, uint32_t* flag) {
+  hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
+  if (e != hipSuccess) return (int)e;
+  uint64_t wgs = (p.n_blocks + 255) / 256;
+  const uint64_t cap = (uint64_t)t->cus * 8;
+  if (wgs > cap) wgs = cap;
+  // descriptors as the rounds kernel normalises them (absent arrays: stride / len)
+  const uint64_t* lo = p.offsets ? p.offsets : reinterpret_cast<const uint64_t*>(t->zero_word);
+  const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
+  hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, lo,
+                     p.offsets ? ~0ull : 0ull, ll, p.lengths ? ~0ull : 0ull, p.offsets ? 0ull : p.stride,
+                     p.lengths ? 0u : p.len, p.n_blocks, elig, flag);
+  return (int)hipGetLastError();
+}
+
+// The trailer writer on rounds-kernel batches (round 3).  Storing the 5-B
+// trailers from the CRC kernel cost ~16 points of HBM throughput on NovaLSM's
+// block shape (partial 64-B pieces, each a read-modify-write at the memory,
+// interleaved with the read stream); the CRC pass instead writes one word per
+// block into a stream-ordered array, and trailer_rmw_kernel then rewrites the
+// whole 64-B piece(s) holding each trailer (profiles/r03_ops_batchepi.log:
+// 66 % -> 72 %).  Without scratch: the one-pass form.
+int trailer_two_pass(CrcParams& p, int G, uint32_t chunk, DevTables* t, hipStream_t stream) {
+  StreamScratch sc;  // flag, eligibility, CRCs; freed in stream order after the second pass
+  if (sc.alloc(sizeof(uint32_t) * (2 * p.n_blocks + 1), stream))
+    return launch_rounds_v<kTrailer, 0>(G, p, t, stream, chunk);
+  uint32_t* flag = static_cast<uint32_t*>(sc.p);
+  uint32_t* elig = flag + 1;
+  uint32_t* tmp = elig + p.n_blocks;
+  int e = trailer_layout(p, t, stream, elig, flag);
+  if (e) return e;
+  CrcParams q = p;
+  q.out = tmp;
+  q.flags = (p.flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT;
+  if ((e = launch_rounds_v<kStore, 0>(G, q, t, stream, chunk))) return e;
+  const uint64_t cap = (uint64_t)t->cus * 8;
+  uint64_t wgs8 = (p.n_blocks * 8 + 255) / 256;
+  if (wgs8 > cap) wgs8 = cap;
+  const uint64_t* lo = p.offsets ? p.offsets : reinterpret_cast<const uint64_t*>(t->zero_word);
+  const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
+  hipLaunchKernelGGL(trailer_rmw_kernel, dim3(wgs8), dim3(256), 0, stream, const_cast<uint8_t*>(p.base), lo,
+                     p.offsets ? ~0ull : 0ull, ll, p.lengths ? ~0ull : 0ull, p.offsets ? 0ull : p.stride,
+                     p.lengths ? 0u : p.len, tmp, elig, flag, p.n_blocks, p.flags);
+  return (int)hipGetLastError();
+}
+
+}  // namespace nova_dev
+
+namespace {
+
 // Few large blocks -> the split-and-combine path (split_*_kernel): uniform
 // blocks over kBurstMaxLen in a batch of at most kSplitMaxBlocks, or a batch of
 // at most kSplitMaxHinted blocks the caller marks HINT_LARGE_BLOCKS (the host
@@ -864,6 +1004,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
                        p.offsets, n, perm, st_pos, crc_pos, mode == kLogWrite ? nullptr : status_out, win);
     return (int)hipGetLastError();
   }
+  if (pl.kernel == kRoundsK && mode == kTrailer) return trailer_two_pass(p, G, pl.chunk, t, stream);
   if (pl.kernel == kRoundsK) {
     switch (mode) {
       case kStore: return launch_rounds<kStore>(G, p, t, stream, pl.chunk);

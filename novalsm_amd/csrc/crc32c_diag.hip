@@ -515,47 +515,6 @@ __global__ void __launch_bounds__(256) bin_scatter_kernel(CrcParams p, uint64_t 
 // Store-form experiments for the trailer writer and log CRC fields (DESIGN.md
 // 3.5b): measured, not faster than the CRC kernel's own byte stores.
 
-// Trailer writer pre-pass.  HBM writes whole 64-B pieces; a store that
-// covers only part of one (a 5-B trailer) costs a read-modify-write at the
-// memory, so the rounds kernel rewrites the whole aligned
-// 64-B piece(s) holding a trailer -- its "window", one piece or two when the
-// trailer crosses a piece boundary -- patched with the trailer bytes.  The
-// window's other bytes are stored back unchanged, which is safe when no other
-// block's trailer lies in it: then nobody else writes those bytes (block data
-// is only read) and no two windows share a piece (every window piece holds a
-// byte of its own trailer).
-//   *flag |= 1 unless the blocks are ascending and disjoint, trailer
-//   included (offset[i+1] >= offset[i] + size[i] + 5): then only the
-//   neighbours' trailers can reach a window, and
-//   elig[i] = 1 iff block i's window holds neither neighbour's trailer, lies
-//   above the first block's start (i == 0) and is not the last block's (its
-//   window may run past the image).  Window bytes outside every block (gaps)
-//   lie between two blocks of the image, so inside the caller's allocation.
-//   Windows are aligned in absolute addresses (ba = the image base), as the
-//   kernels that store them see them.
-__global__ void __launch_bounds__(256) trailer_layout_kernel(uint64_t ba, const uint64_t* offsets,
-                                                             uint64_t omask, const uint32_t* lengths,
-                                                             uint64_t lmask, uint64_t stride,
-                                                             uint32_t len, uint64_t n, uint32_t* elig,
-                                                             uint32_t* flag) {
-  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
-  bool bad = false;
-  auto u0_of = [&](uint64_t i) { return ba + offsets[i & omask] + i * stride; };
-  auto u1_of = [&](uint64_t i) { return u0_of(i) + lengths[i & lmask] + len; };
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth) {
-    const uint64_t u0 = u0_of(i), u1 = u1_of(i);
-    const uint64_t ws = u1 & ~63ull, we = ((u1 + 4) & ~63ull) + 64;
-    bool e = i + 1 < n;
-    if (i + 1 < n) {
-      bad = bad || u0_of(i + 1) < u1 + 5;
-      e = e && u1_of(i + 1) >= we;
-    }
-    e = e && (i == 0 ? ws >= u0 : u1_of(i - 1) + 5 <= ws);
-    elig[i] = e ? 1u : 0u;
-  }
-  if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
-}
-
 // Log write pre-pass (same reasoning as trailer_layout_kernel): the rounds
 // kernel rewrites the whole 64-B piece holding a record's 4-byte CRC field
 // [o, o+4) (db/log_writer.cc:113) instead of storing 4 bytes into it.
@@ -582,50 +541,6 @@ __global__ void __launch_bounds__(256) log_window_kernel(const uint64_t* offs, u
     elig[i] = e ? 1u : 0u;
   }
   if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
-}
-
-// Two-pass trailer writer with whole-piece stores, second pass: the CRC pass
-// left crc[i] = Mask(crc) (type appended); block i's trailer [u1, u1+5) is
-// patched into the aligned 64-B piece(s) holding it, which are read and
-// stored whole when trailer_layout_kernel found them private to the block
-// (*flag == 0, elig[i]); other blocks store their five bytes.  Eight lanes per
-// block: lane k owns the piece line s0 + 16k (k < 4, or < 8 when the trailer
-// crosses a piece).  The stores run after every read of the image, in their
-// own launch.
-__global__ void __launch_bounds__(256) trailer_rmw_kernel(uint8_t* base, const uint64_t* offsets,
-                                                          uint64_t omask, const uint32_t* lengths,
-                                                          uint64_t lmask, uint64_t stride, uint32_t len,
-                                                          const uint32_t* crc, const uint32_t* elig,
-                                                          const uint32_t* flag, uint64_t n,
-                                                          uint32_t flags) {
-  const uint64_t nth = ((uint64_t)gridDim.x * blockDim.x) >> 3;
-  const uint32_t k = threadIdx.x & 7u;
-  const bool layout_ok = *flag == 0;
-  const bool quirk = (flags & NOVA_TRAILER_TB_QUIRK) != 0;
-  const uint32_t type = (flags >> 8) & 0xffu;
-  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3; i < n; i += nth) {
-    uint8_t* t = base + offsets[i & omask] + i * stride + lengths[i & lmask] + len;
-    const uint32_t m = crc[i];
-    if (layout_ok && elig[i]) {
-      const uint64_t u1 = (uint64_t)t, s0 = u1 & ~63ull;
-      const uint32_t np = ((u1 + 4) & ~63ull) != s0 ? 8u : 4u;
-      if (k < np) {
-        const uint32_t mq = quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m;
-        const uint64_t tv = (uint64_t)type | ((uint64_t)mq << 8);
-        const uint64_t a = s0 + 16u * k;
-        auto* pa = (__attribute__((address_space(1))) u32x4*)a;
-        u32x4 w = *pa;
-        const uint4 d = patch_trailer(make_uint4(w.x, w.y, w.z, w.w), a, u1, tv);
-        w.x = d.x;
-        w.y = d.y;
-        w.z = d.z;
-        w.w = d.w;
-        *pa = w;
-      }
-    } else if (k == 0) {
-      store_trailer(t, type, m, quirk);
-    }
-  }
 }
 
 __global__ void __launch_bounds__(256) trailer_scatter_kernel(uint8_t* base, const uint64_t* offsets,
@@ -1281,6 +1196,23 @@ int store_forms(int mode, CrcParams& p, const Plan& pl, DevTables* t, hipStream_
   const int tkn = g_tune_trailer_1pass.load();
   p.wvar = wvar_of(tkn);
   const bool tk_piece = tkn == 3 || tkn == 4 || tkn == 5;
+  // The product's trailer writer on rounds batches is two passes (CRC array,
+  // then whole-piece stores, trailer_two_pass).  Its ablations: 6 = the CRC
+  // pass alone (no trailer writes); 7 = the same without the per-block
+  // epilogue; 9 = the one-pass form (trailer bytes stored by the CRC kernel,
+  // the product until round 3).
+  if (pl.kernel == kRoundsK && mode == kTrailer && (tkn == 6 || tkn == 7) && !small) {
+    StreamScratch sc;
+    if (sc.alloc(sizeof(uint32_t) * p.n_blocks, stream)) return NOVA_E_NOMEM;
+    CrcParams q = p;
+    q.out = static_cast<uint32_t*>(sc.p);
+    q.flags = (p.flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT;
+    q.wvar = tkn == 7 ? 3u : 0u;
+    return tkn == 7 ? launch_rounds_v<kStore, kVarDiag>(G, q, t, stream, pl.chunk)
+                    : launch_rounds_v<kStore, 0>(G, q, t, stream, pl.chunk);
+  }
+  if (pl.kernel == kRoundsK && mode == kTrailer && tkn == 9 && !small)
+    return launch_rounds_v<kTrailer, 0>(G, p, t, stream, pl.chunk);
   if (pl.kernel == kRoundsK && mode == kTrailer && tk_piece && !small) {
     // whole-64-B-piece trailer stores where the layout allows it
     // (trailer_layout_kernel)
@@ -1288,18 +1220,8 @@ int store_forms(int mode, CrcParams& p, const Plan& pl, DevTables* t, hipStream_
     if (sc.alloc(sizeof(uint32_t) * (p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
     uint32_t* flag = static_cast<uint32_t*>(sc.p);
     uint32_t* elig = flag + 1;
-    hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
-    if (e != hipSuccess) return (int)e;
-    uint64_t wgs = (p.n_blocks + 255) / 256;
-    const uint64_t cap = (uint64_t)t->cus * 8;
-    if (wgs > cap) wgs = cap;
-    // descriptors as launch_rounds normalises them (absent arrays: stride / len)
-    const uint64_t* lo = p.offsets ? p.offsets : reinterpret_cast<const uint64_t*>(t->zero_word);
-    const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
-    hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, lo,
-                       p.offsets ? ~0ull : 0ull, ll, p.lengths ? ~0ull : 0ull,
-                       p.offsets ? 0ull : p.stride, p.lengths ? 0u : p.len, p.n_blocks, elig, flag);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    const int e = trailer_layout(p, t, stream, elig, flag);
+    if (e) return e;
     CrcParams q = p;
     q.tr_flag = flag;
     q.init = elig;  // trailer mode reads each block's eligibility in place of an init
@@ -1326,39 +1248,8 @@ int store_forms(int mode, CrcParams& p, const Plan& pl, DevTables* t, hipStream_
     q.init = elig;  // log write reads each record's eligibility in place of an init
     return launch_rounds_v<kLogWrite, kVarDiag>(G, q, t, stream, pl.chunk);
   }
-  if (pl.kernel == kRoundsK && mode == kTrailer && tkn == 8 && !small) {
-    // Two passes: CRCs into this call's own stream-ordered array (with the
-    // layout pre-pass's flag and eligibility), then trailer_rmw_kernel
-    StreamScratch sc;  // flag, eligibility, CRCs; freed in stream order after the second pass
-    if (sc.alloc(sizeof(uint32_t) * (2 * p.n_blocks + 1), stream)) return NOVA_E_NOMEM;
-    uint32_t* flag = static_cast<uint32_t*>(sc.p);
-    uint32_t* elig = flag + 1;
-    uint32_t* tmp = elig + p.n_blocks;
-    hipError_t e = hipMemsetAsync(flag, 0, sizeof(uint32_t), stream);
-    if (e != hipSuccess) return (int)e;
-    uint64_t wgs = (p.n_blocks + 255) / 256;
-    const uint64_t cap = (uint64_t)t->cus * 8;
-    if (wgs > cap) wgs = cap;
-    const uint64_t* lo = p.offsets ? p.offsets : reinterpret_cast<const uint64_t*>(t->zero_word);
-    const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
-    const uint64_t om = p.offsets ? ~0ull : 0ull, lm = p.lengths ? ~0ull : 0ull;
-    const uint64_t st = p.offsets ? 0ull : p.stride;
-    const uint32_t ln = p.lengths ? 0u : p.len;
-    hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, lo,
-                       om, ll, lm, st, ln, p.n_blocks, elig, flag);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-    CrcParams q = p;
-    q.out = tmp;
-    q.flags = (p.flags & 0xff00u) | NOVA_CRC32C_APPEND_TYPE | NOVA_CRC32C_MASK_OUTPUT;
-    const int e2 = launch_rounds_v<kStore, 0>(G, q, t, stream, pl.chunk);
-    if (e2) return e2;
-    uint64_t wgs8 = (p.n_blocks * 8 + 255) / 256;
-    if (wgs8 > cap) wgs8 = cap;
-    hipLaunchKernelGGL(trailer_rmw_kernel, dim3(wgs8), dim3(256), 0, stream,
-                       const_cast<uint8_t*>(p.base), lo, om, ll, lm, st, ln, tmp, elig, flag,
-                       p.n_blocks, p.flags);
-    return (int)hipGetLastError();
-  }
+  if (pl.kernel == kRoundsK && mode == kTrailer && tkn == 8 && !small)
+    return trailer_two_pass(p, G, pl.chunk, t, stream);  // (the product's form since round 3)
   if (pl.kernel == kRoundsK && mode == kTrailer && tkn == 2 && !small) {
     // Two passes: CRCs (type byte appended, masked) into this call's own
     // stream-ordered array, then the trailer bytes (trailer_scatter_kernel).
@@ -1435,6 +1326,13 @@ int hook_init_device(DevTables* t) {
   if ((e = set_lds_attrs_rounds<kLogVerify, kVarDiag>())) return e;
   if ((e = set_lds_attrs_rounds<kVerify, kVarDiag | kVarNoTail>())) return e;
   if ((e = set_lds_attrs_rounds<kLogVerify, kVarDiag | kVarNoTail>())) return e;
+  if ((e = set_lds_attrs_rounds<kStore, kVarDiag | kVarRoundEpi>())) return e;
+  if ((e = set_lds_attrs_rounds<kTrailer, kVarDiag | kVarRoundEpi>())) return e;
+  if ((e = set_lds_attrs_rounds<kVerify, kVarDiag | kVarRoundEpi>())) return e;
+  if ((e = set_lds_attrs_rounds<kLogWrite, kVarDiag | kVarRoundEpi>())) return e;
+  if ((e = set_lds_attrs_rounds<kLogVerify, kVarDiag | kVarRoundEpi>())) return e;
+  if ((e = set_lds_attr_rounds<8, kLogWrite, kVarDiag | kVarRoundEpi | kVarOutPos>())) return e;
+  if ((e = set_lds_attr_rounds<8, kLogVerify, kVarDiag | kVarRoundEpi | kVarOutPos>())) return e;
   if ((e = set_lds_attr_rounds<8, kLogWrite, kVarDiag | kVarOutPos>())) return e;
   if ((e = set_lds_attr_rounds<8, kLogVerify, kVarDiag | kVarOutPos>())) return e;
   if ((e = set_lds_attr_rounds<8, kLogVerify, kVarDiag | kVarNoTail | kVarOutPos>())) return e;
@@ -1492,10 +1390,12 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
     if (var == kVarNoLookup) return launch_rounds_v<kStore, kVarNoLookup>(G, p, t, s, chunk);
     if (var == kVarNarrow) return launch_rounds_v<kStore, kVarNarrow>(G, p, t, s, chunk);
   }
+  const bool round_epi = var == kVarRoundEpi;  // A/B: the per-round epilogue (rounds 1-2 form)
   if constexpr (MODE == kLogWrite || MODE == kLogVerify) {
     if (p.out_pos) {  // the product's sorted large-log path (G = 8), with the ablations
       if (MODE == kLogVerify && var == kVarNoTail)
         return launch_rounds_v<MODE, kVarDiag | kVarNoTail | kVarOutPos>(G, p, t, s, chunk);
+      if (round_epi) return launch_rounds_v<MODE, kVarDiag | kVarRoundEpi | kVarOutPos>(G, p, t, s, chunk);
       if (p.wvar) return launch_rounds_v<MODE, kVarDiag | kVarOutPos>(G, p, t, s, chunk);
       return kNotTaken;
     }
@@ -1503,7 +1403,9 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
   if constexpr (MODE == kVerify || MODE == kLogVerify) {
     if (var == kVarNoTail) return launch_rounds_v<MODE, kVarDiag | kVarNoTail>(G, p, t, s, chunk);
   }
-  if (p.wvar || p.gate || p.tr_flag) return launch_rounds_v<MODE, kVarDiag>(G, p, t, s, chunk);
+  // the whole-piece store forms live in the per-round epilogue
+  if (p.tr_flag || round_epi) return launch_rounds_v<MODE, kVarDiag | kVarRoundEpi>(G, p, t, s, chunk);
+  if (p.wvar || p.gate) return launch_rounds_v<MODE, kVarDiag>(G, p, t, s, chunk);
   if (p.perm) {  // sorted by the whole-batch pre-pass: the product kernels
     if (MODE == kStore && p.init) return launch_rounds_v<kStore, kVarInit>(G, p, t, s, chunk);
     return launch_rounds_v<MODE, 0>(G, p, t, s, chunk);
@@ -1636,6 +1538,14 @@ void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
 void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
 
 void nova_diag_set_log_window(int records) { g_tune_logwin.store(records); }
+
+// The product's host Extend (crc32c_host.cpp, linked into both libraries)
+// called reps times on one buffer, for timing without a Python call per block.
+uint32_t nova_diag_host_extend_loop(const void* data, size_t n, uint64_t reps) {
+  uint32_t acc = 0;
+  for (uint64_t r = 0; r < reps; r++) acc ^= nova_crc32c_extend(acc, static_cast<const char*>(data), n);
+  return acc;
+}
 
 void nova_diag_set_trailer_single_pass(int on) { g_tune_trailer_1pass.store(on); }
 

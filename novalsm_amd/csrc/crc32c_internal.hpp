@@ -104,6 +104,10 @@ constexpr int kVarDiag = 512;
 // stores Mask(crc) to out[pos] and the record's status to ok_out[pos] and
 // leaves the image alone.  log_unperm_kernel finishes the call.
 constexpr int kVarOutPos = 1024;
+// Rounds kernel: the per-block epilogue (tail bytes, mask, store / compare)
+// once per round for the round's groups (rounds 1-2 form; the diagnostics
+// store forms need it) instead of once per chunk for all 64 blocks lane-parallel.
+constexpr int kVarRoundEpi = 2048;
 
 constexpr size_t kLdsMax = 160 * 1024;  // per CU on MI355X
 constexpr int kMaxDevices = 64;
@@ -199,6 +203,13 @@ struct StreamScratch {
 // The kernels' launchers are host templates in crc32c_kernels.hpp
 // (launch_rounds_v<MODE, VAR> and friends): each TU instantiates the variants
 // it launches, the product only VAR 0 (and kVarInit).
+
+// Trailer writer for rounds-kernel batches (crc32c_device.hip): the CRC pass
+// into a stream-ordered array, then the trailers patched into whole 64-B
+// pieces.  trailer_layout: the pieces' eligibility pre-pass
+// (zeroes *flag first); both return 0 or an error.
+int trailer_two_pass(CrcParams& p, int G, uint32_t chunk, DevTables* t, hipStream_t stream);
+int trailer_layout(const CrcParams& p, DevTables* t, hipStream_t stream, uint32_t* elig, uint32_t* flag);
 
 // ---- diagnostics hooks (crc32c_diag.hip fills g_diag; null in the product) --
 // Each returns true when it took over the launch, with its result in *rc.

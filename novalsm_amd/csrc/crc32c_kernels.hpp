@@ -1071,6 +1071,8 @@ struct FlatSet {
   bool head;             // rounds kernel: the step holds a byte of [u0, u0+4) (group-uniform)
   bool l3;               // rounds kernel: the lane's last-swath piece is in the region
   bool wsec;             // rounds kernel, trailer writer: t2 holds this lane's sector piece
+  uint32_t slot;         // rounds kernel (chunk epilogue): the block's sorted slot in its chunk
+  bool cend;             // rounds kernel (chunk epilogue): the chunk's last round ends here
 };
 
 constexpr uint64_t kNoChunk = ~0ull;
@@ -1192,6 +1194,56 @@ __device__ __forceinline__ void write_result(const CrcParams& p, uint64_t wb_a, 
 
 
 
+// The chunk epilogue's two halves (rounds kernel, lane-parallel per block).
+// R(u1) = M_nb(R(E)) ^ tail_raw for the block's last nb = u1 - E < 16 bytes
+// (E = u1 & ~15): tail_raw is those bytes run from a zero register, with the
+// head edge of a block that starts inside the tail line (bytes before u0
+// dropped, ~init at [u0, u0+4)) -- the same steps as finish_block, split by
+// linearity so the data part runs when the block's descriptor is decoded.
+template <uint32_t kTree>
+__device__ __forceinline__ uint32_t tail_raw(const uint8_t* lds, uint32_t byte_tab, uint4 t, uint32_t nb,
+                                             int32_t ht, uint32_t ninit) {
+  const uint8_t* m4 = lds + kTree;
+  const uint32_t w0 = head_word(t.x, ht, ninit), w1 = head_word(t.y, ht - 4, ninit);
+  const uint32_t w2 = head_word(t.z, ht - 8, ninit), w3 = head_word(t.w, ht - 12, ninit);
+  uint32_t R = 0, r;
+  r = lapply(m4, w0);
+  R = nb >= 4 ? r : R;
+  r = lapply(m4, R ^ w1);
+  R = nb >= 8 ? r : R;
+  r = lapply(m4, R ^ w2);
+  R = nb >= 12 ? r : R;
+  const uint32_t wl = sel5(nb >> 2, w0, w1, w2, w3, 0u);
+  const uint32_t nr = nb & 3u;
+  r = (R >> 8) ^ lds_u32(lds, byte_tab + ((R ^ wl) & 255u) * 4u);
+  R = nr >= 1 ? r : R;
+  r = (R >> 8) ^ lds_u32(lds, byte_tab + ((R ^ (wl >> 8)) & 255u) * 4u);
+  R = nr >= 2 ? r : R;
+  r = (R >> 8) ^ lds_u32(lds, byte_tab + ((R ^ (wl >> 16)) & 255u) * 4u);
+  R = nr >= 3 ? r : R;
+  return R;
+}
+// M_nb(R) for nb < 16 zero bytes (M4 word steps, then byte steps).
+template <uint32_t kTree>
+__device__ __forceinline__ uint32_t shift_nb(const uint8_t* lds, uint32_t byte_tab, uint32_t R, uint32_t nb) {
+  const uint8_t* m4 = lds + kTree;
+  uint32_t r;
+  r = lapply(m4, R);
+  R = nb >= 4 ? r : R;
+  r = lapply(m4, R);
+  R = nb >= 8 ? r : R;
+  r = lapply(m4, R);
+  R = nb >= 12 ? r : R;
+  const uint32_t nr = nb & 3u;
+  r = (R >> 8) ^ lds_u32(lds, byte_tab + (R & 255u) * 4u);
+  R = nr >= 1 ? r : R;
+  r = (R >> 8) ^ lds_u32(lds, byte_tab + (R & 255u) * 4u);
+  R = nr >= 2 ? r : R;
+  r = (R >> 8) ^ lds_u32(lds, byte_tab + (R & 255u) * 4u);
+  R = nr >= 3 ? r : R;
+  return R;
+}
+
 // ---- crc32c_rounds_kernel<G, MODE> ---------------------------------------------
 // Variable-length batches in ROUNDS: the wave's lane groups take kGroups blocks
 // at a time, all padded to the round's step count (its largest block, end-
@@ -1201,6 +1253,15 @@ __device__ __forceinline__ void write_result(const CrcParams& p, uint64_t wb_a, 
 // groups, not divergently per block as in the flat kernel; the loads stream
 // across rounds and chunks as in the stream kernel.  For the rounds to be
 // even, each claimed chunk is sorted by step count, largest first.
+//
+// Chunk epilogue (default; kVarRoundEpi keeps the per-round form): when a
+// chunk's descriptors are decoded, each lane (one block per lane) loads its
+// block's tail line and folds the 0..15 tail bytes into one word (tail_raw);
+// a round's end stores only each group's pending word in LDS; after the
+// chunk's last round, lane l finishes slot l's block -- register at E, tail,
+// init of a block under 4 bytes, mask, store or compare -- for all 64 blocks
+// at once.  The per-block work no longer runs once per round in 8 lanes per
+// group, and the steps load no tail lines.
 
 
 
@@ -1216,6 +1277,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   constexpr uint32_t kGroups = 64 / G;
   static_assert(kByteTab == kMainBytes + kLevels * kTreeBytes, "byte table follows the tree");
   constexpr bool kDiag = (VAR & kVarDiag) != 0;  // diagnostics instantiation (crc32c_diag.hip)
+  constexpr bool kBatch = (VAR & (kVarRoundEpi | kVarNoTail)) == 0;  // chunk epilogue
   if (kDiag && p.gate) {  // follow-up of the log-stream kernel
     // gate[0]: precondition flag -> the whole batch; else gate[2] leftover
     // records listed at p.perm (and the log-stream mismatches fold into n_bad)
@@ -1298,6 +1360,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   uint32_t n_chunk = kNone, c_chunk = kNone, t_chunk = kNone;
   // wave-uniform state packed in one word (fewer scalar registers)
   constexpr uint32_t fReady = 1, fRefill = 2, fDry = 4, fDone = 8, fRoundDone = 16, fClaim = 32;
+  constexpr uint32_t fChunkEnd = 64;  // chunk epilogue: the chunk's last step was issued
   uint32_t fl = 0;
   uint32_t stage = 0;  // next pipeline stage due (0: none)
   const uint32_t my = (uint32_t)lane < C ? (uint32_t)lane : C - 1;
@@ -1305,6 +1368,34 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   // shuffles, inverse permutation through the wave's LDS scratch), so each
   // round's blocks have similar lengths while the chunk keeps its locality.
   uint32_t* const sortbuf = reinterpret_cast<uint32_t*>(lds + kByteTab + 1024u + 272u) + wave * 64;
+  // chunk epilogue: the groups' pending words by sorted slot (after all sort scratch)
+  uint32_t* const vbuf = reinterpret_cast<uint32_t*>(lds + kByteTab + 1024u + 272u) + (nwaves + wave) * 64;
+  // chunk epilogue: the tail line (and verify's stored-CRC overflow word) of
+  // the block being decoded, its tail bytes' contribution per bank, and the
+  // chunk being finished ("e" bank: the "c" bank of the previous chunk)
+  uint4 t_tl = make_uint4(0, 0, 0, 0);
+  uint32_t t_t2 = 0, n_tr = 0, c_tr = 0;
+  uint64_t e_u0 = 0;
+  uint32_t e_n = 0, e_rec = 0, e_aux = 0, e_ok = 0, e_tr = 0;
+  typedef __attribute__((address_space(1))) const uint32_t gcu32;
+  auto tail_issue = [&](uint64_t u0, uint32_t n, bool ok) {
+    const uint64_t u1 = u0 + n, E = u1 & ~15ull;
+    // verify: the stored CRC starts at u1 (the line is needed even when nb = 0)
+    t_tl = gload16<VAR | kVarCached>((ok && (kTail2 || (u1 & 15))) ? E : zl);
+    if constexpr (kTail2) t_t2 = *(gcu32*)((ok && u1 + 4 > E + 16) ? E + 16 : zl);
+  };
+  auto tail_finish = [&]() {  // n_tr; verify: the stored CRC into n_aux
+    const uint64_t u1 = n_u0 + n_n, E = u1 & ~15ull;
+    const uint32_t nb = (uint32_t)(u1 - E);
+    const uint32_t ninit = (raw || n_n < 4) ? 0u : ~(any_init ? n_aux : 0u);
+    n_tr = tail_raw<kMainBytes>(lds, kByteTab, t_tl, nb, rel32(n_u0, E, 16), ninit);
+    if constexpr (kTail2) {
+      const uint32_t k = nb >> 2;
+      const uint32_t wlo = sel5(k, t_tl.x, t_tl.y, t_tl.z, t_tl.w, t_t2);
+      const uint32_t whi = sel5(k, t_tl.y, t_tl.z, t_tl.w, t_t2, 0u);
+      n_aux = __builtin_amdgcn_alignbyte(whi, wlo, nb & 3u);  // table/table.cc:434-436
+    }
+  };
   auto sort_nxt = [&]() {
     n_ok = t_ok;
     if (!p.sort_local) return;
@@ -1330,6 +1421,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     n_n = __shfl(n_n, src);
     n_rec = __shfl(n_rec, src);
     n_aux = __shfl(n_aux, src);
+    if constexpr (kBatch) n_tr = __shfl(n_tr, src);
     n_ok = __shfl(t_ok, src);
   };
   auto pipe = [&](uint32_t st) {  // run stage st (its inputs are complete or waited for)
@@ -1372,10 +1464,25 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         n_rec = t_rec;
         n_aux = t_aux;
         n_chunk = t_chunk;
-        sort_nxt();
-        fl |= fReady;
-        stage = 0;
+        if constexpr (kBatch) {
+          tail_issue(n_u0, n_n, t_ok != 0);
+          stage = 4;
+        } else {
+          sort_nxt();
+          fl |= fReady;
+          stage = 0;
+        }
       }
+    } else if (st == 4 && !kLog) {  // (chunk epilogue) the tail bytes, then sort
+      tail_finish();
+      sort_nxt();
+      fl |= fReady;
+      stage = 0;
+    } else if (st == 5) {  // (chunk epilogue, log records) the tail bytes, then sort
+      tail_finish();
+      sort_nxt();
+      fl |= fReady;
+      stage = 0;
     } else if (st == 4) {
       const uint64_t o = ((uint64_t)t_ohi << 32) | t_olo;
       n_u0 = base + o + 6;  // CRC input: type byte + payload
@@ -1390,9 +1497,14 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       n_aux = ls == NOVA_LOG_OK ? (MODE == kLogWrite ? t_aux : (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)))
                                 : ls;
       n_chunk = t_chunk;
-      sort_nxt();
-      fl |= fReady;
-      stage = 0;
+      if constexpr (kBatch) {
+        tail_issue(n_u0, n_n, t_ok != 0 && n_n != 0);
+        stage = 5;
+      } else {
+        sort_nxt();
+        fl |= fReady;
+        stage = 0;
+      }
     }
   };
   auto start_refill = [&](uint32_t chunk) {  // stage 1 of chunk (or none)
@@ -1408,8 +1520,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
 
   // ---- rounds (load side; group-uniform / wave-uniform state) ---------------------
   uint64_t g_u0 = 0, g_u1 = 0, g_lp = 0, g_end = 0, g_rec = 0;
-  uint32_t g_ninit = 0, g_st = 0;
-  bool g_valid = false;
+  uint32_t g_ninit = 0, g_st = 0, g_slot = 0;
+  bool g_valid = false, r_clast = false;
   uint32_t r_idx = R, r_step = 0, r_S = 0;
   constexpr uint64_t kLine = 16 * G;  // one swath of a lane group
   uint64_t g_le = 0;                  // the group's region end on the line grid
@@ -1423,6 +1535,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     for (;;) {
       if (r_idx == R) {  // chunk exhausted: switch to nxt, start loading the one after
         if (!(fl & fReady)) return;  // stall: nxt still in the pipeline
+        if constexpr (kBatch) c_tr = n_tr;
         c_u0 = n_u0;
         c_n = n_n;
         c_rec = n_rec;
@@ -1438,6 +1551,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         fl |= fRefill;
       }
       const uint32_t slot = r_idx * kGroups + (uint32_t)grp;
+      g_slot = slot;
       r_idx++;
       const bool ok = __shfl(c_ok, (int)slot) != 0;
       const uint32_t a_lo = __shfl((uint32_t)c_u0, (int)slot);
@@ -1452,7 +1566,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       g_rec = rec;
       // ~init goes into the data's first 4 bytes; a block shorter than 4 bytes
       // gets it at the end instead (finish_block)
-      g_ninit = (raw || n < 4) ? 0u : ~((kLog || MODE == kTrailer) ? 0u : aux);
+      g_ninit = (raw || n < 4) ? 0u : ~((kLog || MODE == kTrailer || MODE == kVerify) ? 0u : aux);
       g_st = aux;
       g_end = g_u1 & ~15ull;
       // steps on the group's 16G-byte line grid: lines from the one holding
@@ -1465,6 +1579,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       r_S = m;
       if (r_S != 0) break;  // an empty round (past the batch's end): next one
     }
+    // the chunk's last round: no rounds left, or only empty ones (invalid
+    // slots are the chunk's last: positions past the batch, sorted last)
+    r_clast = r_idx == R ||
+              __builtin_amdgcn_readlane((int)c_ok, (int)__builtin_amdgcn_readfirstlane(r_idx * kGroups)) == 0;
     g_lp = g_le - (uint64_t)r_S * kStep;
     r_step = 0;
     // Per-lane 32-bit thresholds for the round's steps (issue/fold run no 64-bit
@@ -1488,9 +1606,24 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   // (an empty asm reading them): the compiler then resolves their loads with
   // exact counts instead of waiting for all loads where its paths merge.
   auto take = [&](bool first) {
+    if (kBatch && (fl & fChunkEnd)) {
+      // The chunk whose last step the previous take issued, for its epilogue
+      // (which runs when that step folds, after this take): copied before a
+      // switch can replace "c", and after the previous chunk's epilogue ran.
+      fl &= ~fChunkEnd;
+      e_u0 = c_u0;
+      e_n = c_n;
+      e_rec = c_rec;
+      e_aux = c_aux;
+      e_ok = c_ok;
+      e_tr = c_tr;
+    }
     if (first) {
       asm volatile("" ::"v"(req), "v"(t_olo), "v"(t_ohi), "v"(t_len), "v"(t_aux));
+      if constexpr (kBatch && kLog)  // stage 4's tail loads, for stage 5
+        asm volatile("" ::"v"(t_tl.x), "v"(t_tl.y), "v"(t_tl.z), "v"(t_tl.w));
       if (stage == 3) pipe(3);
+      else if (kBatch && kLog && stage == 5) pipe(5);
       if ((fl & fRefill) && stage == 0 && !(fl & fReady)) {
         fl &= ~fRefill;
         uint32_t nc = kNone;
@@ -1508,6 +1641,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       asm volatile("" ::"v"(t_rec));
       if constexpr (kLog)
         asm volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(h4), "v"(h5), "v"(h6));
+      if constexpr (kBatch && !kLog) {  // stage 3's tail loads, for stage 4
+        asm volatile("" ::"v"(t_tl.x), "v"(t_tl.y), "v"(t_tl.z), "v"(t_tl.w));
+        if constexpr (kTail2) asm volatile("" ::"v"(t_t2));
+      }
       if (stage == 2) pipe(2);
       else if (stage == 4) pipe(4);
       if (fl & fClaim) {
@@ -1535,7 +1672,9 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       X.d2 = gload16<VAR>((vz && w + 2 >= g_w0) ? pa + 32 * G : zl);
       X.d3 = gload16<VAR>((vz && w + 3 >= g_w0 && (!last || g_l3)) ? pa + 48 * G : zl);
       const bool vl = v && last;
-      if constexpr ((VAR & kVarNoTail) != 0) {  // timing ablation (diagnostics)
+      if constexpr (kBatch) {
+        // (the chunk epilogue loaded the tail lines with the descriptors)
+      } else if constexpr ((VAR & kVarNoTail) != 0) {  // timing ablation (diagnostics)
         X.t = make_uint4(0, 0, 0, 0);
         if constexpr (kTail2) X.t2 = make_uint4(0, 0, 0, 0);
       } else if constexpr (kTail2) {
@@ -1576,18 +1715,84 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     X.pa = g_lp;
     X.u0 = g_u0;
     X.u1 = g_u1;
-    X.rec = g_rec;
+    if constexpr (!kBatch) {
+      X.rec = g_rec;
+      X.st = g_st;
+    } else {
+      X.slot = g_slot;
+      X.cend = last && r_clast;
+    }
     // An invalid group's step (or a stalled one) reads zeros; with no init
     // xor-ed in it leaves the group's zero registers zero for its next block.
     X.ninit = v ? g_ninit : 0u;
-    X.st = g_st;
     X.valid = v;
     X.last = last;
     if (run) {
       g_lp += kStep;
-      if (++r_step == r_S) fl |= fRoundDone;
+      if (++r_step == r_S) fl |= kBatch && r_clast ? (fRoundDone | fChunkEnd) : fRoundDone;
     }
     return live;
+  };
+
+  // Lane l finishes sorted slot l of the chunk whose last round just folded
+  // (its descriptors are in the e bank).  Stores go out after the next step's
+  // loads were issued (fold runs after issue).
+  auto chunk_epilogue = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (kDiag && p.wvar == 3) return;  // timing ablation: no per-block epilogue, no result (WRONG)
+    typedef __attribute__((address_space(1))) uint8_t gu8;
+    typedef __attribute__((address_space(1))) uint32_t gu32;
+    const bool ok = e_ok != 0;
+    const bool wr = ok && (!kDiag || p.wvar < 2);
+    const uint64_t u1 = e_u0 + e_n;
+    const uint32_t nb = (uint32_t)(u1 & 15u);
+    uint32_t R = shift_nb<kMainBytes>(lds, kByteTab, lapply(lds + kMainBytes, vbuf[lane]), nb) ^ e_tr;
+    if (e_n < 4 && !raw) {  // the data ran from a zero register: add M_n(~init)
+      uint32_t l = ~(any_init ? e_aux : 0u);
+      for (uint32_t i = 0; i < 3; i++) {
+        const uint32_t r = (l >> 8) ^ lds_u32(lds, kByteTab + (l & 255u) * 4u);
+        l = i < e_n ? r : l;
+      }
+      R ^= l;
+    }
+    uint32_t crc = raw ? R : ~R;
+    bool bad = false;
+    if constexpr (MODE == kLogWrite) {
+      const bool status_only = e_n == 0;  // a record not read: e_aux holds its status
+      const uint32_t m = mask_crc(crc);  // db/log_writer.cc:113
+      if constexpr ((VAR & kVarOutPos) != 0) {
+        if (wr) {
+          *(gu32*)(p.out + e_rec) = m;
+          *(gu8*)(p.ok_out + e_rec) = (uint8_t)(status_only ? e_aux : (uint32_t)NOVA_LOG_OK);
+        }
+      } else if (wr && !status_only) {
+        store_u32_unaligned((uint8_t*)(e_u0 - 6), m);
+      }
+    } else if constexpr (MODE == kLogVerify) {
+      const uint32_t st = e_n == 0 ? e_aux : (unmask_crc(e_aux) == crc ? 1u : 0u);  // db/log_reader.cc:254-256
+      if (wr) *(gu8*)(p.ok_out + e_rec) = (uint8_t)st;
+      bad = wr && (st == NOVA_LOG_CHECKSUM_MISMATCH || st == NOVA_LOG_BAD_LENGTH);
+    } else if constexpr (MODE == kVerify) {
+      const uint32_t st = unmask_crc(e_aux) == crc ? 1u : 0u;  // table/table.cc:435-437
+      if (wr) *(gu8*)(p.ok_out + e_rec) = (uint8_t)st;
+      bad = wr && !st;
+    } else {
+      if (p.flags & NOVA_CRC32C_APPEND_TYPE) crc = ~byte_step(~crc, (p.flags >> 8) & 0xffu);
+      if constexpr (MODE == kTrailer) {
+        if (wr)
+          store_trailer((uint8_t*)u1, (p.flags >> 8) & 0xffu, mask_crc(crc),
+                        (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
+      } else {
+        if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
+        if (wr) *(gu32*)(p.out + e_rec) = crc;
+      }
+    }
+    if constexpr (MODE == kVerify || MODE == kLogVerify) {
+      const uint64_t b = __builtin_amdgcn_ballot_w64(bad);  // one atomic per chunk
+      if (b && lane == 0 && p.n_bad) atomicAdd(p.n_bad, (uint32_t)__builtin_popcountll(b));
+    }
   };
 
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
@@ -1643,8 +1848,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     }
     // the tail line(s) are used only on a block's last step: consume anyway, so
     // the compiler resolves their loads here with an exact count
-    asm volatile("" ::"v"(Y.t.x), "v"(Y.t.y), "v"(Y.t.z), "v"(Y.t.w));
-    if constexpr (kTail2) asm volatile("" ::"v"(Y.t2.x), "v"(Y.t2.y), "v"(Y.t2.z), "v"(Y.t2.w));
+    if constexpr (!kBatch) {
+      asm volatile("" ::"v"(Y.t.x), "v"(Y.t.y), "v"(Y.t.z), "v"(Y.t.w));
+      if constexpr (kTail2) asm volatile("" ::"v"(Y.t2.x), "v"(Y.t2.y), "v"(Y.t2.z), "v"(Y.t2.w));
+    }
     if (Y.last) {  // wave-uniform: every group ends its block on this step
       // On the line grid lane q's pieces sit at position (q - e) mod G of the
       // 16G-byte swaths that end at E (e = (E mod 16G) / 16); group_fold wants
@@ -1657,6 +1864,11 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       c3 = __shfl(c3, src);
       const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
       c0 = c1 = c2 = c3 = 0;
+      if constexpr (kBatch) {
+        if (q == 0 && Y.valid) vbuf[Y.slot] = v;
+        if (Y.cend) chunk_epilogue();  // wave-uniform
+        return;
+      }
       bool elig = false;
       uint4 piece = Y.t;
       if constexpr (MODE == kLogWrite) {
@@ -1771,7 +1983,8 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   A.d0 = A.d1 = A.d2 = A.d3 = A.t = A.t2 = make_uint4(0, 0, 0, 0);
   A.pa = A.u0 = A.u1 = A.rec = 0;
   A.ninit = A.st = 0;
-  A.valid = A.last = A.head = A.l3 = A.wsec = false;
+  A.valid = A.last = A.head = A.l3 = A.wsec = A.cend = false;
+  A.slot = 0;
   for (;;) {
     take(true);
     issue(B);
@@ -2229,7 +2442,7 @@ int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream
     if (G != 8) return NOVA_E_INVAL;
     hipLaunchKernelGGL((crc32c_rounds_kernel<8, MODE, VAR>), grid, block, lds, stream, p);
     return (int)hipGetLastError();
-  }
+  } else {
   switch (G) {
     case 2: hipLaunchKernelGGL((crc32c_rounds_kernel<2, MODE, VAR>), grid, block, lds, stream, p); break;
     case 4: hipLaunchKernelGGL((crc32c_rounds_kernel<4, MODE, VAR>), grid, block, lds, stream, p); break;
@@ -2237,6 +2450,7 @@ int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream
     default: hipLaunchKernelGGL((crc32c_rounds_kernel<16, MODE, VAR>), grid, block, lds, stream, p); break;
   }
   return (int)hipGetLastError();
+  }
 }
 
 // Descriptor arrays the rounds kernel always loads: absent ones read word 0
@@ -2300,7 +2514,8 @@ int launch_rounds_v(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint3
   p.sched = sched_slot(t, stream);
   if (!p.sched) return NOVA_E_NOMEM;
   const dim3 block(64 * nwaves);
-  const size_t lds = flat_lds_g(G) + 272 + nwaves * 64 * 4;  // + prefix masks, per-wave sort scratch
+  // + prefix masks, per-wave sort scratch (and the chunk epilogue's slot words)
+  const size_t lds = flat_lds_g(G) + 272 + nwaves * 64 * 4 * ((VAR & (kVarRoundEpi | kVarNoTail)) ? 1 : 2);
   return launch_rounds_g<MODE, VAR>(G, dim3(wgs), block, lds, stream, p);
 }
 

@@ -397,10 +397,12 @@ size_t env_size(const char* name, size_t def) {
   return end && *end == 0 ? (size_t)x : def;
 }
 
-// Below this size Extend stays on the host: a 1 MiB buffer is ~40 us on one
-// core (SSE4.2), about the cost of H2D + a launch + D2H + a sync.
+// Below this size Extend stays on the host.  Measured on the GPU box
+// (tools/hook_crossover.py, profiles/r03_hook_crossover.log): the host Extend
+// runs ~33 GiB/s (4 MiB: 117 us), the device path (H2D + kernels + fold) 146 us
+// at 4 MiB and 399 us vs 468 us at 16 MiB: the crossover is ~9 MiB.
 size_t hook_min_bytes() {
-  static const size_t v = env_size("NOVA_HOOK_MIN_BYTES", 1u << 20);
+  static const size_t v = env_size("NOVA_HOOK_MIN_BYTES", 8u << 20);
   return v;
 }
 // Largest device staging buffer the hook allocates (a larger call runs on the host).

@@ -277,7 +277,7 @@ def test_stream_host_matches_device(torch_gpu, oracle):
 
 def test_accelerated_hook(torch_gpu, oracle):
     """port::AcceleratedCRC32C self-test (util/crc32c.cc:477-485), then sizes on
-    both sides of NOVA_HOOK_MIN_BYTES (1 MiB): the 1-byte type-byte Extend of
+    both sides of NOVA_HOOK_MIN_BYTES (8 MiB): the 1-byte type-byte Extend of
     table/table_builder.cc:203 and a 4 KiB block never launch a kernel; large
     buffers run on the GPU."""
     assert C.AcceleratedCRC32C(0, b"TestCRCBuffer") == 0xDCBC59FA
@@ -287,7 +287,7 @@ def test_accelerated_hook(torch_gpu, oracle):
         assert C.AcceleratedCRC32C(init, d) == oracle.extend(init, d)
     s1 = C.port_stats()
     assert s1["device"] == s0["device"] and s1["host"] - s0["host"] == 3
-    for n, init in [(1 << 20, 0x1234), (3 << 20 | 77, 9)]:
+    for n, init in [(8 << 20, 0x1234), (9 << 20 | 77, 9)]:
         d = splitmix64_bytes(n, n).tobytes()
         assert C.AcceleratedCRC32C(init, d) == oracle.extend(init, d)
     s2 = C.port_stats()
@@ -302,7 +302,7 @@ def test_accelerated_hook_device_failure_falls_back(torch_gpu, oracle, tmp_path)
     code = ("import sys; sys.path.insert(0, %r)\n"
             "from novalsm_amd import crc32c as C\n"
             "from novalsm_amd.synth import splitmix64_bytes\n"
-            "d = splitmix64_bytes(3, 2 << 20).tobytes()\n"
+            "d = splitmix64_bytes(3, 9 << 20).tobytes()\n"
             "print(C.AcceleratedCRC32C(7, d), C.port_stats()['fallback'], C.port_stats()['device'])\n"
             ) % (str(__import__('pathlib').Path(__file__).resolve().parents[1]),)
     env = dict(__import__('os').environ, NOVA_HOOK_MAX_STAGING=str(1 << 20))
@@ -310,7 +310,7 @@ def test_accelerated_hook_device_failure_falls_back(torch_gpu, oracle, tmp_path)
                        timeout=120)
     assert r.returncode == 0, r.stderr
     crc, fb, devc = (int(x) for x in r.stdout.split()[-3:])
-    d = splitmix64_bytes(3, 2 << 20).tobytes()
+    d = splitmix64_bytes(3, 9 << 20).tobytes()
     assert crc == oracle.extend(7, d) and fb == 1 and devc == 0
 
 
@@ -322,7 +322,7 @@ def test_no_device_memory_growth(torch_gpu, oracle):
     stream's slot."""
     torch = torch_gpu
     import threading
-    d = splitmix64_bytes(4, (1 << 20) + 5).tobytes()
+    d = splitmix64_bytes(4, (8 << 20) + 5).tobytes()  # above NOVA_HOOK_MIN_BYTES: the device path
     want = oracle.extend(0, d)
     host = torch.from_numpy(splitmix64_bytes(6, 64 * 4096)).pin_memory()
     C.AcceleratedCRC32C(0, d)

@@ -110,7 +110,7 @@ def test_hook_never_returns_a_wrong_crc_without_gpu(oracle):
         pytest.skip("GPU present: covered by the gpu suite")
     before = C.port_stats()
     assert C.AcceleratedCRC32C(0, b"TestCRCBuffer") == 0xDCBC59FA  # util/crc32c.cc:479-481
-    for n, init in [(1, 0), (4096, 5), ((1 << 20) + 77, 0x1234), (3 << 20, 0xFFFFFFFF)]:
+    for n, init in [(1, 0), (4096, 5), ((8 << 20) + 77, 0x1234), (9 << 20, 0xFFFFFFFF)]:
         d = splitmix64_bytes(n, n).tobytes()
         assert C.AcceleratedCRC32C(init, d) == oracle.extend(init, d), n
     after = C.port_stats()

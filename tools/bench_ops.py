@@ -160,10 +160,12 @@ def main() -> int:
             # 8 = two passes, the second reading, patching and storing whole
             # 64-B pieces, 3 = whole 64-B pieces, 4 = the same non-temporal, 5 = pieces and
             # 6 = the product form without result writes (timing only)
-            for var, name in ((2, "trailers_two_pass"), (8, "trailers_two_pass_pieces"),
+            # (round 3: the product is 8, the CRC pass then whole-piece stores)
+            for var, name in (() if args.no_ablations else (
+                              (9, "trailers_one_pass"), (2, "trailers_two_pass"),
                               (3, "trailers_pieces"),
                               (4, "trailers_pieces_nt"), (5, "trailers_pieces_no_writes"),
-                              (6, "trailers_no_writes"), (7, "trailers_no_epilogue")):
+                              (6, "trailers_crc_pass_only"), (7, "trailers_crc_pass_no_epilogue"))):
                 with C.diagnostics() as D:
                     D.nova_diag_set_trailer_single_pass(var)
                     sec1 = timed(torch, tw, args.steps, args.warmup, stream)
@@ -184,6 +186,14 @@ def main() -> int:
             ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
             emit("verify", wl, sum_len + 6 * n, sec, ok, {"image": image})
             sweep("verify", vf, sum_len + 6 * n)
+            for vv, name in (() if args.no_ablations else ((2048, "verify_round_epilogue"),)):
+                with C.diagnostics() as D:  # A/B: the per-round epilogue (rounds 1-2)
+                    D.nova_diag_set_variant(vv)
+                    sec1 = timed(torch, vf, args.steps, args.warmup, stream)
+                    D.nova_diag_set_variant(0)
+                gbs1 = (sum_len + 6 * n) / sec1 / 1e9
+                print(json.dumps({"sweep": name, "image": image, "GBps": round(gbs1, 1),
+                                  "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
             with C.diagnostics() as D:  # timing ablation: no ok/mismatch writes
                 D.nova_diag_set_trailer_single_pass(6)
                 sec1 = timed(torch, vf, args.steps, args.warmup, stream)

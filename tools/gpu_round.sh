@@ -27,7 +27,8 @@ WORKLOADS=${WORKLOADS:-cfg3,sst4k,log}
 [[ $STEPS == *trun* ]] && step bench_torchrun 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr 127.0.0.1 --master-port=29533 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
 [[ $STEPS == *cfg3* ]] && step bench_config3 600 python bench.py --config 3 --no-cpu-baseline
 [[ $STEPS == *cfg4* ]] && step bench_config4 600 python bench.py --config 4 --no-cpu-baseline
-[[ $STEPS == *ops* ]] && step bench_ops 600 python -u tools/bench_ops.py
+[[ $STEPS == *ops* ]] && step bench_ops 600 python -u tools/bench_ops.py ${OPS_ARGS:-}
 [[ $STEPS == *sweep* ]] && step sweep 600 python -u tools/sweep_flat.py --workloads "$WORKLOADS" --variants "$VARIANTS"
+[[ $STEPS == *cross* ]] && step hook_crossover 600 python -u tools/hook_crossover.py
 [[ $STEPS == *prof* ]] && step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline
 exit 0

@@ -1,6 +1,7 @@
 #!/bin/bash
 # HBM traffic of the CRC kernel from PMC counters, in separate passes (no
 # sys/runtime tracing next to --pmc).  Usage: bash tools/pmc.sh [config]
+# (config: 2, 3, 4, sst4k_trailers, sst4k_verify -- bench.py's workloads)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -26,42 +26,87 @@ def kernel_label(name: str) -> str:
     return f"{m.group(1)}<{', '.join(args)}>"
 
 
-KERNELS = collections.Counter()
+# the kernels of one step of each workload (the first is the one whose
+# dispatches count the steps) -- bench.py's dispatches
+STEP_KERNELS = {
+    "2": ["crc32c_stream_kernel<8, 0>"],
+    "3": ["crc32c_units_kernel<16, 0>"],
+    "4": ["crc32c_stream_kernel<16, 0>"],
+    "sst4k_trailers": ["crc32c_rounds_kernel<8, 0>", "trailer_layout_kernel", "trailer_rmw_kernel"],
+    "sst4k_verify": ["crc32c_rounds_kernel<8, 2>"],
+}
 
 
-def per_dispatch(ctr, cfg):
-    vals = []
+def label(name: str) -> str:
+    m = re.search(r"(trailer_\w+_kernel|log_\w+_kernel)", name)
+    return m.group(1) if m and "crc32c_" not in name else kernel_label(name)
+
+
+def per_kernel(ctr, cfg):
+    vals = collections.defaultdict(list)
     for path in glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc{cfg}", ctr, "**", "*counter_collection.csv"),
                           recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if "crc32c" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
-                    vals.append(float(row["Counter_Value"]))
-                    KERNELS[kernel_label(row["Kernel_Name"])] += 1
+                if row.get("Counter_Name") == ctr:
+                    vals[label(row.get("Kernel_Name", ""))].append(float(row["Counter_Value"]))
     return vals
+
+
+def step_bytes(vals, kernels):
+    """Median per step: the main kernel's median plus the others' medians."""
+    tot = 0.0
+    for k in kernels:
+        v = sorted(vals.get(k, []))
+        if v:
+            tot += v[len(v) // 2]
+    return tot
+
+
+def algorithmic(cfg):
+    sys.path.insert(0, ROOT)
+    import bench
+    import numpy as np
+    n = 1 << 20
+    if cfg == "2":
+        return 1 << 32
+    if cfg == "4":
+        return 1 << 34
+    if cfg == "3":
+        return int(bench.config3_layout(n, 3)[1].astype(np.uint64).sum())
+    if cfg in ("sst4k_trailers", "sst4k_verify"):
+        s = int(bench.sst4k_layout(n, 5)[1].astype(np.uint64).sum())
+        return s + 5 * n if cfg == "sst4k_trailers" else s + 6 * n
+    return None
 
 
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "2"
-    fetch = per_dispatch("FETCH_SIZE", cfg)
-    write = per_dispatch("WRITE_SIZE", cfg)
-    if not fetch:
-        print("no FETCH_SIZE rows found")
+    kernels = STEP_KERNELS[cfg]
+    fetch = per_kernel("FETCH_SIZE", cfg)
+    write = per_kernel("WRITE_SIZE", cfg)
+    if not fetch.get(kernels[0]):
+        print(f"no FETCH_SIZE rows for {kernels[0]}; kernels seen: {sorted(fetch)}")
         sys.exit(1)
-    f_med = sorted(fetch)[len(fetch) // 2]
-    w_med = sorted(write)[len(write) // 2] if write else None
-    algo = {"2": 1 << 32, "3": 30060563723, "4": 1 << 34}.get(cfg)  # config 3: bench.config3_layout sum
+    f_kb = step_bytes(fetch, kernels)
+    w_kb = step_bytes(write, kernels) if write else None
+    sys.path.insert(0, ROOT)
+    import bench
+    algo = algorithmic(cfg)
     res = {
-        "config": int(cfg),
-        "dispatches": len(fetch),
-        "FETCH_SIZE_kB_median": f_med,
-        "WRITE_SIZE_kB_median": w_med,
-        "hbm_read_bytes_per_launch": 2 * f_med * 1024,
-        "hbm_write_bytes_per_launch": None if w_med is None else w_med * 1024,
-        "hbm_bytes_per_launch": 2 * f_med * 1024 + (0 if w_med is None else w_med * 1024),
+        "config": cfg,
+        "kernels": kernels,
+        "dispatches": len(fetch[kernels[0]]),
+        "FETCH_SIZE_kB_per_step": f_kb,
+        "WRITE_SIZE_kB_per_step": w_kb,
+        "hbm_read_bytes_per_launch": 2 * f_kb * 1024,
+        "hbm_write_bytes_per_launch": None if w_kb is None else w_kb * 1024,
+        "hbm_bytes_per_launch": 2 * f_kb * 1024 + (0 if w_kb is None else w_kb * 1024),
         "algorithmic_bytes_per_launch": algo,
-        "correction": "read = 2 x FETCH_SIZE (gfx950 half-count, MI355X_MICROARCH.md HBM section)",
-        "kernel": KERNELS.most_common(1)[0][0] if KERNELS else None,
+        "correction": "read = 2 x FETCH_SIZE (gfx950 half-count, MI355X_MICROARCH.md HBM section); "
+                      "WRITE_SIZE uncorrected",
+        "kernel": kernels[0],
+        "src_sha16": bench.kernel_src_sha16(),
         "commit": os.environ.get("PMC_COMMIT"),
     }
     if algo:
