@@ -327,8 +327,12 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
             # algorithmic bytes: block + type byte + stored CRC read, one flag written
             bytes_step = sum_len + 6 * n
         dispatch = C.describe(n, 4096 + 128, 0, variable=True)
-        dispatch["op"] = "nova_sstable_write_trailers" if wl["kind"] == "sst_trailers" \
-            else "nova_sstable_verify_blocks"
+        if wl["kind"] == "sst_trailers":  # two passes: the CRC pass in store mode
+            dispatch.update({"op": "nova_sstable_write_trailers",
+                             "kernels": ["trailer_layout_kernel", dispatch["kernel"], "trailer_rmw_kernel"]})
+        else:
+            dispatch.update({"op": "nova_sstable_verify_blocks",
+                             "kernel": dispatch["kernel"].replace(", 0>", ", 2>")})  # MODE 2: verify
     else:
         offs_np, lens_np, total = config3_layout(n, seed)
         buf = torch.empty(total + 64, dtype=torch.uint8, device=ctx.dev)
