@@ -143,6 +143,25 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
                                   size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
                                   uint32_t flags, void* stream);
 
+/* ---- coalescing queue for concurrent per-SSTable callers -----------------
+ * The same operations as nova_sstable_write_trailers / _verify_blocks (same
+ * arguments, same results), host-synchronous: the call returns when the
+ * trailers / ok flags / n_bad are written.  Concurrent calls from different
+ * threads are grouped into one launch (crc32c_queue.hip):
+ * NovaLSM's compaction and reader threads each checksum one SSTable per call
+ * (ltc/stoc_file_client_impl.cpp:274-289, table/table.cc:425-441), too little
+ * work per launch to fill the device alone.  The batch waits for the work
+ * queued on `stream` before the call (an event), so the image may still be
+ * in flight there.  A table of more than 2^20 blocks runs directly on
+ * `stream`.  NOVA_SST_QUEUE_SLOTS=1 keeps one batch in flight (default 2). */
+int nova_sst_queue_write_trailers(void* buf, const uint64_t* offsets, const uint32_t* sizes,
+                                  size_t n_blocks, uint32_t flags, void* stream);
+int nova_sst_queue_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
+                                 size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
+                                 void* stream);
+/* Batches launched, requests served, most tables in one batch (this device). */
+int nova_sst_queue_stats(uint64_t* batches, uint64_t* requests, uint64_t* max_tables_per_batch);
+
 /* ---- MANIFEST / write-ahead log records ----------
  * buf holds buf_len bytes of a log file image starting at a 32 KiB log-block
  * boundary (db/log_format.h:27, kBlockSize).  record_offsets[i] (relative to

@@ -58,6 +58,9 @@ _SIG = {
     "nova_sstable_write_trailers": (_i32, [_vp, _vp, _vp, _sz, _u32, _vp]),
     "nova_sstable_verify_blocks": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "nova_sstable_verify_blocks_ex": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _u32, _vp]),
+    "nova_sst_queue_write_trailers": (_i32, [_vp, _vp, _vp, _sz, _u32, _vp]),
+    "nova_sst_queue_verify_blocks": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "nova_sst_queue_stats": (_i32, [_vp, _vp, _vp]),
     "nova_crc32c_stream_host": (_i32, [_vp, _u64, _u32, _sz, _vp, _u32, _sz, _i32]),
     "nova_crc32c_batch_host": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _sz, _i32]),
     "nova_sstable_write_trailers_host": (_i32, [_vp, _vp, _vp, _sz, _u32, _sz, _i32]),
@@ -88,6 +91,7 @@ _DIAG_SIG = {
     "nova_diag_set_rounds_sort": (None, [_i32]),
     "nova_diag_set_log_window": (None, [_i32]),
     "nova_diag_host_extend_loop": (_u32, [_vp, _sz, ctypes.c_uint64]),
+    "nova_diag_lane_xor_probe": (_i32, [_vp, _vp, _vp, _vp]),
     "nova_diag_set_trailer_single_pass": (None, [_i32]),
     "nova_diag_set_burst_lanes": (None, [_i32]),
     "nova_diag_set_split": (None, [_i32]),
@@ -360,6 +364,44 @@ def verify_blocks(buf, offsets, sizes, stream=None, ok=None, bad=None, hint_larg
         rc = _L().nova_sstable_verify_blocks(*args, _stream_ptr(stream))
     _check(rc, "nova_sstable_verify_blocks")
     return ok, bad
+
+
+def queue_write_trailers(buf, offsets, sizes, type_byte: int = 0, tb_quirk: bool = False, stream=None):
+    """nova_sst_queue_write_trailers: write_trailers through the coalescing
+    queue (host-synchronous; concurrent callers share launches)."""
+    _require_gpu()
+    if sizes.numel() != offsets.numel():
+        raise NovaError("offsets/sizes size mismatch")
+    flags = TYPE(type_byte) | (TB_QUIRK if tb_quirk else 0)
+    dv = buf.device
+    rc = _L().nova_sst_queue_write_trailers(_data(buf, "buf"), _arg(offsets, "offsets", _u64_dtypes(), dv),
+                                            _arg(sizes, "sizes", _u32_dtypes(), dv),
+                                            int(offsets.numel()), flags, _stream_ptr(stream))
+    _check(rc, "nova_sst_queue_write_trailers")
+    return buf
+
+
+def queue_verify_blocks(buf, offsets, sizes, ok, bad=None, stream=None):
+    """nova_sst_queue_verify_blocks: verify_blocks through the coalescing
+    queue (host-synchronous).  `bad` accumulates (zero it first)."""
+    import torch
+    _require_gpu()
+    n = int(offsets.numel())
+    if sizes.numel() != n:
+        raise NovaError("offsets/sizes size mismatch")
+    dv = buf.device
+    rc = _L().nova_sst_queue_verify_blocks(_data(buf, "buf"), _arg(offsets, "offsets", _u64_dtypes(), dv),
+                                           _arg(sizes, "sizes", _u32_dtypes(), dv), n,
+                                           _arg(ok, "ok", (torch.uint8,), dv, n),
+                                           _arg(bad, "bad", _u32_dtypes(), dv, 1), _stream_ptr(stream))
+    _check(rc, "nova_sst_queue_verify_blocks")
+    return ok, bad
+
+
+def queue_stats() -> dict:
+    v = [ctypes.c_uint64(0) for _ in range(3)]
+    _check(_L().nova_sst_queue_stats(*[ctypes.byref(x) for x in v]), "nova_sst_queue_stats")
+    return {"batches": v[0].value, "requests": v[1].value, "max_tables": v[2].value}
 
 
 def log_write_crcs(buf, record_offsets, stream=None, buf_len: Optional[int] = None):

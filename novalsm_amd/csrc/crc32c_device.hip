@@ -1023,6 +1023,14 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   }
 }
 
+}  // namespace
+
+namespace nova_dev {
+int dispatch(int mode, CrcParams& p, hipStream_t stream) { return run(mode, p, false, 0, stream); }
+}  // namespace nova_dev
+
+namespace {
+
 // The device's CU count for plan reports (the same value run() uses), without
 // initialising the device: 256 (MI355X) when no table set exists yet.
 uint32_t cus_hint() {

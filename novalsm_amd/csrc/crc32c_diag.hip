@@ -1009,6 +1009,23 @@ __global__ void __launch_bounds__(1024) read_ceiling_kernel(const uint8_t* base,
 }
 
 
+// lane_xor<K> (crc32c_kernels.hpp) next to __shfl_xor for K = 1 .. 32 on one
+// wave64: out[k * 64 + l] = lane_xor<2^k>(in[l]), ref[k * 64 + l] = __shfl_xor;
+// out[6 * 64 + l] = wave_max(in[l]).
+__global__ void __launch_bounds__(64) lane_xor_probe_kernel(const uint32_t* in, uint32_t* out,
+                                                            uint32_t* ref) {
+  const uint32_t l = threadIdx.x;
+  const uint32_t v = in[l];
+  out[0 * 64 + l] = lane_xor<1>(v);
+  out[1 * 64 + l] = lane_xor<2>(v);
+  out[2 * 64 + l] = lane_xor<4>(v);
+  out[3 * 64 + l] = lane_xor<8>(v);
+  out[4 * 64 + l] = lane_xor<16>(v);
+  out[5 * 64 + l] = lane_xor<32>(v);
+  for (int k = 0; k < 6; k++) ref[k * 64 + l] = (uint32_t)__shfl_xor((int)v, 1 << k);
+  out[6 * 64 + l] = wave_max(v);
+}
+
 // ---- host ----------------------------------------------------------------------
 constexpr uint64_t kLogWindowMin = 1u << 15;  // log records: whole-piece CRC-field stores from here
 constexpr int kNotTaken = -999;               // a hook found nothing to do
@@ -1538,6 +1555,13 @@ void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
 void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
 
 void nova_diag_set_log_window(int records) { g_tune_logwin.store(records); }
+
+int nova_diag_lane_xor_probe(const uint32_t* in_dev, uint32_t* out_dev, uint32_t* ref_dev, void* stream) {
+  if (!in_dev || !out_dev || !ref_dev) return NOVA_E_INVAL;
+  hipLaunchKernelGGL(lane_xor_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, in_dev, out_dev,
+                     ref_dev);
+  return (int)hipGetLastError();
+}
 
 // The product's host Extend (crc32c_host.cpp, linked into both libraries)
 // called reps times on one buffer, for timing without a Python call per block.

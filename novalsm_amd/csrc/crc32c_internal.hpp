@@ -139,6 +139,9 @@ struct DevTables {
 
 DevTables* tables(int* err);
 uint32_t* sched_slot(DevTables* t, hipStream_t stream);
+// The product dispatch (crc32c_device.hip run()) for a variable-length batch
+// described by p (base may be 0 with absolute offsets): crc32c_queue.hip.
+int dispatch(int mode, CrcParams& p, hipStream_t stream);
 int gindex(int G);
 int upload_u32(uint32_t** dst, const uint32_t* src, size_t n);  // hipMalloc + copy
 

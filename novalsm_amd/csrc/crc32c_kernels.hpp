@@ -358,10 +358,21 @@ __device__ __forceinline__ uint4 lds_u128(uint32_t a) {
 }
 __device__ __forceinline__ int32_t clamp16(int32_t x) { return x < 0 ? 0 : (x > 16 ? 16 : x); }
 
-// v of lane (lane ^ K), K a power of two known at compile time.  Within a
-// 16-lane row without an LDS round trip (__shfl_xor is a ds_bpermute): DPP for
-// k <= 8 (quad_perm; xor 4 = row_half_mirror after quad_perm [3,2,1,0]; xor 8 =
-// row_mirror after row_half_mirror); 16 and 32 cross rows (ds_bpermute).
+// v of lane (lane ^ K), K a power of two known at compile time, without an
+// LDS round trip (__shfl_xor is a ds_bpermute, which also takes LDS bandwidth
+// from the table lookups):
+//   K <= 8: DPP within a 16-lane row (quad_perm; xor 4 = row_half_mirror after
+//     quad_perm [3,2,1,0]; xor 8 = row_mirror after row_half_mirror);
+//   K = 16: v_permlane16_swap(v, v) swaps the odd rows of its first operand
+//     with the even rows of its second: the first result holds rows
+//     (r0, r0, r2, r2) of v, the second (r1, r1, r3, r3), so lane l takes the
+//     second in even rows and the first in odd rows;
+//   K = 32: v_permlane32_swap(v, v) swaps the upper half of the first operand
+//     with the lower half of the second: the first result is (lo, lo), the
+//     second (hi, hi); the lower half takes the second.
+// (Round 2 tried the swaps with one result for every lane -- a rotation, not
+// a lane-xor, for half the lanes -- and dropped them after a wrong CRC;
+// tests/test_gpu_parity.py::test_lane_xor pins every K against __shfl_xor.)
 template <int K>
 __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
   if constexpr (K == 1) {
@@ -374,22 +385,32 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
   } else if constexpr (K == 8) {
     return (uint32_t)__builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false),
                                               0x140, 0xF, 0xF, false);
+  } else if constexpr (K == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return ((threadIdx.x >> 4) & 1u) ? r[0] : r[1];
   } else {
-    // 16, 32: ds_bpermute.  With the gfx950 permlane swaps here the burst
-    // kernel's trailer launch took 2.4 us longer at 16 blocks and one
-    // log-stream experiment case (diagnostics build) failed, so they are not used.
-    static_assert(K == 16 || K == 32, "lane_xor: 1, 2, 4, 8, 16 or 32");
-    return (uint32_t)__shfl_xor((int)v, K);
+    static_assert(K == 32, "lane_xor: 1, 2, 4, 8, 16 or 32");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return ((threadIdx.x >> 5) & 1u) ? r[0] : r[1];
   }
 }
-// max over the wave's 64 lanes (every lane gets it)
+// max over the wave's 64 lanes, wave-uniform: DPP xor levels within each
+// 16-lane row, then the four row maxima read into scalar registers
+// (v_readlane) and combined on the scalar unit.  (The cross-row levels as
+// permlane swaps -- both swap results hold a lane's own value and its
+// partner's, so max(r[0], r[1]) needs no lane select -- measured 0.5 points
+// slower on log verify than ds_bpermute; this form leaves no cross-lane VALU
+// level and hands the callers an SGPR round length.)
 __device__ __forceinline__ uint32_t wave_max(uint32_t m) {
-  m = max(m, lane_xor<32>(m));
-  m = max(m, lane_xor<16>(m));
   m = max(m, lane_xor<8>(m));
   m = max(m, lane_xor<4>(m));
   m = max(m, lane_xor<2>(m));
-  return max(m, lane_xor<1>(m));
+  m = max(m, lane_xor<1>(m));
+  const uint32_t a = max((uint32_t)__builtin_amdgcn_readlane((int)m, 0),
+                         (uint32_t)__builtin_amdgcn_readlane((int)m, 16));
+  const uint32_t b = max((uint32_t)__builtin_amdgcn_readlane((int)m, 32),
+                         (uint32_t)__builtin_amdgcn_readlane((int)m, 48));
+  return max(a, b);
 }
 
 // Fold the 4G pending stream words of a lane group (4 per lane, lane q holds

@@ -275,6 +275,28 @@ def test_stream_host_matches_device(torch_gpu, oracle):
     assert np.array_equal(got2, got[:300])
 
 
+def test_lane_xor(torch_gpu):
+    """the kernels' lane_xor<K> (DPP for K <= 8, the gfx950
+    v_permlane16/32_swap for 16 and 32) equals __shfl_xor on every lane of a
+    wave64 for every K, on distinct lane values; wave_max (the swaps without a
+    lane select) gives every lane the wave's maximum."""
+    torch = torch_gpu
+    rng = np.random.default_rng(5)
+    vals = rng.permutation(2**31)[:64].astype(np.uint32)
+    inp = dev(torch, vals.view(np.int32))
+    out = torch.zeros(7 * 64, dtype=torch.int32, device="cuda")
+    ref = torch.zeros(6 * 64, dtype=torch.int32, device="cuda")
+    D = C.load_diag()
+    assert D.nova_diag_lane_xor_probe(inp.data_ptr(), out.data_ptr(), ref.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    o, r = u32(out).reshape(7, 64), u32(ref).reshape(6, 64)
+    lanes = np.arange(64)
+    for k in range(6):
+        assert np.array_equal(r[k], vals[lanes ^ (1 << k)]), k  # the reference itself
+        assert np.array_equal(o[k], r[k]), (1 << k, np.nonzero(o[k] != r[k])[0][:8])
+    assert np.all(o[6] == vals.max())
+
+
 def test_accelerated_hook(torch_gpu, oracle):
     """port::AcceleratedCRC32C self-test (util/crc32c.cc:477-485), then sizes on
     both sides of NOVA_HOOK_MIN_BYTES (8 MiB): the 1-byte type-byte Extend of
@@ -830,6 +852,96 @@ def test_concurrent_split_path(torch_gpu, oracle):
         want = oracle.batch_strided(bufs[t].cpu().numpy(), length, length, n)
         for r in results[i]:
             assert np.array_equal(r, want), i
+
+
+def test_sst_queue_concurrent(torch_gpu, oracle):
+    """Coalescing queue (nova_sst_queue_*): 12 host threads,
+    each on its own stream with its own SSTable image (ragged layouts, 0 to 3000
+    blocks, gaps between blocks, three trailer types, one with the TableBuilder
+    quirk), write trailers then verify with corrupted blocks, many calls each.
+    The image is filled asynchronously on the caller's stream right before the
+    first call (the batch must wait for it).  Every trailer equals the oracle's
+    and every verify flags exactly the corrupted blocks; the calls shared
+    launches (batches < requests)."""
+    torch = torch_gpu
+    import threading
+    T, R = 12, 12
+    rng = np.random.default_rng(77)
+    sizes_n = [0, 1, 7, 64, 500, 3000, 1, 33, 1200, 2048, 250, 9]
+    tabs = []
+    for t in range(T):
+        n = sizes_n[t]
+        sz = rng.integers(1, 8193, n).astype(np.uint32)
+        gap = rng.integers(0, 4, n).astype(np.uint64)
+        offs = np.zeros(n, np.uint64)
+        if n:
+            offs[1:] = np.cumsum(sz[:-1].astype(np.uint64) + 5 + gap[:-1])
+        total = int(offs[-1] + sz[-1] + 5) if n else 16
+        bad = rng.choice(n, size=min(n, 1 + t % 4), replace=False) if n else np.zeros(0, np.int64)
+        tabs.append(dict(n=n, sz=sz, offs=offs, total=total, bad=np.sort(bad), type=t % 3,
+                         quirk=(t == 5)))
+    before = C.queue_stats()
+    results, errors = [None] * T, []
+
+    def work(t):
+        try:
+            tb = tabs[t]
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                img = torch.empty(tb["total"] + 64, dtype=torch.uint8, device="cuda")
+                offs = torch.from_numpy(tb["offs"].view(np.int64)).to("cuda", non_blocking=False)
+                szs = torch.from_numpy(tb["sz"].view(np.int32)).to("cuda", non_blocking=False)
+                C.fill_splitmix64(img, 500 + t, stream=s)  # in flight when the queue is called
+                for _ in range(R):
+                    C.queue_write_trailers(img, offs, szs, tb["type"], tb["quirk"], stream=s)
+                good = img.cpu().numpy().copy()
+                for j in tb["bad"]:  # corrupt one byte of each chosen block, on s
+                    img[int(tb["offs"][j])] ^= 0x5A
+                oks, bads = [], []
+                for _ in range(R):
+                    ok = torch.full((max(tb["n"], 1),), 7, dtype=torch.uint8, device="cuda")
+                    nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+                    C.queue_verify_blocks(img, offs, szs, ok, nb, stream=s)
+                    oks.append(ok.cpu().numpy()[:tb["n"]])
+                    bads.append(int(nb.item()))
+            s.synchronize()
+            results[t] = (good, oks, bads)
+        except Exception as e:  # pragma: no cover
+            errors.append((t, e))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    calls = 0
+    for t in range(T):
+        tb, (good, oks, bads) = tabs[t], results[t]
+        n = tb["n"]
+        calls += 2 * R if n else 0
+        if n:
+            want = oracle.batch(good, tb["offs"], tb["sz"], None,
+                                flags=C.APPEND_TYPE | C.MASK_OUTPUT | C.TYPE(tb["type"]))
+            for j in range(n):
+                o = int(tb["offs"][j] + tb["sz"][j])
+                tr = good[o:o + 5]
+                assert tr[0] == tb["type"], (t, j)
+                word = int(want[j]).to_bytes(4, "little")
+                if tb["quirk"]:
+                    word = word[:3] + b"!"
+                assert tr[1:].tobytes() == word, (t, j)
+        expect = np.ones(n, np.uint8)
+        if tb["quirk"] and n:  # TableBuilder's '!' trailer (table/table_builder.cc:206)
+            expect[:] = (want >> 24) == 0x21  # verifies only where the CRC's top byte is '!'
+        expect[tb["bad"]] = 0
+        for ok, nb in zip(oks, bads):
+            assert np.array_equal(ok, expect), (t, np.nonzero(ok != expect)[0][:8])
+            assert nb == int((expect == 0).sum()), (t, nb)
+    after = C.queue_stats()
+    served = after["requests"] - before["requests"]
+    assert served == calls, (served, calls)
+    assert after["batches"] - before["batches"] < served, (before, after)
 
 
 @pytest.mark.parametrize("kernel", ["default", "logstream"])
