@@ -150,10 +150,11 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
  * threads are grouped into one launch (crc32c_queue.hip):
  * NovaLSM's compaction and reader threads each checksum one SSTable per call
  * (ltc/stoc_file_client_impl.cpp:274-289, table/table.cc:425-441), too little
- * work per launch to fill the device alone.  The batch waits for the work
- * queued on `stream` before the call (an event), so the image may still be
- * in flight there.  A table of more than 2^20 blocks runs directly on
- * `stream`.  NOVA_SST_QUEUE_SLOTS=1 keeps one batch in flight (default 2). */
+ * work per launch to fill the device alone.  Work queued on `stream` before
+ * the call (the image, its descriptors) completes first: the call
+ * synchronises `stream` when it is busy.  A call alone in the queue runs as
+ * the plain call on `stream`; a table of more than 2^20 blocks always does.
+ * NOVA_SST_QUEUE_SLOTS (1..4, default 2): batches in flight at once. */
 int nova_sst_queue_write_trailers(void* buf, const uint64_t* offsets, const uint32_t* sizes,
                                   size_t n_blocks, uint32_t flags, void* stream);
 int nova_sst_queue_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,

@@ -92,6 +92,7 @@ _DIAG_SIG = {
     "nova_diag_set_log_window": (None, [_i32]),
     "nova_diag_host_extend_loop": (_u32, [_vp, _sz, ctypes.c_uint64]),
     "nova_diag_lane_xor_probe": (_i32, [_vp, _vp, _vp, _vp]),
+    "nova_diag_copy_ceiling": (_i32, [_vp, _vp, _sz, _vp, _vp, _i32, _i32, _vp]),
     "nova_diag_set_trailer_single_pass": (None, [_i32]),
     "nova_diag_set_burst_lanes": (None, [_i32]),
     "nova_diag_set_split": (None, [_i32]),
@@ -113,9 +114,13 @@ def lib_path() -> str:
     return _build.LIB
 
 
-def _open(path: str, sig: dict) -> ctypes.CDLL:
+def _open(path: str, sig: dict, optional: tuple = ()) -> ctypes.CDLL:
+    """Bind `sig`; a name in `optional` (diagnostics entry points) may be
+    absent -- an older diagnostics build in an A/B -- and then fails when used."""
     L = ctypes.CDLL(path)
     for name, (res, args) in sig.items():
+        if name in optional and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -145,7 +150,7 @@ def load_diag() -> ctypes.CDLL:
     if _diag is None:
         if not os.path.exists(_build.DIAG_LIB):
             raise ImportError(f"diagnostics library missing: {_build.DIAG_LIB}")
-        _diag = _open(_build.DIAG_LIB, {**_SIG, **_DIAG_SIG})
+        _diag = _open(_build.DIAG_LIB, {**_SIG, **_DIAG_SIG}, tuple(_DIAG_SIG))
     return _diag
 
 

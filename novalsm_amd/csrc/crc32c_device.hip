@@ -758,9 +758,12 @@ int launch_stream(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
   return launch_stream_v<0>(G, p, t, stream);
 }
 
-// the rounds kernel, 6144 on 256 CUs) go to the burst kernel, one wave per
-// block on the compact tables, unless tuning forces a kernel.
-uint64_t burst_max(uint32_t cus) { return 2ull * cus * flat_waves(); }
+// SSTable-block batches up to 4 blocks per wave slot of the rounds kernel
+// (12288 on 256 CUs x 12 waves) go to the burst kernel, one wave per block on
+// the compact tables, unless tuning forces a kernel.  The
+// crossover (tools/latency_burst.py, profiles/r03_latency_burst_mid.log): 8192
+// blocks 26.1 us burst vs 34.4 us rounds, 16384 blocks 39.4 vs 35.4 us.
+uint64_t burst_max(uint32_t cus) { return 4ull * cus * flat_waves(); }
 int burst_lanes(int mode, uint64_t n_blocks, uint32_t cus) {
   if (mode != kStore && mode != kTrailer && mode != kVerify) return 0;
   const int tb = g_tune_burst.load();
@@ -1167,10 +1170,10 @@ int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_fra
   const int v = g_tune_parity.load();
   const int u = (v & 0xf) ? (v & 0xf) : 2;  // sweep (profiles/r01_parity_sweep.log): 2 x 1
   const int fu = ((v >> 4) & 0xf) ? ((v >> 4) & 0xf) : 1;  // x 8/CU best (71%), 4 x 2: 57%
-  const int per_cu = ((v >> 8) & 0xff) ? ((v >> 8) & 0xff) : 8;
+  const int per_cu = ((v >> 8) & 0xff) ? ((v >> 8) & 0xff) : 8;  // 0xff: no cap (one pass)
   uint64_t chunks = (parity_len + 15) / 16;
   uint64_t wgs = (chunks + 256 * (uint64_t)u - 1) / (256 * (uint64_t)u);
-  const uint64_t cap = (uint64_t)t->cus * per_cu;
+  const uint64_t cap = per_cu == 0xff ? (1ull << 31) - 1 : (uint64_t)t->cus * per_cu;
   if (wgs > cap) wgs = cap;
   hipStream_t st = (hipStream_t)stream;
   const uint8_t* b = (const uint8_t*)base;
@@ -1183,7 +1186,7 @@ int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_fra
     return (int)hipGetLastError();                                                            \
   }
   NOVA_XP(1, 1) NOVA_XP(2, 1) NOVA_XP(4, 1) NOVA_XP(4, 2) NOVA_XP(4, 4) NOVA_XP(2, 4) NOVA_XP(2, 2)
-  NOVA_XP(8, 1) NOVA_XP(8, 2)
+  NOVA_XP(8, 1) NOVA_XP(8, 2) NOVA_XP(1, 8) NOVA_XP(2, 8) NOVA_XP(1, 4)
 #undef NOVA_XP
   return NOVA_E_INVAL;
 }

@@ -1009,6 +1009,55 @@ __global__ void __launch_bounds__(1024) read_ceiling_kernel(const uint8_t* base,
 }
 
 
+// Diagnostic: copy ceilings for the XOR parity kernel's traffic shape
+// (VERDICT r02 item 7).  KIND 0: 8 aligned fragment reads + 1 write per 16-B
+// chunk (the parity pattern with nothing else: no alignment paths, no end
+// clamps); 1: the 8 reads only (results folded into a sink); 2: 1 read + 1
+// write (a plain copy); 3: the write only.  U chunks per lane per step, nt or
+// default load / store policy, grid-strided over `wgs` workgroups.
+template <int U, int NTL, int NTS, int KIND>
+__global__ void __launch_bounds__(256) copy_ceiling_kernel(const uint8_t* base, const uint64_t* frag_off,
+                                                           uint64_t n16, uint8_t* out, uint32_t* sink) {
+  constexpr int K = KIND == 2 ? 1 : (KIND == 3 ? 0 : 8);
+  const uint64_t nth = (uint64_t)gridDim.x * 256;
+  uint64_t fa[K > 0 ? K : 1];
+#pragma unroll
+  for (int f = 0; f < K; f++) fa[f] = (uint64_t)base + frag_off[f];
+  uint32_t acc = 0;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; c0 < n16; c0 += U * nth) {
+    u32x4 x[U];
+#pragma unroll
+    for (int k = 0; k < U; k++)  // the write-only kind stores something index-dependent
+      x[k] = KIND == 3 ? u32x4{(uint32_t)c0, 0u, 0u, (uint32_t)k} : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int f = 0; f < K; f++) {
+      u32x4 v[U];
+#pragma unroll
+      for (int k = 0; k < U; k++) {
+        const uint64_t c = c0 + k * nth;
+        const auto* a = reinterpret_cast<gu32x4*>(fa[f] + 16 * (c < n16 ? c : n16 - 1));
+        v[k] = NTL ? __builtin_nontemporal_load(a) : *a;
+      }
+#pragma unroll
+      for (int k = 0; k < U; k++) x[k] ^= v[k];
+    }
+    if constexpr (KIND == 1) {
+#pragma unroll
+      for (int k = 0; k < U; k++) acc ^= x[k].x ^ x[k].y ^ x[k].z ^ x[k].w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; k++) {
+        const uint64_t c = c0 + k * nth;
+        if (c >= n16) break;
+        auto* o = (__attribute__((address_space(1))) u32x4*)(uint64_t)(out + 16 * c);
+        if constexpr (NTS != 0) __builtin_nontemporal_store(x[k], o);
+        else *o = x[k];
+      }
+    }
+  }
+  if (KIND == 1 && acc == 0x9E3779B9u) sink[threadIdx.x] = acc;  // keeps the loads live
+}
+
 // lane_xor<K> (crc32c_kernels.hpp) next to __shfl_xor for K = 1 .. 32 on one
 // wave64: out[k * 64 + l] = lane_xor<2^k>(in[l]), ref[k * 64 + l] = __shfl_xor;
 // out[6 * 64 + l] = wave_max(in[l]).
@@ -1555,6 +1604,37 @@ void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
 void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
 
 void nova_diag_set_log_window(int records) { g_tune_logwin.store(records); }
+
+// Copy ceilings (copy_ceiling_kernel): variant = U | NTL << 4 | NTS << 5 |
+// KIND << 8; wgs 0 = one chunk per lane per step over the whole range.
+int nova_diag_copy_ceiling(const void* base, const uint64_t* frag_off_dev, size_t parity_len,
+                           void* out, uint32_t* sink_dev, int wgs, int variant, void* stream) {
+  if (!base || !frag_off_dev || !out || !sink_dev || (parity_len & 15) || !parity_len || wgs < 0)
+    return NOVA_E_INVAL;
+  const int u = variant & 15, ntl = (variant >> 4) & 1, nts = (variant >> 5) & 1, kind = (variant >> 8) & 3;
+  const uint64_t n16 = parity_len / 16;
+  const uint64_t full = (n16 + 256ull * u - 1) / (256ull * u);
+  const uint32_t g = wgs ? (uint32_t)wgs : (uint32_t)(full < (1u << 30) ? full : (1u << 30));
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t* b = (const uint8_t*)base;
+  uint8_t* o = (uint8_t*)out;
+  int id = (u << 8) | (ntl << 4) | (nts << 5) | kind;
+  switch (id) {
+#define NOVA_CC(U, L, S, K)                                                                          \
+  case ((U) << 8) | ((L) << 4) | ((S) << 5) | (K):                                                  \
+    hipLaunchKernelGGL((copy_ceiling_kernel<U, L, S, K>), dim3(g), dim3(256), 0, st, b, frag_off_dev, \
+                       n16, o, sink_dev);                                                           \
+    return (int)hipGetLastError();
+#define NOVA_CC_K(U, L, S) NOVA_CC(U, L, S, 0) NOVA_CC(U, L, S, 1) NOVA_CC(U, L, S, 2) NOVA_CC(U, L, S, 3)
+#define NOVA_CC_U(U) NOVA_CC_K(U, 0, 0) NOVA_CC_K(U, 0, 1) NOVA_CC_K(U, 1, 0) NOVA_CC_K(U, 1, 1)
+    NOVA_CC_U(1) NOVA_CC_U(2) NOVA_CC_U(4)
+#undef NOVA_CC_U
+#undef NOVA_CC_K
+#undef NOVA_CC
+    default:
+      return NOVA_E_INVAL;
+  }
+}
 
 int nova_diag_lane_xor_probe(const uint32_t* in_dev, uint32_t* out_dev, uint32_t* ref_dev, void* stream) {
   if (!in_dev || !out_dev || !ref_dev) return NOVA_E_INVAL;

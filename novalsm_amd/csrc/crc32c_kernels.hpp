@@ -394,23 +394,18 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
     return ((threadIdx.x >> 5) & 1u) ? r[0] : r[1];
   }
 }
-// max over the wave's 64 lanes, wave-uniform: DPP xor levels within each
-// 16-lane row, then the four row maxima read into scalar registers
-// (v_readlane) and combined on the scalar unit.  (The cross-row levels as
-// permlane swaps -- both swap results hold a lane's own value and its
-// partner's, so max(r[0], r[1]) needs no lane select -- measured 0.5 points
-// slower on log verify than ds_bpermute; this form leaves no cross-lane VALU
-// level and hands the callers an SGPR round length.)
+// max over the wave's 64 lanes (every lane gets it).  The cross-row levels
+// stay ds_bpermute (__shfl_xor): same-box A/Bs on the log-verify image
+// (rounds kernel, one wave_max per round) measured the permlane-swap form
+// (max of both swap results, no lane select) 0.5 points and a DPP + 4 x
+// v_readlane + s_max form 0.3 points slower (profiles/r03_ab_wave_max.log).
 __device__ __forceinline__ uint32_t wave_max(uint32_t m) {
+  m = max(m, (uint32_t)__shfl_xor((int)m, 32));
+  m = max(m, (uint32_t)__shfl_xor((int)m, 16));
   m = max(m, lane_xor<8>(m));
   m = max(m, lane_xor<4>(m));
   m = max(m, lane_xor<2>(m));
-  m = max(m, lane_xor<1>(m));
-  const uint32_t a = max((uint32_t)__builtin_amdgcn_readlane((int)m, 0),
-                         (uint32_t)__builtin_amdgcn_readlane((int)m, 16));
-  const uint32_t b = max((uint32_t)__builtin_amdgcn_readlane((int)m, 32),
-                         (uint32_t)__builtin_amdgcn_readlane((int)m, 48));
-  return max(a, b);
+  return max(m, lane_xor<1>(m));
 }
 
 // Fold the 4G pending stream words of a lane group (4 per lane, lane q holds

@@ -19,13 +19,16 @@
 //   2. the product dispatch (run(): rounds / burst kernels) over that array;
 //   3. verify: qscatter_kernel copies each table's ok flags back to its own
 //      array and adds its mismatches to its own counter.
-// The leader waits for its slot's stream, marks the batch done and wakes the
-// followers.  kSlots batches may be in flight at once (one stream and one
-// scratch set each), so the next batch forms and launches while one runs.
+// A batch of one (no other caller waiting) is the plain call on the caller's
+// own stream.  The leader waits for the batch, marks its requests done and
+// wakes each follower (one condition variable per request: no thundering
+// herd).  kSlots batches may be in flight at once (one stream and one scratch
+// set each), so the next batch forms and launches while one runs.
 // Results are identical to the per-table calls: each block's checksum is
 // computed by the same kernels from the same bytes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
@@ -40,7 +43,8 @@ using namespace nova_dev;
 
 constexpr int kMaxReqs = 32;                 // tables per batch (kernel-argument table)
 constexpr uint64_t kMaxBlocks = 1ull << 20;  // blocks per batch (scratch per slot: 13 MiB)
-constexpr int kSlots = 2;                    // batches in flight (at most)
+constexpr int kSlots = 4;                    // batches in flight (at most)
+constexpr int kDefaultSlots = 2;
 
 struct QTable {
   uint64_t base;          // the table image's device address
@@ -92,7 +96,8 @@ struct Req {
   uint64_t n;
   uint8_t* ok;
   uint32_t* bad;
-  hipEvent_t ready;  // recorded on the caller's stream at submission
+  hipStream_t stream;           // the caller's: idle when the request is queued
+  std::condition_variable cv;   // woken when done, or when it may lead
   bool done = false;
   int rc = 0;
 };
@@ -107,7 +112,6 @@ struct Slot {
 
 struct Queue {
   std::mutex mu;
-  std::condition_variable cv;
   std::deque<Req*> q;
   Slot slot[kSlots];
   uint64_t batches = 0, requests = 0, max_tables = 0;
@@ -125,15 +129,30 @@ struct Queue {
     return 0;
   }
 
-  // One batch on slot s (the leader, without the lock).
+  // One batch (the leader, without the lock).  A batch of one runs as the
+  // plain call on its caller's stream; a larger one on the slot's stream:
+  // gather, the product dispatch over absolute addresses, scatter.
   int run_batch(Slot& s, Req** rs, int nr) {
+    if (nr == 1) {
+      CrcParams p{};
+      p.base = rs[0]->buf;
+      p.offsets = rs[0]->offs;
+      p.lengths = rs[0]->sizes;
+      p.n_blocks = rs[0]->n;
+      p.flags = rs[0]->flags;
+      p.ok_out = rs[0]->ok;
+      p.n_bad = rs[0]->bad;
+      const int rc = dispatch(rs[0]->mode, p, rs[0]->stream);
+      return rc ? rc : (int)hipStreamSynchronize(rs[0]->stream);
+    }
     int rc = init_slot(s);
     if (rc) return rc;
+    // tables in address order: the batch's blocks ascend when each table's
+    // do, which the trailer writer's whole-piece pass needs (trailer_layout)
+    std::sort(rs, rs + nr, [](const Req* a, const Req* b) { return a->buf < b->buf; });
     QBatch b{};
     uint64_t total = 0;
     for (int k = 0; k < nr; k++) {
-      const hipError_t e = hipStreamWaitEvent(s.stream, rs[k]->ready, 0);
-      if (e != hipSuccess) return (int)e;
       b.t[k] = QTable{(uint64_t)rs[k]->buf, rs[k]->offs, rs[k]->sizes, rs[k]->ok, rs[k]->bad, total};
       total += rs[k]->n;
     }
@@ -148,13 +167,9 @@ struct Queue {
     p.offsets = s.offs;
     p.lengths = s.sizes;
     p.n_blocks = total;
+    p.flags = rs[0]->flags;
     const int mode = rs[0]->mode;
-    if (mode == kTrailer) {
-      p.flags = rs[0]->flags;
-    } else {
-      p.ok_out = s.ok;
-      p.flags = rs[0]->flags;
-    }
+    if (mode == kVerify) p.ok_out = s.ok;
     rc = dispatch(mode, p, s.stream);
     if (rc) return rc;
     if (mode == kVerify) {
@@ -165,14 +180,22 @@ struct Queue {
     return e == hipSuccess ? 0 : (int)e;
   }
 
-  // NOVA_SST_QUEUE_SLOTS=1 keeps one batch in flight (read once)
+  // NOVA_SST_QUEUE_SLOTS (1..4, default 2): batches in flight (read once)
   static int slots() {
     static const int n = [] {
       const char* v = getenv("NOVA_SST_QUEUE_SLOTS");
-      const int x = v ? atoi(v) : kSlots;
-      return x >= 1 && x <= kSlots ? x : kSlots;
+      const int x = v ? atoi(v) : kDefaultSlots;
+      return x >= 1 && x <= kSlots ? x : kDefaultSlots;
     }();
     return n;
+  }
+  int free_slot(int ns) const {
+    for (int k = 0; k < ns; k++)
+      if (!slot[k].busy) return k;
+    return -1;
+  }
+  void wake_front() {
+    if (!q.empty()) q.front()->cv.notify_one();
   }
 
   int submit(Req& r) {
@@ -182,17 +205,11 @@ struct Queue {
     int si = -1;
     for (;;) {
       if (r.done) return r.rc;
-      if (q.front() == &r) {
-        for (int k = 0; k < ns; k++)
-          if (!slot[k].busy) {
-            si = k;
-            break;
-          }
-        if (si >= 0) break;
-      }
-      cv.wait(lk);
+      // (a popped request waits for done; front() of an empty deque is undefined)
+      if (!q.empty() && q.front() == &r && (si = free_slot(ns)) >= 0) break;
+      r.cv.wait(lk);
     }
-    // leader: take the compatible requests at the queue's front
+    // leader: take the compatible requests at the queue's front (r first)
     Req* rs[kMaxReqs];
     int nr = 0;
     uint64_t blocks = 0;
@@ -207,24 +224,23 @@ struct Queue {
     batches++;
     requests += (uint64_t)nr;
     if ((uint64_t)nr > max_tables) max_tables = (uint64_t)nr;
-    cv.notify_all();  // the next front may lead on the other slot
+    wake_front();  // it may lead on another free slot
     lk.unlock();
     const int rc = run_batch(slot[si], rs, nr);
     lk.lock();
     slot[si].busy = false;
-    for (int k = 0; k < nr; k++) {
+    for (int k = 0; k < nr; k++) {  // under the lock: a woken caller's Req ends with its call
       rs[k]->rc = rc;
       rs[k]->done = true;
+      if (rs[k] != &r) rs[k]->cv.notify_one();
     }
-    cv.notify_all();
+    wake_front();
     return r.rc;
   }
 };
 
 constexpr int kMaxDev = 16;
 Queue g_q[kMaxDev];
-
-thread_local hipEvent_t t_ev[kMaxDev] = {};
 
 int enqueue(Req& r, hipStream_t stream) {
   int dev = 0;
@@ -234,7 +250,14 @@ int enqueue(Req& r, hipStream_t stream) {
   }
   int err = 0;
   if (!tables(&err)) return err;
-  if (r.n > kMaxBlocks) {  // larger than one batch: the direct path (one launch is efficient)
+  // Work queued on the caller's stream (the image, its descriptors) finishes
+  // before the request can join a batch on another stream.  Done here, in the
+  // caller's thread, so the leader issues no per-request wait.
+  hipError_t e = hipStreamQuery(stream);
+  if (e == hipErrorNotReady) e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) return (int)e;
+  r.stream = stream;
+  if (r.n > kMaxBlocks) {  // larger than one batch: the plain call (one launch is efficient)
     CrcParams p{};
     p.base = r.buf;
     p.offsets = r.offs;
@@ -246,17 +269,6 @@ int enqueue(Req& r, hipStream_t stream) {
     const int rc = dispatch(r.mode, p, stream);
     return rc ? rc : (int)hipStreamSynchronize(stream);
   }
-  hipEvent_t& ev = t_ev[dev];
-  if (!ev) {
-    const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (e != hipSuccess) {
-      ev = nullptr;
-      return (int)e;
-    }
-  }
-  const hipError_t e = hipEventRecord(ev, stream);
-  if (e != hipSuccess) return (int)e;
-  r.ready = ev;
   return g_q[dev].submit(r);
 }
 

@@ -385,12 +385,12 @@ def test_no_device_memory_growth(torch_gpu, oracle):
 
 def test_shared_stream_trailer_threads(torch_gpu, oracle):
     """several host threads writing trailers of large batches (the
-    rounds kernel, > 6144 blocks; blocks of 1..599 B, so the byte-store form) on
+    rounds kernel, > 12288 blocks; blocks of 1..599 B, so the byte-store form) on
     the SAME stream (the default one) each get their own layout-flag scratch:
     every trailer matches the oracle."""
     torch = torch_gpu
     import threading
-    n = 9000
+    n = 13000
     imgs, descs = [], []
     for t in range(4):
         rng = np.random.default_rng(300 + t)
@@ -430,7 +430,7 @@ def test_shared_stream_trailer_threads(torch_gpu, oracle):
 @pytest.mark.parametrize("layout", ["packed", "gaps", "tiny", "small", "permuted", "aligned"])
 @pytest.mark.parametrize("quirk,ctype", [(True, 0), (False, 1)])
 def test_trailer_store_forms(torch_gpu, oracle, layout, quirk, ctype, form):
-    """Large trailer batches (the rounds kernel, > 6144 blocks) in every store
+    """Large trailer batches (the rounds kernel, > 12288 blocks) in every store
     form: 0 the product's byte stores from the CRC kernel; diagnostics 2 (CRC
     array + scatter pass) and 3 (whole 64-B pieces around each trailer where
     trailer_layout_kernel allows: blocks ascending and disjoint, no neighbour's
@@ -442,7 +442,7 @@ def test_trailer_store_forms(torch_gpu, oracle, layout, quirk, ctype, form):
     trailers changes, including gap bytes, the bytes before the first block and
     after the last one."""
     torch = torch_gpu
-    n = 9000
+    n = 13000
     layouts = ["packed", "gaps", "tiny", "small", "permuted", "aligned"]
     rng = np.random.default_rng(layouts.index(layout) * 2 + quirk)
     lens = rng.integers(32, 3000, n).astype(np.uint32)
@@ -944,6 +944,61 @@ def test_sst_queue_concurrent(torch_gpu, oracle):
     assert after["batches"] - before["batches"] < served, (before, after)
 
 
+@pytest.mark.parametrize("threads", [2, 4, 16])
+def test_sst_queue_stress(torch_gpu, oracle, threads):
+    """The coalescing queue under back-to-back calls (tools/concurrent_sst.py's
+    shape): `threads` callers, each verifying its own 1024-block SSTable image
+    (4096+U[0,255] B blocks) 60 times with no pause, every third call on a
+    copy with one corrupted block; every call's flags and count are checked."""
+    torch = torch_gpu
+    import threading
+    n, R = 1024, 60
+    from bench import sst4k_layout
+    offs_np, lens_np = sst4k_layout(n, 5)[:2]
+    total = int(offs_np[-1]) + int(lens_np[-1]) + 5
+    offs = torch.from_numpy(offs_np.view(np.int64)).cuda()
+    lens = torch.from_numpy(lens_np.view(np.int32)).cuda()
+    imgs, bads = [], []
+    for t in range(threads):
+        img = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        C.fill_splitmix64(img, 900 + t)
+        C.write_trailers(img, offs, lens)
+        bad_img = img.clone()
+        j = (37 * t + 11) % n
+        bad_img[int(offs_np[j]) + 100] ^= 1
+        imgs.append((img, bad_img, j))
+    torch.cuda.synchronize()
+    errors = []
+
+    def work(t):
+        try:
+            img, bad_img, j = imgs[t]
+            s = torch.cuda.Stream()
+            ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+            nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+            for r in range(R):
+                corrupt = r % 3 == 2
+                with torch.cuda.stream(s):
+                    nb.zero_()
+                    C.queue_verify_blocks(bad_img if corrupt else img, offs, lens, ok, nb, stream=s)
+                    got, cnt = ok.cpu().numpy(), int(nb.item())
+                want = np.ones(n, np.uint8)
+                if corrupt:
+                    want[j] = 0
+                if not np.array_equal(got, want) or cnt != int(corrupt):
+                    errors.append((t, r, cnt, np.nonzero(got != want)[0][:4]))
+                    return
+        except Exception as e:  # pragma: no cover
+            errors.append((t, e))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:4]
+
+
 @pytest.mark.parametrize("kernel", ["default", "logstream"])
 def test_log_records_write_verify(torch_gpu, golden, oracle, kernel):
     """MANIFEST/WAL record CRCs (db/log_writer.cc:99-114,
@@ -1288,11 +1343,11 @@ def test_large_blocks_hint_same_results(torch_gpu, oracle, mode):
         assert int(bad.item()) == len(victims)
 
 
-@pytest.mark.parametrize("n", [1, 5, 6144, 6145, 49152, 98303, 98304, 196608])
+@pytest.mark.parametrize("n", [1, 5, 12288, 12289, 49152, 98303, 98304, 196608])
 def test_batch_size_dispatch_thresholds(torch_gpu, oracle, n):
-    """plan() sizes the rounds kernel to the batch (16-lane groups with 4-block
-    chunks up to 2 blocks per wave slot = 6144 on 256 CUs x 12 waves, then 8-,
-    16- and 32-block chunks at 16x / 32x that).  Every side of each threshold,
+    """The burst kernel up to 4 blocks per wave slot (12288 on 256 CUs x 12
+    waves), then plan() sizes the rounds kernel to the batch (8-, 16- and
+    32-block chunks at 16x / 32x two blocks per slot).  Every side of each threshold,
     on ragged unaligned blocks, through store, trailers and verify, matches the
     oracle; describe() names the chunk the dispatcher picked."""
     torch = torch_gpu
@@ -1320,7 +1375,7 @@ def test_batch_size_dispatch_thresholds(torch_gpu, oracle, n):
     assert sorted(np.nonzero(ok.cpu().numpy() == 0)[0].tolist()) == sorted(victims.tolist())
     assert int(bad.item()) == len(victims)
     d = C.describe(n, 0, 0, variable=True)
-    if n <= 6144:
+    if n <= 12288:
         assert d["kernel"].startswith("crc32c_burst_kernel"), d
     else:
         want_chunk = 32 if n >= 196608 else 16 if n >= 98304 else 8

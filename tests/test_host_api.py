@@ -176,11 +176,11 @@ def test_device_init_fails_loudly_without_gpu(lib):
 
 
 @pytest.mark.parametrize("n,lanes,chunk", [
-    (1, 64, 0), (6144, 64, 0), (6145, 8, 8), (98303, 8, 8), (98304, 8, 16),
+    (1, 64, 0), (12288, 64, 0), (12289, 8, 8), (98303, 8, 8), (98304, 8, 16),
     (196607, 8, 16), (196608, 8, 32), (1 << 20, 8, 32)])
 def test_rounds_plan_sized_to_the_batch(n, lanes, chunk):
     """Host-side dispatch (no device call): one SSTable's worth of blocks (up to
-    two per rounds-kernel wave slot, 256 CUs x 12 waves x 2 = 6144) goes to the
+    four per rounds-kernel wave slot, 256 CUs x 12 waves x 4 = 12288) goes to the
     burst kernel, one wave per block; larger variable batches to the rounds
     kernel with 8-lane groups and 8/16/32-block chunks; the
     large-blocks hint picks the units kernel above the burst size."""
