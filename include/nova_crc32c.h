@@ -154,7 +154,7 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
  * the call (the image, its descriptors) completes first: the call
  * synchronises `stream` when it is busy.  A call alone in the queue runs as
  * the plain call on `stream`; a table of more than 2^20 blocks always does.
- * NOVA_SST_QUEUE_SLOTS (1..4, default 2): batches in flight at once. */
+ * NOVA_SST_QUEUE_SLOTS (1..4, default 4): batches in flight at once. */
 int nova_sst_queue_write_trailers(void* buf, const uint64_t* offsets, const uint32_t* sizes,
                                   size_t n_blocks, uint32_t flags, void* stream);
 int nova_sst_queue_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,

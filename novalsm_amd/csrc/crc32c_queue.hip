@@ -44,7 +44,7 @@ using namespace nova_dev;
 constexpr int kMaxReqs = 32;                 // tables per batch (kernel-argument table)
 constexpr uint64_t kMaxBlocks = 1ull << 20;  // blocks per batch (scratch per slot: 13 MiB)
 constexpr int kSlots = 4;                    // batches in flight (at most)
-constexpr int kDefaultSlots = 2;
+constexpr int kDefaultSlots = 4;  // tools/concurrent_sst.py: 4 beat 2 in most rows
 
 struct QTable {
   uint64_t base;          // the table image's device address
@@ -180,7 +180,7 @@ struct Queue {
     return e == hipSuccess ? 0 : (int)e;
   }
 
-  // NOVA_SST_QUEUE_SLOTS (1..4, default 2): batches in flight (read once)
+  // NOVA_SST_QUEUE_SLOTS (1..4, default 4): batches in flight (read once)
   static int slots() {
     static const int n = [] {
       const char* v = getenv("NOVA_SST_QUEUE_SLOTS");

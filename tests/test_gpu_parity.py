@@ -371,7 +371,7 @@ def test_no_device_memory_growth(torch_gpu, oracle):
     # 4 threads: at most 4 hook streams + 3 x 4 stream_host streams in the pool
     assert C.stream_slots() <= slots0 + 16
     s = torch.cuda.Stream()  # a batch above the burst size: the stream kernel takes a slot
-    C.batch_strided(dev(torch, splitmix64_bytes(1, 4096 * 8192)), 4096, 4096, 8192, stream=s)
+    C.batch_strided(dev(torch, splitmix64_bytes(1, 4096 * 16384)), 4096, 4096, 16384, stream=s)
     s.synchronize()
     n1 = C.stream_slots()
     C.stream_release(s)
@@ -1119,6 +1119,30 @@ def test_xor_parity(torch_gpu, oracle, align, plen, k):
     host = splitmix64_bytes(plen + k, total)
     out = C.xor_parity(dev(torch, host), dev(torch, offs, torch.int64), plen)
     assert np.array_equal(out.cpu().numpy(), oracle.xor_parity(host, offs, plen))
+
+
+@pytest.mark.parametrize("align", [True, False])
+def test_xor_parity_variants(torch_gpu, oracle, align):
+    """Every instantiated (chunks per lane, fragments per load group) form of
+    xor_parity_kernel, on a capped grid-stride walk and on the product's
+    one-pass grid, equals the oracle (diagnostics knob; the default is 2 x 1,
+    one pass)."""
+    torch = torch_gpu
+    k, plen = 8, (1 << 20) + 3
+    rng = np.random.default_rng(41)
+    offs = np.array([f * (plen + 64) + (0 if align else int(rng.integers(0, 16)))
+                     for f in range(k)], np.uint64)
+    host = splitmix64_bytes(77, int(offs[-1]) + plen)
+    want = oracle.xor_parity(host, offs, plen)
+    d, do = dev(torch, host), dev(torch, offs, torch.int64)
+    with C.diagnostics() as L:
+        for u, fu in [(1, 1), (2, 1), (4, 1), (4, 2), (4, 4), (2, 4), (2, 2), (8, 1), (8, 2),
+                      (1, 8), (2, 8), (1, 4), (1, 2)]:
+            for cap in (8, 0xff):
+                L.nova_diag_set_parity_variant(u | fu << 4 | cap << 8)
+                out = C.xor_parity(d, do, plen)
+                assert np.array_equal(out.cpu().numpy(), want), (u, fu, cap)
+        L.nova_diag_set_parity_variant(0)
 
 
 def test_claim_counters_reset_between_launches(torch_gpu, oracle):
