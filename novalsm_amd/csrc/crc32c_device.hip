@@ -1165,17 +1165,18 @@ int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_fra
   int err = 0;
   DevTables* t = tables(&err);
   if (!t) return err;
-  // variant: U (chunks per thread) x FU (fragments loaded together), grid cap
-  // in workgroups per CU; default from the sweep in profiles.
+  // variant (diagnostics knob): U (chunks per thread, bits 0-4) x FU
+  // (fragments loaded together, bits 5-8), grid cap in workgroups per CU
+  // (bits 9-16); 0 fields take the defaults below.
   const int v = g_tune_parity.load();
-  // Default 2 chunks x 1 fragment per step over a one-pass grid (one 16-B
-  // chunk pair per lane, no grid-stride): 74.2 % against 70.7 % for the
-  // round-1 choice of a grid capped at 8 workgroups per CU, whose strided walk
-  // measured 52-54 % with all 8 fragments' loads in flight
-  // (profiles/r03_parity_sweep.log; r01_parity_sweep.log for the round-1 sweep).
-  const int u = (v & 0xf) ? (v & 0xf) : 2;
-  const int fu = ((v >> 4) & 0xf) ? ((v >> 4) & 0xf) : 1;
-  const int per_cu = ((v >> 8) & 0xff) ? ((v >> 8) & 0xff) : 0xff;  // 0xff: no cap (one pass)
+  // Default 8 chunks x 1 fragment per step over a one-pass grid (each lane's
+  // 8 chunks in flight per fragment, no grid-stride loop): 79.6 %, against
+  // 73.2 % for 2 x 1 and 71.1 % for the round-1 choice (2 x 1 on a grid
+  // capped at 8 workgroups per CU, whose strided walk measured 52-54 % with
+  // all 8 fragments' loads in flight) (profiles/r03_parity_sweep*.log).
+  const int u = (v & 0x1f) ? (v & 0x1f) : 8;
+  const int fu = ((v >> 5) & 0xf) ? ((v >> 5) & 0xf) : 1;
+  const int per_cu = ((v >> 9) & 0xff) ? ((v >> 9) & 0xff) : 0xff;  // 0xff: no cap (one pass)
   uint64_t chunks = (parity_len + 15) / 16;
   uint64_t wgs = (chunks + 256 * (uint64_t)u - 1) / (256 * (uint64_t)u);
   const uint64_t cap = per_cu == 0xff ? (1ull << 31) - 1 : (uint64_t)t->cus * per_cu;
@@ -1191,7 +1192,7 @@ int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_fra
     return (int)hipGetLastError();                                                            \
   }
   NOVA_XP(1, 1) NOVA_XP(2, 1) NOVA_XP(4, 1) NOVA_XP(4, 2) NOVA_XP(4, 4) NOVA_XP(2, 4) NOVA_XP(2, 2)
-  NOVA_XP(8, 1) NOVA_XP(8, 2) NOVA_XP(1, 8) NOVA_XP(2, 8) NOVA_XP(1, 4) NOVA_XP(1, 2)
+  NOVA_XP(8, 1) NOVA_XP(8, 2) NOVA_XP(1, 8) NOVA_XP(2, 8) NOVA_XP(1, 4) NOVA_XP(1, 2) NOVA_XP(16, 1)
 #undef NOVA_XP
   return NOVA_E_INVAL;
 }

@@ -1627,7 +1627,7 @@ int nova_diag_copy_ceiling(const void* base, const uint64_t* frag_off_dev, size_
     return (int)hipGetLastError();
 #define NOVA_CC_K(U, L, S) NOVA_CC(U, L, S, 0) NOVA_CC(U, L, S, 1) NOVA_CC(U, L, S, 2) NOVA_CC(U, L, S, 3)
 #define NOVA_CC_U(U) NOVA_CC_K(U, 0, 0) NOVA_CC_K(U, 0, 1) NOVA_CC_K(U, 1, 0) NOVA_CC_K(U, 1, 1)
-    NOVA_CC_U(1) NOVA_CC_U(2) NOVA_CC_U(4)
+    NOVA_CC_U(1) NOVA_CC_U(2) NOVA_CC_U(4) NOVA_CC_U(8)
 #undef NOVA_CC_U
 #undef NOVA_CC_K
 #undef NOVA_CC

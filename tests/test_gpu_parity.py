@@ -1125,7 +1125,7 @@ def test_xor_parity(torch_gpu, oracle, align, plen, k):
 def test_xor_parity_variants(torch_gpu, oracle, align):
     """Every instantiated (chunks per lane, fragments per load group) form of
     xor_parity_kernel, on a capped grid-stride walk and on the product's
-    one-pass grid, equals the oracle (diagnostics knob; the default is 2 x 1,
+    one-pass grid, equals the oracle (diagnostics knob; the default is 8 x 1,
     one pass)."""
     torch = torch_gpu
     k, plen = 8, (1 << 20) + 3
@@ -1137,9 +1137,9 @@ def test_xor_parity_variants(torch_gpu, oracle, align):
     d, do = dev(torch, host), dev(torch, offs, torch.int64)
     with C.diagnostics() as L:
         for u, fu in [(1, 1), (2, 1), (4, 1), (4, 2), (4, 4), (2, 4), (2, 2), (8, 1), (8, 2),
-                      (1, 8), (2, 8), (1, 4), (1, 2)]:
+                      (1, 8), (2, 8), (1, 4), (1, 2), (16, 1)]:
             for cap in (8, 0xff):
-                L.nova_diag_set_parity_variant(u | fu << 4 | cap << 8)
+                L.nova_diag_set_parity_variant(u | fu << 5 | cap << 9)
                 out = C.xor_parity(d, do, plen)
                 assert np.array_equal(out.cpu().numpy(), want), (u, fu, cap)
         L.nova_diag_set_parity_variant(0)

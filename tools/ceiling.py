@@ -137,7 +137,7 @@ def parity_ceiling(args, torch, C):
     bytes_of = {0: (k + 1) * plen, 1: k * plen, 2: 2 * plen, 3: plen}
     variants = {"product": (lambda: C.xor_parity(buf, fo, plen, out=out, stream=stream), (k + 1) * plen)}
     for kind in (0, 1, 2, 3):
-        for u in (1, 2, 4):
+        for u in (1, 2, 4, 8):
             for ntl in (0, 1):
                 for nts in (0, 1):
                     if (kind == 1 and nts) or (kind == 3 and ntl):
