@@ -36,7 +36,7 @@ def make_workload(wl: str, stream):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from bench_ops import log_layout
     mode = ""
-    if wl.endswith("_tw") or wl.endswith("_vf"):  # sst4k_tw / sst4k_vf: trailer writer / verify
+    if wl.endswith("_tw") or wl.endswith("_vf"):  # sst4k_tw / sst4k_vf / log_vf: trailers / verify
         wl, mode = wl[:-3], wl[-2:]
     if wl == "cfg2":
         n, ln = 1 << 20, 4096
@@ -87,6 +87,12 @@ def make_workload(wl: str, stream):
         buf[o + 5] = (ln >> 8).to(torch.uint8)
         buf[o + 6] = torch.from_numpy(types).cuda()
         alg = int(lens.astype(np.uint64).sum()) + 7 * len(offs)
+        if mode == "vf":  # log_vf: verify the records the writer just checksummed
+            C.log_write_crcs(buf, o, stream=stream)
+            st = torch.empty(len(offs), dtype=torch.uint8, device="cuda")
+            bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+            return (lambda: C.log_verify_records(buf, o, stream=stream, ok=st, bad=bad)), alg, \
+                (buf, o, st, bad)
         return (lambda: C.log_write_crcs(buf, o, stream=stream)), alg, (buf, o)
     ls = torch.from_numpy(lens.view(np.int32)).cuda()
     out = torch.empty(len(offs), dtype=torch.int32, device="cuda")
