@@ -972,10 +972,10 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // unsorted (each claimed chunk still sorts itself).
   StreamScratch log_sc;  // order + position-indexed results, freed in stream order
   const int lsort = g_tune_sort.load();  // 2 default; 3-5 diagnostics A/B (crc32c_internal.hpp)
-  // Log write stays in file order: its CRC-field stores cost ~4 points of
-  // HBM throughput in file order, ~10 in sorted order from the CRC kernel and
-  // ~9 as a separate file-order pass (profiles/r03_ops_logsort3.log), more
-  // than the sort gains; the sort is a diagnostics option there.
+  // Log write stays in file order: every write-side sort form measured at or
+  // below file order (profiles/r03_ops_logsort3.log) -- its CRC-field stores
+  // cost ~7 points even in file order and more out of it; the
+  // sort is a diagnostics option there.
   const bool lsort_mode = mode == kLogVerify || (mode == kLogWrite && g_diag && g_tune_logwin.load() < 0);
   if (pl.kernel == kRoundsK && lsort_mode && G == 8 &&
       p.n_blocks >= kLogSortMin && p.n_blocks < (1ull << 32) && lsort >= 2 &&
