@@ -154,12 +154,14 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
  * the call (the image, its descriptors) completes first: the call
  * synchronises `stream` when it is busy.  A call alone in the queue runs as
  * the plain call on `stream`; a table of more than 2^20 blocks always does.
- * NOVA_SST_QUEUE_SLOTS (1..4, default 4): batches in flight at once. */
+ * NOVA_SST_QUEUE_SLOTS (1..4, default 4): batches in flight at once;
+ * nova_sst_queue_set_slots overrides it for this device (0: back to it). */
 int nova_sst_queue_write_trailers(void* buf, const uint64_t* offsets, const uint32_t* sizes,
                                   size_t n_blocks, uint32_t flags, void* stream);
 int nova_sst_queue_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
                                  size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
                                  void* stream);
+int nova_sst_queue_set_slots(int slots);
 /* Batches launched, requests served, most tables in one batch (this device). */
 int nova_sst_queue_stats(uint64_t* batches, uint64_t* requests, uint64_t* max_tables_per_batch);
 

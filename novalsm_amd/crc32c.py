@@ -61,6 +61,7 @@ _SIG = {
     "nova_sst_queue_write_trailers": (_i32, [_vp, _vp, _vp, _sz, _u32, _vp]),
     "nova_sst_queue_verify_blocks": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "nova_sst_queue_stats": (_i32, [_vp, _vp, _vp]),
+    "nova_sst_queue_set_slots": (_i32, [ctypes.c_int]),
     "nova_crc32c_stream_host": (_i32, [_vp, _u64, _u32, _sz, _vp, _u32, _sz, _i32]),
     "nova_crc32c_batch_host": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _sz, _i32]),
     "nova_sstable_write_trailers_host": (_i32, [_vp, _vp, _vp, _sz, _u32, _sz, _i32]),
@@ -401,6 +402,12 @@ def queue_verify_blocks(buf, offsets, sizes, ok, bad=None, stream=None):
                                            _arg(bad, "bad", _u32_dtypes(), dv, 1), _stream_ptr(stream))
     _check(rc, "nova_sst_queue_verify_blocks")
     return ok, bad
+
+
+def queue_set_slots(slots: int) -> None:
+    """Batches the coalescing queue keeps in flight on this device (1..4; 0:
+    NOVA_SST_QUEUE_SLOTS or the default 4)."""
+    _check(_L().nova_sst_queue_set_slots(int(slots)), "nova_sst_queue_set_slots")
 
 
 def queue_stats() -> dict:

@@ -254,20 +254,20 @@ __global__ void __launch_bounds__(256) split_finish_kernel(CrcParams p, int mode
     split_finish(p, mode, extra, i, acc[i]);
 }
 
-// ---- log records: windowed sort by step count ---------------
+// ---- log records: windowed sort by line count ---------------
 // The rounds kernel pads a round's kGroups records to the longest; sorting each
 // claimed chunk of 64 records leaves ~21 % of the loaded step capacity as
 // padding on U[1,4096] B records (tools/sim_rounds.py).  This pre-pass sorts
 // windows of kLogSortWin consecutive records (~1 MiB of log, so a chunk's
-// records stay close together in memory) by their step count, largest first,
+// records stay close together in memory) by their line count, largest first,
 // into perm[]; the kernel then takes chunks of that order.  The key comes from
 // the offsets alone -- record i's length is at most the gap to the next
 // record's header or to its 32 KiB block's end -- so the pre-pass reads 8 B
 // per record and no header byte; a wrong estimate (unsorted offsets, a block
 // trailer) only costs padding, never a wrong CRC.  One workgroup per window,
-// counting sort in LDS (order within a step count is arbitrary).
+// counting sort in LDS (order within a line count is arbitrary).
 constexpr uint32_t kLogSortWin = 512;  // records per window (at most; g_tune_logwin)
-constexpr uint32_t kLogSortBins = 128;
+constexpr uint32_t kLogSortBins = 288;  // line counts (a 32 KiB log block is 256 lines of 128 B)
 __global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint64_t* __restrict__ offs,
                                                        uint64_t n, uint64_t buf_len, uint32_t line,
                                                        uint32_t win, uint32_t* __restrict__ perm) {
@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint
       const uint64_t E = u1 & ~15ull;
       const uint64_t first = (u0 & ~15ull) & ~(uint64_t)(line - 1);
       const uint64_t Le = (E + line - 1) & ~(uint64_t)(line - 1);
-      const uint64_t S = Le > first ? (Le - first + 4ull * line - 1) / (4ull * line) : 1;
+      const uint64_t S = Le > first ? (Le - first) / line : 1;  // lines (the rounds kernel's cost)
       key[k] = S < kLogSortBins ? (uint32_t)S : kLogSortBins - 1;
       atomicAdd(&cnt[key[k]], 1u);
     }
@@ -544,7 +544,7 @@ void init_device(int dev, DevTables* t) {
     s = compose(s, s);
   }
   if ((t->err = upload(&t->sh16, sh))) return;
-  if ((t->err = upload(&t->zero_word, std::vector<uint32_t>(4, 0u)))) return;
+  if ((t->err = upload(&t->zero_word, std::vector<uint32_t>(256, 0u)))) return;  // 1 KiB of zeros
   {
     std::vector<uint32_t> b8(256);
     for (uint32_t b = 0; b < 256; b++) b8[b] = m1(b);

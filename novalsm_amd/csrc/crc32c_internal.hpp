@@ -59,7 +59,7 @@ struct CrcParams {
   uint32_t steal_limit;      // stream kernel: max other workgroups probed when out of work
   uint32_t bpg;              // stream kernel: consecutive blocks per lane group per round
   const uint32_t* tab_byte;  // flat kernel: one-byte step table M_1 (256 u32)
-  const uint8_t* zline;      // flat kernel: 16 zero bytes (target of masked-off loads)
+  const uint8_t* zline;      // 1 KiB of zeros (target of masked-off loads)
   // flat kernel: descriptor arrays are always loaded (no branch), absent ones
   // read word 0 of zline through a zero mask; offset = offsets[i & omask] +
   // i * stride, length = lengths[i & lmask] + len, init = init[i & imask].
@@ -119,7 +119,8 @@ struct DevTables {
   uint32_t* tree = nullptr;
   uint32_t* ft = nullptr;
   uint32_t* sh16 = nullptr;
-  uint32_t* zero_word = nullptr;  // 16 zero bytes: the NULL-init stand-in
+  uint32_t* zero_word = nullptr;  // 1 KiB of zeros: the NULL-init stand-in and the zero line
+                                  // (the rounds kernel reads up to 48G + 16 bytes past it)
   uint32_t* byte8 = nullptr;      // M_1 byte table (flat kernel tail steps)
   uint32_t* byte8lm = nullptr;    // the same + 17 x 16-B prefix masks (rounds kernel head steps)
   uint32_t* op1024 = nullptr;     // M_1024 byte tables (burst kernel stream step)

@@ -408,6 +408,15 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t m) {
   return max(m, lane_xor<1>(m));
 }
 
+__device__ __forceinline__ uint32_t wave_min(uint32_t m) {
+  m = min(m, (uint32_t)__shfl_xor((int)m, 32));
+  m = min(m, (uint32_t)__shfl_xor((int)m, 16));
+  m = min(m, lane_xor<8>(m));
+  m = min(m, lane_xor<4>(m));
+  m = min(m, lane_xor<2>(m));
+  return min(m, lane_xor<1>(m));
+}
+
 // Fold the 4G pending stream words of a lane group (4 per lane, lane q holds
 // the words at byte offsets 16q+0,4,8,12 of each 16G-byte swath) into the
 // pending word V of the group's last word: in-lane M4, M8, then cross-lane
@@ -609,8 +618,12 @@ __device__ __forceinline__ void lds_fill_tables(uint8_t* lds, const void* tab_ma
   }
 }
 
+// Launch bound 12 waves (the launch size, kUnitsWaves): 168 VGPRs.  At the
+// 16-wave bound the compiler had 128 and spilled 5-7 VGPRs to scratch in every
+// instantiation (tools/kernel_meta.py).
+constexpr int kUnitsMaxWaves = 12;
 template <int G, int MODE, int VAR = 0>
-__global__ void __launch_bounds__(kThreads) crc32c_units_kernel(CrcParams p) {
+__global__ void __launch_bounds__(kUnitsMaxWaves * 64) crc32c_units_kernel(CrcParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, nullptr, 0);
@@ -1089,6 +1102,7 @@ struct FlatSet {
   bool wsec;             // rounds kernel, trailer writer: t2 holds this lane's sector piece
   uint32_t slot;         // rounds kernel (chunk epilogue): the block's sorted slot in its chunk
   bool cend;             // rounds kernel (chunk epilogue): the chunk's last round ends here
+  uint32_t skip;         // rounds kernel: leading swaths of a round's first step no lane needs (0-3)
 };
 
 constexpr uint64_t kNoChunk = ~0ull;
@@ -1262,13 +1276,13 @@ __device__ __forceinline__ uint32_t shift_nb(const uint8_t* lds, uint32_t byte_t
 
 // ---- crc32c_rounds_kernel<G, MODE> ---------------------------------------------
 // Variable-length batches in ROUNDS: the wave's lane groups take kGroups blocks
-// at a time, all padded to the round's step count (its largest block, end-
+// at a time, all padded to the round's line count (its largest block, end-
 // aligned, so shorter blocks start later on zero pieces that leave a zero
 // register unchanged).  Every group starts and ends the round together, so the
 // per-block work (group fold, tail, epilogue) runs once per round for all
 // groups, not divergently per block as in the flat kernel; the loads stream
 // across rounds and chunks as in the stream kernel.  For the rounds to be
-// even, each claimed chunk is sorted by step count, largest first.
+// even, each claimed chunk is sorted by line count, largest first.
 //
 // Chunk epilogue (default; kVarRoundEpi keeps the per-round form): when a
 // chunk's descriptors are decoded, each lane (one block per lane) loads its
@@ -1281,8 +1295,12 @@ __device__ __forceinline__ uint32_t shift_nb(const uint8_t* lds, uint32_t byte_t
 
 
 
+// The per-block-init variant (kVarInit) carries the general head masking: at
+// the 12-wave bound (168 VGPRs) it spilled 6 VGPRs, so it launches 8 waves.
+constexpr int kInitMaxWaves = 8;
 template <int G, int MODE, int VAR = 0>
-__global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p0) {
+__global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatThreads)
+    crc32c_rounds_kernel(CrcParams p0) {
   CrcParams p = p0;  // the log-stream follow-up narrows the batch below
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
@@ -1380,7 +1398,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   uint32_t fl = 0;
   uint32_t stage = 0;  // next pipeline stage due (0: none)
   const uint32_t my = (uint32_t)lane < C ? (uint32_t)lane : C - 1;
-  // Sort the loaded chunk's slots by step count, largest first (rank by
+  // Sort the loaded chunk's slots by line count, largest first (rank by
   // shuffles, inverse permutation through the wave's LDS scratch), so each
   // round's blocks have similar lengths while the chunk keeps its locality.
   uint32_t* const sortbuf = reinterpret_cast<uint32_t*>(lds + kByteTab + 1024u + 272u) + wave * 64;
@@ -1416,9 +1434,11 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     n_ok = t_ok;
     if (!p.sort_local) return;
     uint32_t S = 0;
-    if (t_ok) {
+    if (t_ok) {  // key: lines on the group's line grid (a round costs its longest block's lines)
       const uint64_t E = (n_u0 + n_n) & ~15ull;
-      const uint64_t s64 = (E - (n_u0 & ~15ull) + kStep - 1) / kStep;
+      constexpr uint64_t kL = 16 * G;
+      const uint64_t Le = (E + (kL - 1)) & ~(kL - 1);
+      const uint64_t s64 = (Le - (n_u0 & ~(kL - 1))) / kL;
       S = s64 == 0 ? 1u : (s64 > 0xffffffffull ? 0xffffffffu : (uint32_t)s64);
     }
     uint32_t rank = 0;
@@ -1538,7 +1558,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   uint64_t g_u0 = 0, g_u1 = 0, g_lp = 0, g_end = 0, g_rec = 0;
   uint32_t g_ninit = 0, g_st = 0, g_slot = 0;
   bool g_valid = false, r_clast = false;
-  uint32_t r_idx = R, r_step = 0, r_S = 0;
+  uint32_t r_idx = R, r_step = 0, r_S = 0, r_sk = 0, r_fast = 0;
   constexpr uint64_t kLine = 16 * G;  // one swath of a lane group
   uint64_t g_le = 0;                  // the group's region end on the line grid
   uint32_t g_w0 = 0, g_hs = 0, g_hs2 = 0;  // first region swath of this lane; head steps
@@ -1588,11 +1608,27 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       // steps on the group's 16G-byte line grid: lines from the one holding
       // the first byte to the one holding byte E-1 (load_step, kLines)
       g_le = (g_end + (kLine - 1)) & ~(kLine - 1);
-      uint64_t S = (g_le - (a & ~(kLine - 1)) + kStep - 1) / kStep;
-      if (S == 0) S = 1;
-      uint32_t m = ok ? (uint32_t)S : 0u;
+      // the round runs the wave's largest line count m, in steps of 4 swaths:
+      // r_S = ceil(m / 4) steps, the first of which skips its 4 r_S - m leading
+      // swaths (no lane of the wave holds a region piece there)
+      uint64_t NL = (g_le - (a & ~(kLine - 1))) / kLine;
+      if (NL == 0) NL = 1;
+      const uint32_t nl = NL > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)NL;
+      uint32_t m = ok ? nl : 0u;
+      // the shortest non-empty region: its first line is the latest one, so
+      // from step r_fast on every lane's four pieces are region pieces
+      uint32_t mn = (ok && n > 0) ? nl : 0xffffffffu;
       m = wave_max(m);
-      r_S = m;
+      mn = wave_min(mn);
+      r_S = (uint32_t)__builtin_amdgcn_readfirstlane((int)((m + 3) >> 2));  // wave-uniform: scalar control flow
+      r_sk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(4 * r_S - m));
+      {
+        // a lane's first region swath is at most line 4 r_S - nl + 1 of the
+        // round (lanes whose piece of the first line lies before u0 & ~15)
+        const uint32_t mnl = (uint32_t)__builtin_amdgcn_readfirstlane((int)mn);
+        const uint32_t gmax = mnl == 0xffffffffu ? 0u : (mnl >= 4 * r_S ? 1u : 4 * r_S - mnl + 1);
+        r_fast = (gmax + 3) >> 2;
+      }
       if (r_S != 0) break;  // an empty round (past the batch's end): next one
     }
     // the chunk's last round: no rounds left, or only empty ones (invalid
@@ -1622,6 +1658,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   // (an empty asm reading them): the compiler then resolves their loads with
   // exact counts instead of waiting for all loads where its paths merge.
   auto take = [&](bool first) {
+    // fl and stage are wave-uniform; saying so keeps the control flow below
+    // scalar (the compiler's divergence analysis could not prove it)
+    fl = (uint32_t)__builtin_amdgcn_readfirstlane((int)fl);
+    stage = (uint32_t)__builtin_amdgcn_readfirstlane((int)stage);
     if (kBatch && (fl & fChunkEnd)) {
       // The chunk whose last step the previous take issued, for its epilogue
       // (which runs when that step folds, after this take): copied before a
@@ -1675,6 +1715,11 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
   };
 
   auto issue = [&](FlatSet& X) -> bool {
+    fl = (uint32_t)__builtin_amdgcn_readfirstlane((int)fl);  // (wave-uniform: a scalar loop exit)
+    r_step = (uint32_t)__builtin_amdgcn_readfirstlane((int)r_step);
+    r_S = (uint32_t)__builtin_amdgcn_readfirstlane((int)r_S);
+    r_fast = (uint32_t)__builtin_amdgcn_readfirstlane((int)r_fast);  // (a divergent branch
+    // between the two load forms made the compiler drain every load: vmcnt(0))
     const bool live = !(fl & fDone);
     const bool run = r_S != 0;             // a round is active (else: stalled, empty step)
     const bool v = g_valid && run;
@@ -1683,10 +1728,28 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
       const bool vz = g_nz && run;
       const uint32_t w = 4 * r_step;
       const uint64_t pa = g_lp + 16 * q;
-      X.d0 = gload16<VAR>((vz && w >= g_w0) ? pa : zl);
-      X.d1 = gload16<VAR>((vz && w + 1 >= g_w0) ? pa + 16 * G : zl);
-      X.d2 = gload16<VAR>((vz && w + 2 >= g_w0) ? pa + 32 * G : zl);
-      X.d3 = gload16<VAR>((vz && w + 3 >= g_w0 && (!last || g_l3)) ? pa + 48 * G : zl);
+      // The addresses are chosen in a wave-uniform branch and the four loads
+      // issued after it: loads inside the branch made the compiler drain
+      // every load (vmcnt(0)) where its register reuse met the other path.
+      uint64_t a0, a1, a2, a3;
+      if (run && !last && r_step >= r_fast) {
+        // all four pieces of every lane are region pieces (or its group has
+        // no data: the zero block, 1 KiB) -- one select
+        const uint64_t b = vz ? pa : zl;
+        a0 = b;
+        a1 = b + 16 * G;
+        a2 = b + 32 * G;
+        a3 = b + 48 * G;
+      } else {
+        a0 = (vz && w >= g_w0) ? pa : zl;
+        a1 = (vz && w + 1 >= g_w0) ? pa + 16 * G : zl;
+        a2 = (vz && w + 2 >= g_w0) ? pa + 32 * G : zl;
+        a3 = (vz && w + 3 >= g_w0 && (!last || g_l3)) ? pa + 48 * G : zl;
+      }
+      X.d0 = gload16<VAR>(a0);
+      X.d1 = gload16<VAR>(a1);
+      X.d2 = gload16<VAR>(a2);
+      X.d3 = gload16<VAR>(a3);
       const bool vl = v && last;
       if constexpr (kBatch) {
         // (the chunk epilogue loaded the tail lines with the descriptors)
@@ -1743,6 +1806,7 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
     X.ninit = v ? g_ninit : 0u;
     X.valid = v;
     X.last = last;
+    X.skip = (run && r_step == 0) ? r_sk : 0u;  // wave-uniform
     if (run) {
       g_lp += kStep;
       if (++r_step == r_S) fl |= kBatch && r_clast ? (fRoundDone | fChunkEnd) : fRoundDone;
@@ -1830,25 +1894,42 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         d2 = head_piece(d2, h - 32 * G, Y.ninit);
         d3 = head_piece(d3, h - 48 * G, Y.ninit);
       } else {  // ~init is ~0 (Value) or 0 (RAW, n < 4): ((d ^ LM[lo4]) & ~LM[lo])
+        // At most one of the lane's four pieces (16G bytes apart) holds a byte
+        // of [u0, u0+4): swath kk with -4 < h - 16G kk < 16.  Its pieces before
+        // u0's came from the zero line, so only that piece is masked -- two
+        // 16-B mask reads per lane instead of eight.
+        const int32_t hh = h + 3;
+        const int32_t kk = hh < 0 ? 4 : (hh >> (4 + __builtin_ctz(G)));  // hh / 16G
+        const int32_t hk0 = h - 16 * G * kk;
+        const int32_t hk = (kk < 4 && hk0 < 16) ? hk0 : -4;  // -4: masks of nothing
         const int32_t i4 = Y.ninit ? 4 : 0;
-        auto mask = [&](uint4& d, int32_t hk) {
-          const uint4 B = lds_u128(kLM + 16u * (uint32_t)clamp16(hk));
-          const uint4 I = lds_u128(kLM + 16u * (uint32_t)clamp16(hk + i4));
-          d.x = (d.x ^ I.x) & ~B.x;
-          d.y = (d.y ^ I.y) & ~B.y;
-          d.z = (d.z ^ I.z) & ~B.z;
-          d.w = (d.w ^ I.w) & ~B.w;
+        const uint4 B = lds_u128(kLM + 16u * (uint32_t)clamp16(hk));
+        const uint4 I = lds_u128(kLM + 16u * (uint32_t)clamp16(hk + i4));
+        // word by word, in registers (a select of whole uint4 values went
+        // through a private-memory array: 2.4x slower launches)
+        const bool s0 = kk == 0, s1 = kk == 1, s2 = kk == 2, s3 = kk == 3;
+        auto word = [&](uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3, uint32_t b, uint32_t i) {
+          const uint32_t x = s0 ? a0 : (s1 ? a1 : (s2 ? a2 : a3));
+          const uint32_t y = (x ^ i) & ~b;
+          a0 = s0 ? y : a0;
+          a1 = s1 ? y : a1;
+          a2 = s2 ? y : a2;
+          a3 = s3 ? y : a3;
         };
-        mask(d0, h);
-        mask(d1, h - 16 * G);
-        mask(d2, h - 32 * G);
-        mask(d3, h - 48 * G);
+        word(d0.x, d1.x, d2.x, d3.x, B.x, I.x);
+        word(d0.y, d1.y, d2.y, d3.y, B.y, I.y);
+        word(d0.z, d1.z, d2.z, d3.z, B.z, I.z);
+        word(d0.w, d1.w, d2.w, d3.w, B.w, I.w);
       }
     }
+    // A round's first step skips the leading swaths in which no lane of the
+    // wave holds a region piece (they read the zero line into zero registers),
+    // so a round costs its longest block's lines, not whole 4-swath steps.
+    const uint32_t sk = (uint32_t)__builtin_amdgcn_readfirstlane((int)Y.skip);
     if (Y.last) {  // wave-uniform: the region's last line may end past E
-      swath4<VAR>(lds, c0, c1, c2, c3, d0, lo0, lo1, lo2, lo3);
-      swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);
-      swath4<VAR>(lds, c0, c1, c2, c3, d2, lo0, lo1, lo2, lo3);
+      if (sk < 1) swath4<VAR>(lds, c0, c1, c2, c3, d0, lo0, lo1, lo2, lo3);
+      if (sk < 2) swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);
+      if (sk < 3) swath4<VAR>(lds, c0, c1, c2, c3, d2, lo0, lo1, lo2, lo3);
       const uint32_t k0 = c0, k1 = c1, k2 = c2, k3 = c3;
       swath4<VAR>(lds, c0, c1, c2, c3, d3, lo0, lo1, lo2, lo3);
       if (!Y.l3) {  // piece at or after E: not in the region
@@ -1857,6 +1938,10 @@ __global__ void __launch_bounds__(kFlatThreads) crc32c_rounds_kernel(CrcParams p
         c2 = k2;
         c3 = k3;
       }
+    } else if (sk != 0) {
+      if (sk < 2) swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);
+      if (sk < 3) swath4<VAR>(lds, c0, c1, c2, c3, d2, lo0, lo1, lo2, lo3);
+      swath4<VAR>(lds, c0, c1, c2, c3, d3, lo0, lo1, lo2, lo3);
     } else if constexpr ((VAR & kVarNarrow) != 0) {
       fold4<VAR>(lds, c0, c1, c2, c3, d0, d1, d2, d3, lo0, lo1, lo2, lo3);
     } else {
@@ -2391,7 +2476,8 @@ int launch_units_v(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
     p.chunk = (ch > 0 && ch <= 16) ? (uint32_t)ch : 8u;
   }
   p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
-  const uint64_t nwaves = waves_per_wg(kUnitsWaves);
+  uint64_t nwaves = waves_per_wg(kUnitsWaves);
+  if (nwaves > (uint64_t)kUnitsMaxWaves) nwaves = kUnitsMaxWaves;  // the kernel's launch bound
   uint64_t wgs = (p.n_chunks + nwaves - 1) / nwaves;
   if (wgs > (uint64_t)t->cus) wgs = t->cus;
   if (wgs > 256) wgs = 256;
@@ -2521,7 +2607,8 @@ int launch_rounds_v(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint3
     p.chunk = c;
   }
   p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
-  const uint64_t nwaves = flat_waves();
+  uint64_t nwaves = flat_waves();
+  if ((VAR & kVarInit) && nwaves > (uint64_t)kInitMaxWaves) nwaves = kInitMaxWaves;  // launch bound
   uint64_t wgs = (p.n_chunks + nwaves - 1) / nwaves;
   if (wgs > (uint64_t)t->cus) wgs = t->cus;
   if (wgs > 256) wgs = 256;

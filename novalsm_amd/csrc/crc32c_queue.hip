@@ -180,8 +180,9 @@ struct Queue {
     return e == hipSuccess ? 0 : (int)e;
   }
 
-  // NOVA_SST_QUEUE_SLOTS (1..4, default 4): batches in flight (read once)
-  static int slots() {
+  // Batches in flight: NOVA_SST_QUEUE_SLOTS (1..4, default 4, read once) or
+  // nova_sst_queue_set_slots (0 restores that default).
+  static int env_slots() {
     static const int n = [] {
       const char* v = getenv("NOVA_SST_QUEUE_SLOTS");
       const int x = v ? atoi(v) : kDefaultSlots;
@@ -189,6 +190,8 @@ struct Queue {
     }();
     return n;
   }
+  int set_slots = 0;  // under mu
+  int slots() const { return set_slots ? set_slots : env_slots(); }
   int free_slot(int ns) const {
     for (int k = 0; k < ns; k++)
       if (!slot[k].busy) return k;
@@ -199,8 +202,8 @@ struct Queue {
   }
 
   int submit(Req& r) {
-    const int ns = slots();
     std::unique_lock<std::mutex> lk(mu);
+    const int ns = slots();
     q.push_back(&r);
     int si = -1;
     for (;;) {
@@ -304,6 +307,20 @@ int nova_sst_queue_verify_blocks(const void* buf, const uint64_t* offsets, const
   r.ok = ok_out;
   r.bad = n_bad_out;
   return enqueue(r, (hipStream_t)stream);
+}
+
+int nova_sst_queue_set_slots(int slots) {
+  if (slots < 0 || slots > kSlots) return NOVA_E_INVAL;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) {
+    (void)hipGetLastError();
+    return NOVA_E_NODEV;
+  }
+  Queue& q = g_q[dev];
+  std::lock_guard<std::mutex> lk(q.mu);
+  q.set_slots = slots;
+  q.wake_front();  // more slots: the front request may lead now
+  return 0;
 }
 
 int nova_sst_queue_stats(uint64_t* batches, uint64_t* requests, uint64_t* max_tables_per_batch) {

@@ -882,6 +882,11 @@ def test_sst_queue_concurrent(torch_gpu, oracle):
                          quirk=(t == 5)))
     before = C.queue_stats()
     results, errors = [None] * T, []
+    # One batch in flight: while it runs, the other threads' calls queue up
+    # behind it and the next leader takes them together.  (With 4 slots a fast
+    # box can serve Python-paced callers one by one, so "batches < requests"
+    # depended on timing.)
+    C.queue_set_slots(1)
 
     def work(t):
         try:
@@ -910,10 +915,13 @@ def test_sst_queue_concurrent(torch_gpu, oracle):
             errors.append((t, e))
 
     th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
-    for x in th:
-        x.start()
-    for x in th:
-        x.join()
+    try:
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    finally:
+        C.queue_set_slots(0)
     assert not errors, errors
     calls = 0
     for t in range(T):
