@@ -6,7 +6,8 @@
 # tools/bench_ops.py (OPS, default log_write,log_verify,trailers,verify on the
 # SSTable-like image) and appends them to gpurun_out/ab_ops.log; with LAT=1 each
 # leg also runs tools/latency_burst.py (burst-kernel launch times, default lanes)
-# into gpurun_out/ab_lat.log.  Every step has
+# into gpurun_out/ab_lat.log; with LATR=1 tools/latency.py's mid-size batches
+# (rounds kernel, default plan) into gpurun_out/ab_latr.log.  Every step has
 # its own time limit and the script stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -23,6 +24,10 @@ for leg in new old new old; do
   echo "== $leg"
   timeout -k 10 300 python -u tools/bench_ops.py --ops "$OPS" --images sst4k > gpurun_out/ops_$leg.log 2>&1 || exit 3
   grep '"op"' gpurun_out/ops_$leg.log | sed "s/^/$leg /" >> gpurun_out/ab_ops.log
+  if [ "${LATR:-0}" = 1 ]; then  # mid-size batches, default dispatch (rounds kernel), events
+    timeout -k 10 200 python -u tools/latency.py --sizes 16384,32768,65536,262144 --variants auto > gpurun_out/latr_$leg.log 2>&1 || exit 3
+    grep '^{' gpurun_out/latr_$leg.log | sed "s/^/$leg /" >> gpurun_out/ab_latr.log
+  fi
   if [ "${LAT:-0}" = 1 ]; then
     timeout -k 10 200 python -u tools/latency_burst.py --lanes 64,16 --sizes 16,256,1024,4096 > gpurun_out/lat_$leg.log 2>&1 || exit 3
     grep '^{' gpurun_out/lat_$leg.log | sed "s/^/$leg /" >> gpurun_out/ab_lat.log
