@@ -188,6 +188,44 @@ def test_variable_batch_vs_oracle(torch_gpu, oracle, lanes, seg, chunk, steal, w
         _variable_batch_checks(torch, oracle, lanes, seg)
 
 
+@pytest.mark.parametrize("lanes", [2, 4, 8, 16])
+def test_rounds_tiny_and_mixed_blocks(torch_gpu, oracle, lanes):
+    """Rounds kernel at every group width on blocks that hold no full 16-B
+    piece (the tail path alone: 5 B at several alignments) and on rounds that
+    mix long and tiny blocks.  Round 3's continuous-rounds experiment (DESIGN.md
+    3.5a) failed exactly these shapes at G = 2 and 4 before it was fixed; the
+    test stays as a guard for any change to the rounds' line bookkeeping."""
+    torch = torch_gpu
+    host = splitmix64_bytes(99, 64 * 70000 + 256)
+    buf = dev(torch, host)
+    cases = []
+    for L in (5, 17, 129, 4099):
+        for align in (0, 1, 7, 13):
+            n = 256
+            stride = ((L + 64 + 15) // 16) * 16
+            cases.append((np.arange(n, dtype=np.uint64) * np.uint64(stride) + np.uint64(align),
+                          np.full(n, L, np.uint32)))
+    for a, b in ((4096, 17), (500, 5), (129, 3), (300, 40), (16384, 1)):
+        n = 384
+        lens = np.where(np.arange(n) % 3 == 0, a, b).astype(np.uint32)
+        offs = np.zeros(n, np.uint64)
+        pos = 3
+        for i in range(n):
+            offs[i] = pos
+            pos += int(lens[i]) + 5
+        cases.append((offs, lens))
+    try:
+        C.set_tuning(lanes, 0)
+        for offs, lens in cases:
+            want = oracle.batch(host, offs, lens, np.full(len(offs), 0xFFFFFFFF, np.uint32)) ^ np.uint32(
+                0xFFFFFFFF)
+            out = C.batch(buf, dev(torch, offs, torch.int64), dev(torch, lens, torch.int32), flags=C.RAW)
+            bad = np.nonzero(u32(out) != want)[0]
+            assert bad.size == 0, (lanes, int(lens[0]), int(offs[0]) % 16, bad[:8].tolist())
+    finally:
+        C.set_tuning(0, 0)
+
+
 def _variable_batch_checks(torch, oracle, lanes, seg):
     rng = np.random.default_rng(lanes * 1000 + seg)
     n = 1500

@@ -3,7 +3,8 @@
 count the steps the waves execute and the rounds they run under a given lane
 group width G, swaths per step, sort window and round width, and report the
 useful fraction of the loaded step capacity (CRC input bytes / bytes of steps
-executed by all groups).  Used to pick the log-record schedule.
+executed by all groups); replay_continuous models round 3's continuous rounds
+(rounds of a chunk back to back, swath by swath).  Used to pick the log-record schedule.
 
   python tools/sim_rounds.py --workload log --records 200000
 """
@@ -69,6 +70,28 @@ def replay(u0, u1, G, sw, window, chunk=None):
             "steps_per_round": round(steps / max(rounds, 1), 2)}
 
 
+def replay_continuous(u0, u1, G, window, chunk):
+    """Continuous rounds (round 3): a round runs max(m, 4) lines (m = its
+    longest region in lines); rounds of one chunk follow each other swath by
+    swath, a chunk's last round pads its step to the 4-swath boundary."""
+    S = steps_of(u0, u1, G, 1)
+    groups = 64 // G
+    swaths = 0
+    for c0 in range(0, len(u0), window):
+        s = np.sort(S[c0:c0 + window])[::-1]
+        for k0 in range(0, len(s), chunk):
+            c = s[k0:k0 + chunk]
+            pad = (-len(c)) % groups
+            c = np.concatenate([c, np.zeros(pad, c.dtype)]).reshape(-1, groups)
+            m = c.max(axis=1)
+            m = m[m > 0]
+            lines = int(np.maximum(m, 4).sum())
+            swaths += (lines + 3) // 4 * 4
+    useful = int((u1 - u0).sum())
+    return {"G": G, "continuous": True, "window": window, "chunk": chunk,
+            "useful_frac": round(useful / (swaths * groups * 16 * G), 4)}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="log")
@@ -78,6 +101,9 @@ def main() -> int:
     for G, sw in ((8, 4), (8, 2), (16, 2), (16, 4), (4, 4)):
         for window in (64, 128, 256, 512, 4096):
             print(replay(u0, u1, G, sw, window))
+    chunk = 64 if args.workload == "log" else 32
+    for window in (chunk, 512):
+        print(replay_continuous(u0, u1, 8, window, chunk))
     return 0
 
 
