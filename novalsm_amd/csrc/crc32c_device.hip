@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(256) split_finish_kernel(CrcParams p, int mode
 // per record and no header byte; a wrong estimate (unsorted offsets, a block
 // trailer) only costs padding, never a wrong CRC.  One workgroup per window,
 // counting sort in LDS (order within a line count is arbitrary).
-constexpr uint32_t kLogSortWin = 512;  // records per window (at most; g_tune_logwin)
+constexpr uint32_t kLogSortWin = 1024;  // records per window (at most; g_tune_logwin)
 constexpr uint32_t kLogSortBins = 288;  // line counts (a 32 KiB log block is 256 lines of 128 B)
 __global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint64_t* __restrict__ offs,
                                                        uint64_t n, uint64_t buf_len, uint32_t line,
@@ -783,6 +783,18 @@ int launch_burst_g(int V, CrcParams& p, DevTables* t, hipStream_t stream) {
 
 
 constexpr uint64_t kLogSortMin = 1u << 16;  // records: the log_sort_kernel pre-pass from here
+// Records per sort window: the power of two nearest to ~512 KiB of log.  A wider
+// window cuts more round padding but spreads a chunk's reads over more of the
+// image; measured over payloads U[1,512] .. U[1,16384] B the best window spanned
+// 0.25-1 MiB, and a fixed 512 records lost up to 15 points on large records
+// (profiles/r03_logsort_sweep6.log).
+uint32_t log_sort_window(uint64_t n, uint64_t bytes) {
+  const uint64_t avg = n && bytes / n ? bytes / n : 1;
+  const uint64_t w = (512u * 1024u) / avg;
+  uint32_t win = 64;
+  while (win < kLogSortWin && w >= win + win / 2) win *= 2;
+  return win;
+}
 
 }  // namespace
 
@@ -982,7 +994,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
       !log_sc.alloc(p.n_blocks * (mode == kLogWrite ? 9 : 5), stream)) {
     const uint64_t n = p.n_blocks;
     const int tw = g_tune_logwin.load() < 0 ? -g_tune_logwin.load() : g_tune_logwin.load();
-    const uint32_t win = (tw > 0 && tw <= (int)kLogSortWin) ? (uint32_t)tw : kLogSortWin;
+    const uint32_t win = (tw > 0 && tw <= (int)kLogSortWin) ? (uint32_t)tw : log_sort_window(n, p.buf_len);
     const bool by_pos = lsort == 2 || lsort == 3;
     uint32_t* perm = static_cast<uint32_t*>(log_sc.p);
     uint32_t* crc_pos = perm + n;  // log write only

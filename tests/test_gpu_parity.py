@@ -1552,7 +1552,8 @@ def test_logstream_preconditions(torch_gpu, oracle, case):
         assert np.array_equal(fresh.cpu().numpy(), exp)
 
 
-@pytest.mark.parametrize("order", ["file", "shuffled", "windows_only", "in_place", "unsorted"])
+@pytest.mark.parametrize("order", ["file", "shuffled", "windows_only", "in_place", "unsorted",
+                                   "window_1024", "window_64"])
 def test_log_sorted_windows(torch_gpu, oracle, order):
     """Log verify of >= 64K records runs in the order of the windowed
     step-count sort (log_sort_kernel), keyed from the offsets
@@ -1560,8 +1561,10 @@ def test_log_sorted_windows(torch_gpu, oracle, order):
     results are the oracle's whatever the key says: offsets in file order,
     shuffled (the keys are then garbage), the window sort without the
     per-chunk sort (diagnostics; log write sorted too, by position), results
-    stored in place (window 128), and no sort at all; write is bit-exact over
-    the image, verify finds exactly the corrupted records."""
+    stored in place (window 128), no sort at all, and the widest and narrowest
+    windows the adaptive choice takes (1024; 64 with log write sorted too);
+    write is bit-exact over the image, verify finds exactly the corrupted
+    records."""
     from novalsm_amd.synth import log_image
     torch = torch_gpu
     rng = np.random.default_rng(91)
@@ -1593,10 +1596,11 @@ def test_log_sorted_windows(torch_gpu, oracle, order):
         for v in victims:
             buf[int(offs[v]) + 6] ^= 0x02
 
-    if order in ("windows_only", "in_place", "unsorted"):
+    if order in ("windows_only", "in_place", "unsorted", "window_1024", "window_64"):
         with C.diagnostics() as L:
-            L.nova_diag_set_rounds_sort({"windows_only": 3, "in_place": 5, "unsorted": 0}[order])
-            L.nova_diag_set_log_window({"windows_only": -512, "in_place": -128, "unsorted": 0}[order])
+            L.nova_diag_set_rounds_sort({"windows_only": 3, "in_place": 5, "unsorted": 0}.get(order, 2))
+            L.nova_diag_set_log_window({"windows_only": -512, "in_place": -128, "unsorted": 0,
+                                        "window_1024": 1024, "window_64": -64}[order])
             run()
     else:
         run()

@@ -46,15 +46,15 @@ def timed(torch, fn, steps, warmup, stream):
     return sum(ms) / len(ms) / 1e3
 
 
-def log_layout(total_target: int, seed: int):
+def log_layout(total_target: int, seed: int, pmax: int = 4096):
     """A log file of ~total_target bytes as log::Writer lays it out
     (db/log_writer.cc:53-97, novalsm_amd/synth.log_layout): logical records of
-    U[1,4096] B payload from splitmix64(seed), fragmented at 32 KiB blocks.
+    U[1,pmax] B payload from splitmix64(seed), fragmented at 32 KiB blocks.
     Returns the physical records' (offsets, payload lengths, types, total)."""
     from novalsm_amd.synth import splitmix64_words, log_layout as writer_layout
-    n = total_target // (7 + 2048)
+    n = total_target // (7 + (pmax + 1) // 2)
     r = splitmix64_words(seed, 0, n)
-    plens = ((r % np.uint64(4096)) + np.uint64(1)).astype(np.int64)
+    plens = ((r % np.uint64(pmax)) + np.uint64(1)).astype(np.int64)
     offs, lens, types, _, total = writer_layout(plens)
     return offs, lens.astype(np.uint64), types, total
 
@@ -74,6 +74,8 @@ def main() -> int:
     ap.add_argument("--sort-sweep", default="",
                     help="log ops: comma list of nova_diag_set_rounds_sort values (0 in order, "
                          "2 windows + chunks, 3 windows only)")
+    ap.add_argument("--log-seed", type=int, default=6, help="log image: payload-length seed")
+    ap.add_argument("--log-payload-max", type=int, default=4096, help="log image: payloads U[1,max] B")
     ap.add_argument("--no-ablations", action="store_true", help="skip the diagnostics ablations")
     args = ap.parse_args()
     import torch
@@ -214,7 +216,8 @@ def main() -> int:
         torch.cuda.empty_cache()
 
     if "log_write" in ops or "log_verify" in ops:
-        offs_np, lens_np, types_np, total = log_layout(4 << 30, 6)
+        pmax = args.log_payload_max
+        offs_np, lens_np, types_np, total = log_layout(4 << 30, args.log_seed, pmax)
         n = len(offs_np)
         buf = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
         C.fill_splitmix64(buf, 41)
@@ -225,7 +228,7 @@ def main() -> int:
         buf[o + 5] = (ln >> 8).to(torch.uint8)
         buf[o + 6] = torch.from_numpy(types_np).cuda()
         sum_rec = int(lens_np.sum()) + 7 * n
-        wl = f"log image: {n} records, payload U[1,4096] B, {total / 2**30:.2f} GiB"
+        wl = f"log image: {n} records, payload U[1,{pmax}] B, {total / 2**30:.2f} GiB"
         sample = np.linspace(0, n - 1, 129).astype(np.int64)
         if "log_write" in ops:
             sec = timed(torch, lambda: C.log_write_crcs(buf, o, stream=stream), args.steps,
