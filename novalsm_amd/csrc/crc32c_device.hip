@@ -650,6 +650,15 @@ uint64_t flat_waves() {
 // the groups widen to 16 lanes with 4-block chunks, halving the steps per
 // block (tools/latency.py, profiles/r01_latency.log: 4K x 4 KiB verify
 // 77 -> 31 us, 64K blocks 83 -> 70 us; 256K blocks unchanged).
+//
+// Logs pass their mean record span (bytes per record) as bytes_per_block.
+// Short records run in 4-lane groups: twice the records per round halves the
+// per-record steps.  Measured crossover over payloads U[1,512] .. U[1,4096] B
+// (profiles/r03_log_lanes_sweep.log): verify gains 1.5-11 points below ~1 KiB
+// mean span and loses 7 at 2 KiB; write, which also pays a scattered store per
+// record, gains only below ~400 B (+3.5 at 263 B, -2 at 520 B).
+constexpr uint64_t kLogNarrowVerify = 1280;
+constexpr uint64_t kLogNarrowWrite = 400;
 Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, bool large,
           uint32_t cus) {
   const bool log = mode == kLogWrite || mode == kLogVerify;
@@ -669,6 +678,10 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, b
   if (pl.kernel == kFlatK || pl.kernel == kRoundsK) {
     pl.seg = 0;
     if (pl.G == 1) pl.G = 2;  // at most 32 groups per wave (chunk >= 2 groups <= 64)
+  }
+  if (pl.kernel == kRoundsK && log && tk == kAuto && tg == 0 && bytes_per_block &&
+      bytes_per_block < (mode == kLogVerify ? kLogNarrowVerify : kLogNarrowWrite)) {
+    pl.G = 4;  // short records: 4-lane groups (log verify then runs without the pre-sort)
   }
   if (pl.kernel == kRoundsK && log && tk == kAuto && tg == 0 && g_tune_chunk.load() == 0) {
     // log records (~2 KiB): 16-record chunks below 32 chunks' worth per wave
@@ -1154,7 +1167,7 @@ int nova_log_write_crcs(void* buf, size_t buf_len, const uint64_t* record_offset
   p.buf_len = buf_len;
   p.offsets = record_offsets;
   p.n_blocks = n_records;
-  return run(kLogWrite, p, false, 0, (hipStream_t)stream);
+  return run(kLogWrite, p, false, n_records ? buf_len / n_records : 0, (hipStream_t)stream);
 }
 
 int nova_log_verify_records(const void* buf, size_t buf_len, const uint64_t* record_offsets,
@@ -1167,7 +1180,7 @@ int nova_log_verify_records(const void* buf, size_t buf_len, const uint64_t* rec
   p.ok_out = ok_out;
   p.n_bad = n_bad_out;
   p.n_blocks = n_records;
-  return run(kLogVerify, p, false, 0, (hipStream_t)stream);
+  return run(kLogVerify, p, false, n_records ? buf_len / n_records : 0, (hipStream_t)stream);
 }
 
 int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_frags,

@@ -1552,7 +1552,7 @@ def test_logstream_preconditions(torch_gpu, oracle, case):
         assert np.array_equal(fresh.cpu().numpy(), exp)
 
 
-@pytest.mark.parametrize("order", ["file", "shuffled", "windows_only", "in_place", "unsorted",
+@pytest.mark.parametrize("order", ["file", "file_g8", "shuffled", "windows_only", "in_place", "unsorted",
                                    "window_1024", "window_64"])
 def test_log_sorted_windows(torch_gpu, oracle, order):
     """Log verify of >= 64K records runs in the order of the windowed
@@ -1564,7 +1564,9 @@ def test_log_sorted_windows(torch_gpu, oracle, order):
     stored in place (window 128), no sort at all, and the widest and narrowest
     windows the adaptive choice takes (1024; 64 with log write sorted too);
     write is bit-exact over the image, verify finds exactly the corrupted
-    records."""
+    records.  These records average ~0.7 KiB, so the default plan ("file")
+    runs 4-lane groups without the sort; every other case forces the 8-lane
+    groups the sort runs with."""
     from novalsm_amd.synth import log_image
     torch = torch_gpu
     rng = np.random.default_rng(91)
@@ -1596,8 +1598,11 @@ def test_log_sorted_windows(torch_gpu, oracle, order):
         for v in victims:
             buf[int(offs[v]) + 6] ^= 0x02
 
+    if order != "file":
+        C.set_tuning(8, 0)  # (reset by the autouse fixture)
     if order in ("windows_only", "in_place", "unsorted", "window_1024", "window_64"):
         with C.diagnostics() as L:
+            C.set_tuning(8, 0)  # the diagnostics library's own knob (reset on exit)
             L.nova_diag_set_rounds_sort({"windows_only": 3, "in_place": 5, "unsorted": 0}.get(order, 2))
             L.nova_diag_set_log_window({"windows_only": -512, "in_place": -128, "unsorted": 0,
                                         "window_1024": 1024, "window_64": -64}[order])

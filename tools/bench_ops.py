@@ -106,7 +106,7 @@ def main() -> int:
     def sweep(op, fn, alg_bytes):
         if not args.lanes_sweep:
             return
-        for g in (4, 8, 16):
+        for g in (2, 4, 8, 16):
             C.set_tuning(g, 0)  # default segment size
             sec = timed(torch, fn, args.steps, args.warmup, stream)
             print(json.dumps({"sweep": op, "lanes": g, "GBps": round(alg_bytes / sec / 1e9, 1),
