@@ -258,8 +258,8 @@ __global__ void __launch_bounds__(256) split_finish_kernel(CrcParams p, int mode
 // The rounds kernel pads a round's kGroups records to the longest; sorting each
 // claimed chunk of 64 records leaves ~21 % of the loaded step capacity as
 // padding on U[1,4096] B records (tools/sim_rounds.py).  This pre-pass sorts
-// windows of kLogSortWin consecutive records (~1 MiB of log, so a chunk's
-// records stay close together in memory) by their line count, largest first,
+// windows of consecutive records (~512 KiB of log, log_sort_window(), so a
+// chunk's records stay close together in memory) by line count, largest first,
 // into perm[]; the kernel then takes chunks of that order.  The key comes from
 // the offsets alone -- record i's length is at most the gap to the next
 // record's header or to its 32 KiB block's end -- so the pre-pass reads 8 B
