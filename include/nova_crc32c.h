@@ -182,7 +182,10 @@ int nova_sst_queue_stats(uint64_t* batches, uint64_t* requests, uint64_t* max_ta
  * written for them).
  * Verify: status_out[i] is one of NOVA_LOG_*; *n_bad_out (device u32, zeroed
  * by the caller, may be NULL) counts the records the reader reports as
- * corruption (CHECKSUM_MISMATCH, BAD_LENGTH). */
+ * corruption (CHECKSUM_MISMATCH, BAD_LENGTH).
+ * Performance only: the dispatch sizes its groups and sort windows from the
+ * mean record span buf_len / n_records, so pass the log's length, not a larger
+ * allocation (results are identical either way). */
 #define NOVA_LOG_CHECKSUM_MISMATCH 0 /* :251-262 "checksum mismatch" */
 #define NOVA_LOG_OK 1                /* Unmask(stored) == Value(header+6, 1+length) */
 #define NOVA_LOG_BAD_LENGTH 2        /* :228-235 "bad record length": payload past a full block (not read) */
