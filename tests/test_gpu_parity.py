@@ -1611,6 +1611,38 @@ def test_log_sorted_windows(torch_gpu, oracle, order):
         run()
 
 
+@pytest.mark.parametrize("pmax", [64, 600, 1500, 3000])
+def test_log_plan_by_record_size(torch_gpu, oracle, pmax):
+    """The default log plan picks its group width from the mean record span
+    (buf_len / n): 4-lane groups for write below 400 B and for verify below
+    1280 B, 8-lane groups with the windowed pre-sort above.
+    Each side of both thresholds: write is bit-exact over the image, verify is
+    clean, and finds exactly the records whose payload was corrupted."""
+    from novalsm_amd.synth import log_image
+    torch = torch_gpu
+    rng = np.random.default_rng(pmax)
+    n = max(70000, (48 << 20) // (pmax // 2 + 7))
+    n = min(n, 300000)
+    plen = rng.integers(1, pmax + 1, n)
+    host, offs, _, _ = log_image(31, plen)
+    assert len(offs) >= 1 << 16
+    buf = dev(torch, host)
+    doffs = dev(torch, offs, torch.int64)
+    want = host.copy()
+    oracle.log_write(want, offs)
+    C.log_write_crcs(buf, doffs)
+    assert np.array_equal(buf.cpu().numpy(), want)
+    ok, bad = C.log_verify_records(buf, doffs)
+    assert (ok.cpu().numpy() == C.LOG_OK).all() and int(bad.item()) == 0
+    victims = rng.choice(len(offs), 50, replace=False)
+    for v in victims:
+        buf[int(offs[v]) + 6] ^= 0x02  # the type byte is CRC input
+    ok, bad = C.log_verify_records(buf, doffs)
+    okh = ok.cpu().numpy()
+    assert sorted(np.nonzero(okh == C.LOG_CHECKSUM_MISMATCH)[0].tolist()) == sorted(victims.tolist())
+    assert int(bad.item()) == len(victims)
+
+
 @pytest.mark.parametrize("kernel", ["default", "logstream"])
 def test_log_96mib(torch_gpu, oracle, kernel):
     """A 96 MiB log::Writer image with U[1,4096] B payloads (the bench_ops log
