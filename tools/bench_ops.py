@@ -76,6 +76,8 @@ def main() -> int:
                          "2 windows + chunks, 3 windows only)")
     ap.add_argument("--log-seed", type=int, default=6, help="log image: payload-length seed")
     ap.add_argument("--log-payload-max", type=int, default=4096, help="log image: payloads U[1,max] B")
+    ap.add_argument("--chunk-sweep", default="",
+                    help="comma list of rounds-kernel chunk sizes (nova_diag_set_chunk_blocks), log ops")
     ap.add_argument("--no-ablations", action="store_true", help="skip the diagnostics ablations")
     args = ap.parse_args()
     import torch
@@ -101,6 +103,14 @@ def main() -> int:
                 D.nova_diag_set_log_window(0)
             print(json.dumps({"sweep": op, "rounds_sort": int(so), "log_window": int(win or 0),
                               "GBps": round(alg_bytes / sec / 1e9, 1),
+                              "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}), flush=True)
+
+    def chunk_sweep(op, fn, alg_bytes):
+        for c in [int(x) for x in args.chunk_sweep.split(",") if x]:
+            with C.diagnostics() as D:
+                D.nova_diag_set_chunk_blocks(c)
+                sec = timed(torch, fn, args.steps, args.warmup, stream)
+            print(json.dumps({"sweep": op, "chunk": c, "GBps": round(alg_bytes / sec / 1e9, 1),
                               "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}), flush=True)
 
     def sweep(op, fn, alg_bytes):
@@ -242,6 +252,7 @@ def main() -> int:
             emit("log_write", wl, sum_rec, sec, ok)
             sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
             sort_sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
+            chunk_sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
             for var, name in (() if args.no_ablations else ((3, "log_write_pieces"), (4, "log_write_pieces_nt"),
                               (5, "log_write_pieces_no_writes"), (6, "log_write_no_writes"),
                               (7, "log_write_no_epilogue"))):
@@ -265,6 +276,7 @@ def main() -> int:
             ok = int(bad.item()) == 0 and bool((okb.cpu().numpy() == C.LOG_OK).all())
             emit("log_verify", wl, sum_rec + n, sec, ok)
             sort_sweep("log_verify", lv, sum_rec + n)
+            chunk_sweep("log_verify", lv, sum_rec + n)
             for var, name in (() if args.no_ablations else
                               ((0, "log_verify_no_writes"), (256, "log_verify_no_tail_loads_no_writes"))):
                 with C.diagnostics() as D:  # timing ablations (no result writes; 256: WRONG CRCs)
