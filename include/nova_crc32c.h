@@ -143,27 +143,50 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
                                   size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
                                   uint32_t flags, void* stream);
 
-/* ---- coalescing queue for concurrent per-SSTable callers -----------------
+/* ---- per-SSTable calls from many threads: the persistent engine ----------
  * The same operations as nova_sstable_write_trailers / _verify_blocks (same
  * arguments, same results), host-synchronous: the call returns when the
- * trailers / ok flags / n_bad are written.  Concurrent calls from different
- * threads are grouped into one launch (crc32c_queue.hip):
- * NovaLSM's compaction and reader threads each checksum one SSTable per call
- * (ltc/stoc_file_client_impl.cpp:274-289, table/table.cc:425-441), too little
- * work per launch to fill the device alone.  Work queued on `stream` before
- * the call (the image, its descriptors) completes first: the call
- * synchronises `stream` when it is busy.  A call alone in the queue runs as
- * the plain call on `stream`; a table of more than 2^20 blocks always does.
- * NOVA_SST_QUEUE_SLOTS (1..4, default 4): batches in flight at once;
- * nova_sst_queue_set_slots overrides it for this device (0: back to it). */
+ * trailers / ok flags / n_bad are in device memory.  NovaLSM's compaction and
+ * reader threads each checksum one SSTable per call
+ * (ltc/stoc_file_client_impl.cpp:274-289, :843-882, table/table.cc:425-441):
+ * too little work for a launch of its own.  These calls run on a persistent
+ * kernel (crc32c_engine.hip) that stays resident while
+ * requests arrive -- one workgroup per CU, tables loaded once -- and exits
+ * after NOVA_SST_ENGINE_IDLE_US (default 1000) without one; the next call
+ * starts it again.  While it is resident it holds every CU's LDS, so this
+ * process's other kernels (plain calls included) wait for its idle exit.
+ * Work queued on `stream` before the call (the image, its descriptors)
+ * completes first: the call synchronises `stream` when it is busy.  A table
+ * of more than 2^20 blocks runs as the plain call on `stream`, and so does a
+ * request the engine cannot run (no device memory, an engine error, or
+ * NOVA_SST_ENGINE_TIMEOUT_MS, default 10000, without a result; the engine is
+ * then not used again by this process; a verify counter is zeroed before the
+ * plain call recomputes it).  NOVA_SST_ENGINE=0: the round-3 coalescing
+ * queue instead (concurrent calls grouped into shared launches,
+ * NOVA_SST_QUEUE_SLOTS 1..4 batches in flight, nova_sst_queue_set_slots;
+ * DESIGN.md 3.5d). */
 int nova_sst_queue_write_trailers(void* buf, const uint64_t* offsets, const uint32_t* sizes,
                                   size_t n_blocks, uint32_t flags, void* stream);
 int nova_sst_queue_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
                                  size_t n_blocks, uint8_t* ok_out, uint32_t* n_bad_out,
                                  void* stream);
 int nova_sst_queue_set_slots(int slots);
-/* Batches launched, requests served, most tables in one batch (this device). */
+/* Coalescing queue (NOVA_SST_ENGINE=0): batches launched, requests served,
+ * most tables in one batch (this device). */
 int nova_sst_queue_stats(uint64_t* batches, uint64_t* requests, uint64_t* max_tables_per_batch);
+
+/* The engine of this device: start it now (it also starts on the first
+ * queued call), stop it (waits for requests in flight; the next call starts
+ * it again), its counters (requests run, instances launched, requests that
+ * fell back to the plain call, whether an instance is resident), and the idle
+ * time before an instance exits (from the next instance; 0: 1000 us). */
+int nova_sst_engine_start(void);
+int nova_sst_engine_stop(void);
+int nova_sst_engine_stats(uint64_t* requests, uint64_t* launches, uint64_t* fallbacks, int* running);
+int nova_sst_engine_set_idle_us(uint32_t us);
+/* Route the nova_sst_queue_* calls of this process: 1 the engine, 0 the
+ * coalescing queue, -1 back to NOVA_SST_ENGINE (default: the engine). */
+int nova_sst_engine_set_enabled(int on);
 
 /* ---- MANIFEST / write-ahead log records ----------
  * buf holds buf_len bytes of a log file image starting at a 32 KiB log-block
@@ -273,7 +296,9 @@ const char* nova_crc32c_kernel_name(int lanes_per_unit);
  * (0 = auto).  Per calling thread: other threads keep the automatic plan. */
 void nova_crc32c_set_tuning(int lanes_per_unit, uint32_t seg_bytes);
 const char* nova_error_string(int err);
-/* ABI version: bump on any signature change (2: log entry points take buf_len). */
+/* ABI version: bump on any signature or result-meaning change (2: log entry
+ * points take buf_len; 3: log verify status NOVA_LOG_BLOCK_TRAILER (5), not
+ * counted in n_bad, and the nova_sst_engine_* entry points). */
 int nova_crc32c_abi_version(void);
 
 /* ---- diagnostics: libnova_crc32c_diag.so ONLY ---------------------------

@@ -28,7 +28,8 @@ LIB = os.path.join(LIB_DIR, "libnova_crc32c.so")
 DIAG_LIB = os.path.join(LIB_DIR, "libnova_crc32c_diag.so")
 ARCH = os.environ.get("NOVA_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["crc32c_device.hip", "crc32c_stream.cpp", "crc32c_host.cpp", "crc32c_queue.hip"]
+SOURCES = ["crc32c_device.hip", "crc32c_stream.cpp", "crc32c_host.cpp", "crc32c_queue.hip",
+           "crc32c_engine.hip"]
 DIAG_SOURCE = "crc32c_diag.hip"
 HEADERS = ["gf2_crc32c.hpp", "crc32c_kernels.hpp", "crc32c_internal.hpp",
            os.path.join("..", "..", "include", "nova_crc32c.h"),

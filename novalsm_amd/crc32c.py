@@ -62,6 +62,11 @@ _SIG = {
     "nova_sst_queue_verify_blocks": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "nova_sst_queue_stats": (_i32, [_vp, _vp, _vp]),
     "nova_sst_queue_set_slots": (_i32, [ctypes.c_int]),
+    "nova_sst_engine_start": (_i32, []),
+    "nova_sst_engine_stop": (_i32, []),
+    "nova_sst_engine_stats": (_i32, [_vp, _vp, _vp, _vp]),
+    "nova_sst_engine_set_idle_us": (_i32, [_u32]),
+    "nova_sst_engine_set_enabled": (_i32, [ctypes.c_int]),
     "nova_crc32c_stream_host": (_i32, [_vp, _u64, _u32, _sz, _vp, _u32, _sz, _i32]),
     "nova_crc32c_batch_host": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _sz, _i32]),
     "nova_sstable_write_trailers_host": (_i32, [_vp, _vp, _vp, _sz, _u32, _sz, _i32]),
@@ -100,7 +105,7 @@ _DIAG_SIG = {
     "nova_diag_read_stream": (_i32, [_vp, _sz, _vp, _i32, _vp]),
     "nova_diag_read_ceiling": (_i32, [_vp, _sz, _vp, _i32, _i32, _vp]),
 }
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # log verify status codes (include/nova_crc32c.h, db/log_reader.cc:228-262)
 LOG_CHECKSUM_MISMATCH = 0
@@ -414,6 +419,37 @@ def queue_stats() -> dict:
     v = [ctypes.c_uint64(0) for _ in range(3)]
     _check(_L().nova_sst_queue_stats(*[ctypes.byref(x) for x in v]), "nova_sst_queue_stats")
     return {"batches": v[0].value, "requests": v[1].value, "max_tables": v[2].value}
+
+
+def engine_start() -> None:
+    """Start the persistent per-SSTable engine now (queue_* calls start it too)."""
+    _check(_L().nova_sst_engine_start(), "nova_sst_engine_start")
+
+
+def engine_stop() -> None:
+    """Stop the engine (requests in flight finish first; the next queue_* call
+    starts it again)."""
+    _check(_L().nova_sst_engine_stop(), "nova_sst_engine_stop")
+
+
+def engine_stats() -> dict:
+    v = [ctypes.c_uint64(0) for _ in range(3)]
+    run = ctypes.c_int(0)
+    _check(_L().nova_sst_engine_stats(*[ctypes.byref(x) for x in v], ctypes.byref(run)),
+           "nova_sst_engine_stats")
+    return {"requests": v[0].value, "launches": v[1].value, "fallbacks": v[2].value,
+            "running": bool(run.value)}
+
+
+def engine_set_enabled(on: int) -> None:
+    """Route queue_* calls: 1 the persistent engine, 0 the coalescing queue,
+    -1 the NOVA_SST_ENGINE default."""
+    _check(_L().nova_sst_engine_set_enabled(int(on)), "nova_sst_engine_set_enabled")
+
+
+def engine_set_idle_us(us: int) -> None:
+    """Idle time before an engine instance exits (from the next instance)."""
+    _check(_L().nova_sst_engine_set_idle_us(int(us)), "nova_sst_engine_set_idle_us")
 
 
 def log_write_crcs(buf, record_offsets, stream=None, buf_len: Optional[int] = None):

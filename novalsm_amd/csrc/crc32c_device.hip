@@ -359,11 +359,14 @@ __global__ void __launch_bounds__(256) log_unperm_kernel(uint8_t* base, const ui
 //   lie between two blocks of the image, so inside the caller's allocation.
 //   Windows are aligned in absolute addresses (ba = the image base), as the
 //   kernels that store them see them.
+//   last (may be null): blocks that are never eligible (the first and last
+//   block of each table of a coalesced batch: their windows may reach another
+//   caller's memory, crc32c_queue.hip).
 __global__ void __launch_bounds__(256) trailer_layout_kernel(uint64_t ba, const uint64_t* offsets,
                                                              uint64_t omask, const uint32_t* lengths,
                                                              uint64_t lmask, uint64_t stride,
                                                              uint32_t len, uint64_t n, uint32_t* elig,
-                                                             uint32_t* flag) {
+                                                             uint32_t* flag, const uint8_t* last) {
   const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
   bool bad = false;
   auto u0_of = [&](uint64_t i) { return ba + offsets[i & omask] + i * stride; };
@@ -377,6 +380,7 @@ __global__ void __launch_bounds__(256) trailer_layout_kernel(uint64_t ba, const 
       e = e && u1_of(i + 1) >= we;
     }
     e = e && (i == 0 ? ws >= u0 : u1_of(i - 1) + 5 <= ws);
+    if (last) e = e && !last[i];
     elig[i] = e ? 1u : 0u;
   }
   if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
@@ -824,7 +828,7 @@ int trailer_layout(const CrcParams& p, DevTables* t, hipStream_t stream, uint32_
   const uint32_t* ll = p.lengths ? p.lengths : t->zero_word;
   hipLaunchKernelGGL(trailer_layout_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, lo,
                      p.offsets ? ~0ull : 0ull, ll, p.lengths ? ~0ull : 0ull, p.offsets ? 0ull : p.stride,
-                     p.lengths ? 0u : p.len, p.n_blocks, elig, flag);
+                     p.lengths ? 0u : p.len, p.n_blocks, elig, flag, p.tr_last);
   return (int)hipGetLastError();
 }
 
@@ -1075,7 +1079,7 @@ uint32_t cus_hint() {
 
 extern "C" {
 
-int nova_crc32c_abi_version(void) { return 2; }
+int nova_crc32c_abi_version(void) { return 3; }
 
 int nova_device_init(void) {
   int err = 0;

@@ -1,0 +1,706 @@
+// Persistent per-SSTable engine.
+//
+// NovaLSM checksums one SSTable per call (~4K blocks, ~16.5 MiB) from many
+// threads at once: the flush and compaction EnvBGThreads finishing tables
+// (ltc/compaction_thread.h:77-107, StoCWritableFileClient::Format,
+// ltc/stoc_file_client_impl.cpp:183-377) and readers verifying a fetched
+// table (ReadAll, :843-882; table/table.cc:425-441).  One such table is
+// ~2.6 us of HBM time, but a launch of any kernel over it pays a fixed
+// ~25-29 us (launch, LDS table fill, ramp, tail: DESIGN.md 3.5d), so
+// per-table launches -- direct, or coalesced by a host queue -- stay at
+// 14-29 % of the HBM roofline.
+//
+// The engine pays the launch and the table fill once per burst of requests:
+//   * one workgroup per CU stays resident with the units kernel's LDS tables
+//     (crc32c_units_kernel, whole blocks as units, G lanes per block);
+//   * a submitting thread writes its request (image, descriptor arrays,
+//     outputs, op) into a ring in pinned host memory and bumps a tail word;
+//   * wave 0 of workgroup 0 -- the dispatcher -- polls the tail, copies new
+//     requests into device-memory slots and publishes their chunk tickets
+//     (chunks of cb blocks) by advancing one end word;
+//   * every other wave takes tickets from its XCD's head (eight heads: one
+//     device-scope atomic per ticket, MI355X_MICROARCH.md "dequeue"), claims
+//     the next ticket while it checksums the current chunk with the units
+//     kernel's chunk body (units_chunk), and counts the chunk done; the wave
+//     that finishes a request's last chunk writes the request's completion
+//     word in pinned host memory, on which its submitter spins.
+// Once no request arrives for the idle time (default 1 ms) and every taken
+// request is done, the dispatcher stops the workers and the kernel exits,
+// recording the first request it did not take; a submitter that finds its
+// request untaken relaunches the engine, which starts there.  Every spin is
+// bounded: workers give up (error word) after 20 s without new tickets and no
+// stop, the dispatcher after 20 s with a request unfinished and none new,
+// submitters after NOVA_SST_ENGINE_TIMEOUT_MS; a failed or
+// timed-out request is recomputed by the plain call (crc32c_queue.hip), so
+// results never depend on the engine.
+//
+// Memory visibility (cdna_hip_programming.md Guideline 16):
+//   * host -> engine: requests and the tail word are read with system-scope
+//     loads (fine-grained host memory, no cache);
+//   * dispatcher -> workers: slot fields and the end word are stored and
+//     loaded with agent-scope atomics (write-through, L1-bypassing), drained
+//     before the end word is advanced;
+//   * caller memory: the chunk body loads descriptors, block bytes and stored
+//     CRCs non-temporally (kVarEngine), so no L1 line of a buffer rewritten
+//     since an earlier request is used;
+//   * results: stored write-through (agent-scope atomic stores) and drained
+//     (s_waitcnt vmcnt(0)) before the chunk's done count is added -- no L2
+//     write-back fence, which at one per chunk serialised the engine at
+//     ~15 us per request; the last chunk's wave then stores the completion
+//     word (system scope).
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+
+#include "crc32c_kernels.hpp"
+
+namespace {
+
+using namespace nova_dev;
+
+constexpr uint32_t kRing = 1024;  // requests in flight (host ring and device slots)
+constexpr int kEngG = 16;         // lanes per block (units kernel: G = 16)
+constexpr int kEngMaxWaves = 12;  // launch bound (the units kernel's: 168 VGPRs)
+constexpr uint32_t kXcds = 8;
+
+struct EngHostReq {  // a host ring entry (64 B), written by its submitter
+  uint64_t base, offs, sizes, out, bad, n;
+  uint32_t mode, flags;
+  uint32_t cb, pad;
+};
+struct EngSlot {  // a device slot (128 B), written by the dispatcher
+  uint64_t seq1;          // request seq + 1 (0: never written)
+  uint64_t cstart, cend;  // its chunk tickets [cstart, cend)
+  uint64_t base, offs, sizes, out, bad, n;
+  uint32_t mode, flags, cb, pad;
+  uint64_t pad2[3];
+};
+struct EngCtl {  // pinned host memory (fine-grained)
+  uint64_t htail;  // host: requests [first_seq, htail) are in the ring
+  uint32_t hstop;  // host: exit once idle
+  uint32_t pad0;
+  uint64_t pad1[14];
+  uint64_t consumed;  // engine: the first seq it did not take (valid once exited)
+  uint32_t exited;    // engine: this instance takes no more requests
+  uint32_t error;     // engine: give-up code (1: a worker saw no new ticket for the give-up
+                      // time, 2: a published ticket without a slot, 3: a request unfinished
+                      // for the give-up time after the last arrival)
+  uint64_t pad2[14];
+};
+struct EngDev {  // device memory, zeroed before every launch
+  uint64_t dend;  // chunk tickets published
+  uint64_t p0[15];
+  uint32_t dstop;
+  uint32_t p1[31];
+  uint64_t reqs_done;
+  uint64_t p2[15];
+  uint32_t head[kXcds][32];  // per-XCD ticket heads, one 128-B line each
+  uint32_t cdone[kRing];     // chunks finished, per slot
+  EngSlot slot[kRing];
+};
+struct EngParams {
+  const EngHostReq* hring;
+  uint64_t* hdone;  // hdone[seq % kRing] = seq + 1 once the request's results are in memory
+  EngCtl* ctl;
+  EngDev* dev;
+  uint64_t first_seq;
+  uint64_t idle_ticks;     // s_memrealtime ticks (100 MHz) without a request before exiting
+  uint64_t give_up_ticks;  // no new ticket (worker) / an unfinished request (dispatcher) this long: exit
+  CrcParams tab;           // tables and zero line for every chunk
+};
+
+typedef __attribute__((address_space(1))) uint32_t g32;
+typedef __attribute__((address_space(1))) uint64_t g64;
+
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* a) {
+  return __hip_atomic_load((const __attribute__((address_space(1))) T*)a, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T* a, T v) {
+  __hip_atomic_store((__attribute__((address_space(1))) T*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_sys(const T* a) {
+  return __hip_atomic_load((const __attribute__((address_space(1))) T*)a, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ void st_sys(T* a, T v) {
+  __hip_atomic_store((__attribute__((address_space(1))) T*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Wave 0 of workgroup 0: host ring -> device slots, tickets published.
+__device__ void engine_dispatch(const EngParams& e) {
+  const int lane = threadIdx.x & 63;
+  EngDev* d = e.dev;
+  uint64_t seen = e.first_seq, cend = 0;
+  uint64_t last = now_ticks();
+  for (;;) {
+    uint64_t ht = 0;
+    if (lane == 0) ht = ld_sys(&e.ctl->htail);
+    ht = uni64(ht);
+    if (ht > seen) {
+      const uint32_t m = (uint32_t)(ht - seen < 64 ? ht - seen : 64);
+      EngHostReq r{};
+      uint64_t nch = 0;
+      if ((uint32_t)lane < m) {
+        const EngHostReq* h = e.hring + (seen + lane) % kRing;
+        r.base = ld_sys(&h->base);
+        r.offs = ld_sys(&h->offs);
+        r.sizes = ld_sys(&h->sizes);
+        r.out = ld_sys(&h->out);
+        r.bad = ld_sys(&h->bad);
+        r.n = ld_sys(&h->n);
+        r.mode = ld_sys(&h->mode);
+        r.flags = ld_sys(&h->flags);
+        r.cb = ld_sys(&h->cb);
+        if (r.cb == 0 || r.cb > 16) r.cb = 16;
+        nch = (r.n + r.cb - 1) / r.cb;
+      }
+      // inclusive prefix of the chunk counts over the lanes
+      uint64_t inc = nch;
+#pragma unroll
+      for (int s = 1; s < 64; s <<= 1) {
+        const uint64_t o = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(inc >> 32), s) << 32) |
+                           (uint32_t)__shfl_up((int)(uint32_t)inc, s);
+        if (lane >= s) inc += o;
+      }
+      if ((uint32_t)lane < m) {
+        const uint64_t seq = seen + lane;
+        EngSlot* S = &d->slot[seq % kRing];
+        st_agent(&d->cdone[seq % kRing], 0u);  // the slot's previous request (seq - kRing) is done
+        st_agent(&S->cstart, cend + inc - nch);
+        st_agent(&S->cend, cend + inc);
+        st_agent(&S->base, r.base);
+        st_agent(&S->offs, r.offs);
+        st_agent(&S->sizes, r.sizes);
+        st_agent(&S->out, r.out);
+        st_agent(&S->bad, r.bad);
+        st_agent(&S->n, r.n);
+        st_agent(&S->mode, r.mode);
+        st_agent(&S->flags, r.flags);
+        st_agent(&S->cb, r.cb);
+        st_agent(&S->seq1, seq + 1);
+      }
+      const uint64_t total = uni64(((uint64_t)(uint32_t)__shfl((int)(uint32_t)(inc >> 32), 63) << 32) |
+                                   (uint32_t)__shfl((int)(uint32_t)inc, 63));
+      drain_vm();  // every lane's slot stores are written through before the end moves
+      cend += total;
+      if (lane == 0) st_agent(&d->dend, cend);
+      seen += m;
+      last = now_ticks();
+      continue;
+    }
+    uint32_t stop = 0;
+    if (lane == 0) stop = ld_sys(&e.ctl->hstop);
+    stop = uni32(stop);
+    const uint64_t quiet = now_ticks() - last;
+    if (stop || quiet > e.idle_ticks) {
+      uint64_t done = 0;
+      if (lane == 0) done = ld_agent(&d->reqs_done);
+      const bool all_done = uni64(done) == seen - e.first_seq;  // every request taken is finished
+      // a request unfinished long after the last arrival cannot finish: give up
+      const bool lost = !all_done && quiet > e.give_up_ticks;
+      if (all_done || lost) {
+        if (lane == 0) {
+          if (lost) st_sys(&e.ctl->error, 3u);
+          st_agent(&d->dstop, 1u);
+          st_sys(&e.ctl->consumed, seen);
+          __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)&e.ctl->exited, 1u,
+                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+      }
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
+// Every other wave: tickets -> chunks of the units kernel's body.
+template <int G>
+__device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wpre) {
+  const int lane = threadIdx.x & 63;
+  EngDev* d = e.dev;
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & (kXcds - 1);
+  auto claim = [&]() -> uint64_t {
+    uint32_t k = 0;
+    if (lane == 0)
+      k = __hip_atomic_fetch_add((g32*)&d->head[xcc][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return xcc + (uint64_t)kXcds * uni32(k);
+  };
+  uint64_t r = e.first_seq;  // request cursor (the wave's tickets only grow)
+  uint64_t dend = 0;
+  uint64_t t = claim();
+  for (;;) {
+    if (t >= dend) {  // wait for the ticket to be published, or for the stop
+      uint64_t t0 = now_ticks();
+      for (uint32_t spin = 0;; spin++) {
+        uint64_t x = 0;
+        uint32_t stop = 0;
+        if (lane == 0) {
+          x = ld_agent(&d->dend);
+          stop = ld_agent(&d->dstop);
+        }
+        x = uni64(x);
+        if (t < x) {
+          dend = x;
+          break;
+        }
+        if (uni32(stop)) return;
+        if (x != dend) {  // progress: restart the give-up clock
+          dend = x;
+          t0 = now_ticks();
+        } else if (now_ticks() - t0 > e.give_up_ticks) {
+          if (lane == 0) st_sys(&e.ctl->error, 1u);
+          return;
+        }
+        if (spin < 32)
+          __builtin_amdgcn_s_sleep(2);
+        else
+          __builtin_amdgcn_s_sleep(12);
+      }
+    }
+    // The request holding ticket t.  Slot r % kRing is reused for seq
+    // r + kRing only after request r is done, and a live request's seq is
+    // above (newest written seq) - kRing, so a slot found holding a newer
+    // seq s1 - 1 moves the cursor to s1 - kRing (still at or below it).
+    EngSlot* S = nullptr;
+    for (;;) {
+      S = &d->slot[r % kRing];
+      uint64_t s1 = 0, ce = 0;
+      if (lane == 0) {
+        s1 = ld_agent(&S->seq1);
+        ce = ld_agent(&S->cend);
+      }
+      s1 = uni64(s1);
+      ce = uni64(ce);
+      if (s1 > r + 1) {
+        r = s1 - kRing > r + 1 ? s1 - kRing : r + 1;
+        continue;
+      }
+      if (s1 == r + 1 && t >= ce) {
+        r++;
+        continue;
+      }
+      if (s1 == r + 1) break;
+      if (lane == 0) st_sys(&e.ctl->error, 2u);  // published tickets with no slot: cannot happen
+      return;
+    }
+    uint64_t cstart = 0, cend = 0, base = 0, offs = 0, sizes = 0, out = 0, bad = 0, n = 0;
+    uint32_t mode = 0, flags = 0, cb = 0;
+    if (lane == 0) {
+      cstart = ld_agent(&S->cstart);
+      cend = ld_agent(&S->cend);
+      base = ld_agent(&S->base);
+      offs = ld_agent(&S->offs);
+      sizes = ld_agent(&S->sizes);
+      out = ld_agent(&S->out);
+      bad = ld_agent(&S->bad);
+      n = ld_agent(&S->n);
+      mode = ld_agent(&S->mode);
+      flags = ld_agent(&S->flags);
+      cb = ld_agent(&S->cb);
+    }
+    cstart = uni64(cstart);
+    cend = uni64(cend);
+    CrcParams p = e.tab;
+    p.base = (const uint8_t*)uni64(base);
+    p.offsets = (const uint64_t*)uni64(offs);
+    p.lengths = (const uint32_t*)uni64(sizes);
+    p.n_blocks = uni64(n);
+    p.flags = uni32(flags);
+    p.chunk = uni32(cb);
+    mode = uni32(mode);
+    const uint64_t nt = claim();  // the next ticket, in flight during this chunk
+    const uint64_t c = t - cstart;
+    if (mode == kVerify) {
+      p.ok_out = (uint8_t*)uni64(out);
+      p.n_bad = (uint32_t*)uni64(bad);
+      units_chunk<G, kVerify, kVarEngine>(lds, p, c, wpre);
+    } else if (mode == kTrailer) {
+      units_chunk<G, kTrailer, kVarEngine>(lds, p, c, wpre);
+    } else {
+      p.out = (uint32_t*)uni64(out);
+      units_chunk<G, kStore, kVarEngine>(lds, p, c, wpre);
+    }
+    // publish the chunk: its results were stored write-through (st_through);
+    // once drained they are in memory, so the count needs no release fence
+    drain_vm();
+    if (lane == 0) {
+      const uint32_t prev = __hip_atomic_fetch_add((g32*)&d->cdone[r % kRing], 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint64_t)prev + 1 == cend - cstart) {  // the request's last chunk: every other
+        // chunk's wave drained its results before its add, this one before its own
+        st_sys(&e.hdone[r % kRing], r + 1);
+        __hip_atomic_fetch_add((g64*)&d->reqs_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    t = nt;
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(kEngMaxWaves * 64) crc32c_engine_kernel(EngParams e) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
+  lds_fill_tables(lds, e.tab.tab_main, e.tab.tab_tree, kLevels * kTreeBytes / 16, nullptr, 0);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  if (blockIdx.x == 0 && wave == 0) {
+    engine_dispatch(e);
+    return;
+  }
+  uint32_t* wpre = reinterpret_cast<uint32_t*>(lds + kMainBytes + kLevels * kTreeBytes + wave * kWaveScratch);
+  engine_work<G>(e, lds, wpre);
+}
+
+template <int G>
+constexpr size_t engine_lds(int waves) {
+  return kMainBytes + (2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16)) * kTreeBytes + waves * kWaveScratch;
+}
+
+// ---- host side --------------------------------------------------------------
+uint64_t env_u64(const char* name, uint64_t def) {
+  const char* v = getenv(name);
+  if (!v || !*v) return def;
+  char* end = nullptr;
+  const unsigned long long x = strtoull(v, &end, 10);
+  return end && *end == 0 ? (uint64_t)x : def;
+}
+
+struct Engine {
+  std::mutex mu;
+  bool ready = false, broken = false, running = false;
+  int dev = 0;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+  EngHostReq* ring = nullptr;  // pinned
+  uint64_t* hdone = nullptr;   // pinned
+  EngCtl* ctl = nullptr;       // pinned
+  EngDev* ddev = nullptr;
+  uint64_t next_seq = 0;     // the next request's seq
+  uint64_t inst_first = 0;   // the running instance's first seq
+  uint64_t gen = 0;          // instances launched
+  std::atomic<uint64_t> inflight{0};
+  uint64_t requests = 0, relaunches = 0, fallbacks = 0;
+  uint32_t idle_us = 0, waves = 0;
+
+  int init_locked(int d) {
+    if (ready) return 0;
+    dev = d;
+    int err = 0;
+    DevTables* t = tables(&err);
+    if (!t) return err;
+    cus = t->cus;
+    hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+    if (e == hipSuccess)
+      e = hipHostMalloc((void**)&ring, sizeof(EngHostReq) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess)
+      e = hipHostMalloc((void**)&hdone, sizeof(uint64_t) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess)
+      e = hipHostMalloc((void**)&ctl, sizeof(EngCtl), hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) e = hipMalloc((void**)&ddev, sizeof(EngDev));
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)engine_lds<kEngG>(kEngMaxWaves));
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      broken = true;
+      return (int)e;
+    }
+    memset(ring, 0, sizeof(EngHostReq) * kRing);
+    memset(hdone, 0, sizeof(uint64_t) * kRing);
+    memset(ctl, 0, sizeof(EngCtl));
+    if (!idle_us) idle_us = (uint32_t)env_u64("NOVA_SST_ENGINE_IDLE_US", 1000);
+    waves = (uint32_t)env_u64("NOVA_SST_ENGINE_WAVES", kEngMaxWaves);
+    if (waves < 2 || waves > (uint32_t)kEngMaxWaves) waves = kEngMaxWaves;
+    ready = true;
+    return 0;
+  }
+
+  // A fresh instance over requests [first, ...): the previous one has exited.
+  int launch_locked(uint64_t first) {
+    hipError_t e = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = hipMemsetAsync(ddev, 0, sizeof(EngDev), stream);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      broken = true;
+      return (int)e;
+    }
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    volatile EngCtl* c = ctl;
+    c->exited = 0;
+    c->consumed = 0;
+    c->hstop = 0;
+    c->error = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    int err = 0;
+    DevTables* t = tables(&err);
+    if (!t) return err;
+    EngParams p{};
+    p.hring = ring;
+    p.hdone = hdone;
+    p.ctl = ctl;
+    p.dev = ddev;
+    p.first_seq = first;
+    p.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
+    p.give_up_ticks = 20ull * 100000000ull;  // 20 s (every spin of the engine is bounded)
+    p.tab.tab_main = t->main[gindex(kEngG)];
+    p.tab.tab_tree = t->tree;
+    p.tab.tab_ft = t->ft;
+    p.tab.tab_sh16 = t->sh16;
+    p.tab.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
+    p.tab.seg = 0;  // whole blocks are units
+    hipLaunchKernelGGL((crc32c_engine_kernel<kEngG>), dim3((uint32_t)cus), dim3(64 * waves),
+                       engine_lds<kEngG>((int)waves), stream, p);
+    e = hipGetLastError();
+    if (e != hipSuccess) {
+      broken = true;
+      return (int)e;
+    }
+    inst_first = first;
+    running = true;
+    gen++;
+    return 0;
+  }
+
+  // The running instance took no more requests (idle exit, or a stop): a
+  // fresh one starts at the first request it did not take.
+  int relaunch_if_exited_locked() {
+    volatile EngCtl* c = ctl;
+    if (running && !c->exited) return 0;
+    const uint64_t first = running ? c->consumed : inst_first;
+    running = false;
+    relaunches++;
+    return launch_locked(first);
+  }
+
+  bool ring_slot_free(uint64_t seq) const {
+    if (seq < kRing) return true;
+    const volatile uint64_t* h = hdone;
+    return h[seq % kRing] == seq - kRing + 1;
+  }
+};
+
+constexpr int kMaxDev = 16;
+Engine g_eng[kMaxDev];
+
+void stop_all_at_exit();
+
+Engine* engine_for_device(int* err) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) {
+    (void)hipGetLastError();
+    *err = NOVA_E_NODEV;
+    return nullptr;
+  }
+  static std::once_flag once;
+  std::call_once(once, [] { atexit(stop_all_at_exit); });
+  *err = 0;
+  return &g_eng[dev];
+}
+
+int engine_stop(Engine& g) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (!g.ready || !g.running) return 0;
+  volatile EngCtl* c = g.ctl;
+  c->hstop = 1;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!c->exited) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      g.broken = true;
+      return NOVA_E_NODEV;
+    }
+    std::this_thread::yield();
+  }
+  const hipError_t e = hipStreamSynchronize(g.stream);
+  g.inst_first = c->consumed;
+  g.running = false;
+  c->hstop = 0;
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+void stop_all_at_exit() {
+  for (Engine& g : g_eng)
+    if (g.ready && g.running) (void)engine_stop(g);
+}
+
+}  // namespace
+
+namespace nova_dev {
+
+// Runs one request on the engine and waits for it.  Returns 0, or nonzero when
+// the engine cannot run it (the caller then makes the plain call).
+int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uint32_t* sizes, uint64_t n,
+                  uint32_t flags, void* out, uint32_t* bad) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  Engine& g = *gp;
+  static const uint64_t timeout_ms = env_u64("NOVA_SST_ENGINE_TIMEOUT_MS", 10000);
+  uint64_t seq = 0;
+  {
+    std::unique_lock<std::mutex> lk(g.mu);
+    if (g.broken) return NOVA_E_NODEV;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if ((err = g.init_locked(dev))) return err;
+    seq = g.next_seq;
+    while (!g.ring_slot_free(seq)) {  // kRing requests in flight: wait for the oldest
+      lk.unlock();
+      std::this_thread::yield();
+      lk.lock();
+      seq = g.next_seq;
+    }
+    g.next_seq = seq + 1;
+    // blocks per chunk: one round per wave when the request is alone (latency),
+    // four rounds when others are in flight (fewer tickets, longer streams)
+    const uint64_t others = g.inflight.fetch_add(1);
+    EngHostReq r{};
+    r.base = (uint64_t)base;
+    r.offs = (uint64_t)offs;
+    r.sizes = (uint64_t)sizes;
+    r.out = (uint64_t)out;
+    r.bad = (uint64_t)bad;
+    r.n = n;
+    r.mode = (uint32_t)mode;
+    r.flags = flags;
+    r.cb = others ? 16u : (uint32_t)(64 / kEngG);
+    volatile EngHostReq* h = g.ring + seq % kRing;
+    h->base = r.base;
+    h->offs = r.offs;
+    h->sizes = r.sizes;
+    h->out = r.out;
+    h->bad = r.bad;
+    h->n = r.n;
+    h->mode = r.mode;
+    h->flags = r.flags;
+    h->cb = r.cb;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    reinterpret_cast<volatile uint64_t*>(&g.ctl->htail)[0] = seq + 1;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    g.requests++;
+    if ((err = g.relaunch_if_exited_locked())) {
+      g.inflight.fetch_sub(1);
+      return err;
+    }
+  }
+  // wait for the completion word; relaunch if the instance exited without
+  // taking this request
+  const volatile uint64_t* hd = g.hdone + seq % kRing;
+  const volatile EngCtl* c = g.ctl;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 0;; spin++) {
+    if (*hd == seq + 1) break;
+    if ((spin & 255) == 255) {
+      if (c->error) {
+        std::lock_guard<std::mutex> lk(g.mu);
+        g.broken = true;
+        g.inflight.fetch_sub(1);
+        return NOVA_E_NODEV;
+      }
+      if (c->exited) {
+        std::lock_guard<std::mutex> lk(g.mu);
+        if (*hd != seq + 1 && (err = g.relaunch_if_exited_locked())) {
+          g.inflight.fetch_sub(1);
+          return err;
+        }
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+        std::lock_guard<std::mutex> lk(g.mu);
+        g.broken = true;  // later requests take the plain path
+        g.inflight.fetch_sub(1);
+        return NOVA_E_NODEV;
+      }
+      if (spin > (1u << 16)) std::this_thread::yield();
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  g.inflight.fetch_sub(1);
+  return 0;
+}
+
+std::atomic<int> g_engine_override{-1};  // nova_sst_engine_set_enabled (-1: NOVA_SST_ENGINE)
+
+bool engine_enabled() {
+  static const bool env_on = env_u64("NOVA_SST_ENGINE", 1) != 0;
+  const int o = g_engine_override.load();
+  return o < 0 ? env_on : o != 0;
+}
+
+void engine_count_fallback() {
+  int err = 0;
+  Engine* g = engine_for_device(&err);
+  if (!g) return;
+  std::lock_guard<std::mutex> lk(g->mu);
+  g->fallbacks++;
+}
+
+}  // namespace nova_dev
+
+extern "C" {
+
+int nova_sst_engine_start(void) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<std::mutex> lk(gp->mu);
+  if (gp->broken) return NOVA_E_NODEV;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if ((err = gp->init_locked(dev))) return err;
+  return gp->relaunch_if_exited_locked();
+}
+
+int nova_sst_engine_stop(void) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  return engine_stop(*gp);
+}
+
+int nova_sst_engine_stats(uint64_t* requests, uint64_t* launches, uint64_t* fallbacks, int* running) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<std::mutex> lk(gp->mu);
+  if (requests) *requests = gp->requests;
+  if (launches) *launches = gp->gen;
+  if (fallbacks) *fallbacks = gp->fallbacks;
+  if (running) *running = gp->running && gp->ctl && !((volatile EngCtl*)gp->ctl)->exited ? 1 : 0;
+  return 0;
+}
+
+int nova_sst_engine_set_enabled(int on) {
+  if (on < -1 || on > 1) return NOVA_E_INVAL;
+  g_engine_override.store(on);
+  return 0;
+}
+
+int nova_sst_engine_set_idle_us(uint32_t us) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<std::mutex> lk(gp->mu);
+  gp->idle_us = us ? us : 1000;  // the next instance
+  return 0;
+}
+
+}  // extern "C"

@@ -79,6 +79,9 @@ struct CrcParams {
   // pre-pass's eligibility array) rewrite the whole 64-B pieces holding its
   // trailer; null or nonzero: byte stores
   const uint32_t* tr_flag;
+  // trailer writer, two-pass form: 1 at blocks whose whole-piece window must not
+  // be used (the first and last block of each table of a coalesced batch); may be null
+  const uint8_t* tr_last;
   uint32_t out_pos;  // host: launch the kVarOutPos instantiation (log records in p.perm's order)
   uint32_t wvar;  // diagnostics (timing, kVarDiag): 1 = whole-piece stores non-temporal,
                   // 2 = no result writes, 3 = no per-block epilogue and no writes
@@ -108,6 +111,11 @@ constexpr int kVarOutPos = 1024;
 // once per round for the round's groups (rounds 1-2 form; the diagnostics
 // store forms need it) instead of once per chunk for all 64 blocks lane-parallel.
 constexpr int kVarRoundEpi = 2048;
+// Units chunk body inside the persistent SSTable engine (crc32c_engine.hip):
+// every load of caller memory is non-temporal (no stale L1 lines of a buffer
+// rewritten between requests) and verify loads each stored CRC with its
+// descriptor.
+constexpr int kVarEngine = 4096;
 
 constexpr size_t kLdsMax = 160 * 1024;  // per CU on MI355X
 constexpr int kMaxDevices = 64;
@@ -213,6 +221,16 @@ struct StreamScratch {
 // pieces.  trailer_layout: the pieces' eligibility pre-pass
 // (zeroes *flag first); both return 0 or an error.
 int trailer_two_pass(CrcParams& p, int G, uint32_t chunk, DevTables* t, hipStream_t stream);
+
+// The persistent per-SSTable engine (crc32c_engine.hip):
+// engine_submit runs one request (kStore: out = uint32_t* CRCs; kTrailer: out
+// unused; kVerify: out = uint8_t* ok flags, bad = mismatch counter) and waits
+// for it; nonzero = the engine could not run it (the caller makes the plain
+// call).  NOVA_SST_ENGINE=0 turns it off (engine_enabled).
+int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uint32_t* sizes, uint64_t n,
+                  uint32_t flags, void* out, uint32_t* bad);
+bool engine_enabled();
+void engine_count_fallback();
 int trailer_layout(const CrcParams& p, DevTables* t, hipStream_t stream, uint32_t* elig, uint32_t* flag);
 
 // ---- diagnostics hooks (crc32c_diag.hip fills g_diag; null in the product) --

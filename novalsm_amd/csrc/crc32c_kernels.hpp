@@ -108,6 +108,16 @@ __device__ __forceinline__ uint4 gload16(uint64_t addr) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// A scalar-typed load of caller memory; NT: non-temporal (bypasses L1), as the
+// persistent engine needs for buffers a caller may rewrite between requests.
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_nt(const T* a) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load((const __attribute__((address_space(1))) T*)a);
+  else
+    return *a;
+}
+
 // Read a dword at an absolute LDS byte address.  The kernel holds no static
 // __shared__ objects, so the dynamic LDS region starts at address 0 and the
 // v_perm-built table address is used as is (no base add per lookup).
@@ -305,6 +315,24 @@ __device__ __forceinline__ void store_u32_unaligned(uint8_t* d, uint32_t v) {
 __device__ __forceinline__ void store_trailer(uint8_t* d, uint32_t type, uint32_t m, bool quirk) {
   *(__attribute__((address_space(1))) uint8_t*)d = (uint8_t)type;
   store_u32_unaligned(d + 1, quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m);
+}
+
+// Write-through stores (agent scope: the line goes to memory, not just this
+// XCD's L2) for the persistent engine's results: once its wave has drained
+// them (s_waitcnt vmcnt(0)) they are where a copy or a kernel of any stream
+// reads them, with no L2 write-back (a per-chunk release fence, buffer_wbl2,
+// serialised the engine at ~15 us per request).
+template <typename T>
+__device__ __forceinline__ void st_through(T* a, T v) {
+  __hip_atomic_store((__attribute__((address_space(1))) T*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_trailer_through(uint8_t* d, uint32_t type, uint32_t m, bool quirk) {
+  const uint32_t w = quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m;
+  st_through(d, (uint8_t)type);
+  st_through(d + 1, (uint8_t)w);
+  st_through(d + 2, (uint8_t)(w >> 8));
+  st_through(d + 3, (uint8_t)(w >> 16));
+  st_through(d + 4, (uint8_t)(w >> 24));
 }
 
 // Patch the NB little-endian bytes of tv (a trailer: type | LE32 << 8, NB 5;
@@ -618,24 +646,22 @@ __device__ __forceinline__ void lds_fill_tables(uint8_t* lds, const void* tab_ma
   }
 }
 
-// Launch bound 12 waves (the launch size, kUnitsWaves): 168 VGPRs.  At the
-// 16-wave bound the compiler had 128 and spilled 5-7 VGPRs to scratch in every
-// instantiation (tools/kernel_meta.py).
-constexpr int kUnitsMaxWaves = 12;
+// One claimed chunk of the units kernel (and of the persistent SSTable engine,
+// crc32c_engine.hip): lane i < p.chunk owns block chunk * p.chunk + i; the
+// chunk's units run in rounds of kGroups (one per lane group), largest first;
+// lane i finishes its block.  wpre: the wave's kWaveScratch bytes of LDS.
+// kVarEngine (the engine): every load of caller memory (descriptors, block
+// bytes, stored CRCs) bypasses L1 -- the engine stays resident between
+// requests, so no kernel start invalidates the CU's L1 lines of a buffer the
+// caller has since rewritten.
 template <int G, int MODE, int VAR = 0>
-__global__ void __launch_bounds__(kUnitsMaxWaves * 64) crc32c_units_kernel(CrcParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
-  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, nullptr, 0);
-  __syncthreads();
-
+__device__ __forceinline__ void units_chunk(const uint8_t* lds, const CrcParams& p, uint64_t chunk,
+                                            uint32_t* wpre) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
   const int q = lane & (G - 1);   // lane within its group
   const int grp = lane / G;       // group within the wave
   constexpr int kGroups = 64 / G;
-  uint32_t* wpre = reinterpret_cast<uint32_t*>(lds + kMainBytes + kLevels * kTreeBytes +
-                                               wave * kWaveScratch);
+  constexpr bool kEng = (VAR & kVarEngine) != 0;
   uint32_t* wacc = wpre + 64;
   uint32_t* wsort = wpre + 32;  // chunk lanes in descending unit-size order
   const uint64_t zl = (uint64_t)p.zline;  // 16 zero bytes
@@ -643,41 +669,17 @@ __global__ void __launch_bounds__(kUnitsMaxWaves * 64) crc32c_units_kernel(CrcPa
   const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
   const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
   const uint32_t extra = (MODE == kVerify) ? 1u : 0u;  // verify covers block + type byte
-
-  // Chunks of p.chunk (<= 16) blocks.  Workgroup w owns the interleaved chunks
-  // w, w+nwg, ... and its waves claim them from a per-workgroup counter (one
-  // relaxed device-scope atomic per chunk); a wave whose workgroup ran out
-  // steals from up to p.steal_limit other workgroups.  Wave k's first chunk is
-  // implicit.  (Static chunk assignment left the tail unbalanced, as measured
-  // for the streaming kernel in DESIGN.md 3.3.)
-  const uint32_t nwg = gridDim.x;
-  const uint32_t nwaves = blockDim.x >> 6;
-  uint32_t victim = blockIdx.x, tried = 0;
-  uint64_t chunk = (uint64_t)wave * nwg + blockIdx.x;
-  auto next_chunk = [&]() -> uint64_t {
-    for (;;) {
-      uint32_t idx = 0;
-      if (lane == 0)
-        idx = __hip_atomic_fetch_add(p.sched + victim * 16, 1u, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-      idx = __builtin_amdgcn_readfirstlane(idx);
-      const uint64_t c = ((uint64_t)idx + nwaves) * nwg + victim;
-      if (c < p.n_chunks) return c;
-      if (++tried >= p.steal_limit + 1) return ~0ull;
-      victim = (victim + 1) % nwg;
-    }
-  };
-  if (chunk >= p.n_chunks) chunk = next_chunk();
-
-  for (; chunk != ~0ull; chunk = next_chunk()) {
+  {
     // -- prologue: lane i < chunk owns block b = chunk*chunk_size + i
     const uint64_t b = chunk * p.chunk + lane;
     const bool valid = lane < (int)p.chunk && b < p.n_blocks;
     uint64_t a = 0;
     uint32_t n = 0, init = 0;
     uint32_t lstat = NOVA_LOG_OK;  // log modes: record status (log_status)
+    uint32_t stored = 0;  // engine, verify: the block's stored CRC, loaded with its descriptor
+    bool eng_bad = false;  // engine, verify: this lane's block failed
     if (valid) {
-      a = (uint64_t)p.base + (p.offsets ? p.offsets[b] : b * p.stride);
+      a = (uint64_t)p.base + (p.offsets ? ld_nt<kEng>(p.offsets + b) : b * p.stride);
       if (MODE == kLogWrite || MODE == kLogVerify) {
         const uint64_t o = a - (uint64_t)p.base;
         if (log_header_fits(o, p.buf_len)) {
@@ -690,9 +692,14 @@ __global__ void __launch_bounds__(kUnitsMaxWaves * 64) crc32c_units_kernel(CrcPa
         }
         a += 6;  // CRC input starts at the type byte
       } else {
-        n = (p.lengths ? p.lengths[b] : p.len) + extra;
+        n = (p.lengths ? ld_nt<kEng>(p.lengths + b) : p.len) + extra;
       }
-      init = p.init ? p.init[b] : 0u;
+      init = p.init ? ld_nt<kEng>(p.init + b) : 0u;
+      if (kEng && MODE == kVerify) {
+        const uint8_t* d = (const uint8_t*)a + n;
+        stored = (uint32_t)ld_nt<true>(d) | ((uint32_t)ld_nt<true>(d + 1) << 8) |
+                 ((uint32_t)ld_nt<true>(d + 2) << 16) | ((uint32_t)ld_nt<true>(d + 3) << 24);
+      }
     }
     const uint32_t ninit = raw ? 0u : ~init;
     // Units: blocks >= seg bytes are cut into floor(n/seg) segments (seg..2seg-1
@@ -706,7 +713,7 @@ __global__ void __launch_bounds__(kUnitsMaxWaves * 64) crc32c_units_kernel(CrcPa
         nq = (p.seg == 0 || n < p.seg) ? 1u : n / p.seg;
       } else {  // tiny block: bytewise on this lane
         uint32_t l = ninit;
-        for (uint32_t i = 0; i < n; i++) l = byte_step(l, ((const uint8_t*)a)[i]);
+        for (uint32_t i = 0; i < n; i++) l = byte_step(l, ld_nt<kEng>((const uint8_t*)a + i));
         small_crc = raw ? l : ~l;
       }
     }
@@ -844,26 +851,94 @@ __global__ void __launch_bounds__(kUnitsMaxWaves * 64) crc32c_units_kernel(CrcPa
           if (!ok && p.n_bad) atomicAdd(p.n_bad, 1u);
         }
       } else if (MODE == kVerify) {
-        const uint8_t* d = (const uint8_t*)a;
-        const uint32_t stored = (uint32_t)d[n] | ((uint32_t)d[n + 1] << 8) |
-                                ((uint32_t)d[n + 2] << 16) | ((uint32_t)d[n + 3] << 24);
+        if (!kEng) {
+          const uint8_t* d = (const uint8_t*)a;
+          stored = (uint32_t)d[n] | ((uint32_t)d[n + 1] << 8) | ((uint32_t)d[n + 2] << 16) |
+                   ((uint32_t)d[n + 3] << 24);
+        }
         const bool ok = unmask_crc(stored) == crc;  // table/table.cc:435-437
-        p.ok_out[b] = ok ? 1 : 0;
-        if (!ok && p.n_bad) atomicAdd(p.n_bad, 1u);
+        if constexpr (kEng) {
+          st_through(p.ok_out + b, (uint8_t)(ok ? 1 : 0));
+          eng_bad = !ok;
+        } else {
+          p.ok_out[b] = ok ? 1 : 0;
+          if (!ok && p.n_bad) atomicAdd(p.n_bad, 1u);
+        }
       } else {
         if (p.flags & NOVA_CRC32C_APPEND_TYPE) {  // table/table_builder.cc:203
           crc = ~byte_step(~crc, (p.flags >> 8) & 0xffu);
         }
         if (MODE == kTrailer) {
           const uint32_t m = mask_crc(crc);
-          store_trailer((uint8_t*)a + n, (p.flags >> 8) & 0xffu, m,
-                        (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
+          if constexpr (kEng)
+            store_trailer_through((uint8_t*)a + n, (p.flags >> 8) & 0xffu, m,
+                                  (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
+          else
+            store_trailer((uint8_t*)a + n, (p.flags >> 8) & 0xffu, m,
+                          (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
         } else {
           if (p.flags & NOVA_CRC32C_MASK_OUTPUT) crc = mask_crc(crc);
-          p.out[b] = crc;
+          if constexpr (kEng)
+            st_through(p.out + b, crc);
+          else
+            p.out[b] = crc;
         }
       }
     }
+    // engine, verify: one add per chunk (system scope: performed in memory,
+    // where the caller's next copy reads the counter)
+    if constexpr (kEng && MODE == kVerify) {
+      const uint32_t nb = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(eng_bad));
+      if (lane == 0 && nb && p.n_bad)
+        __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t*)p.n_bad, nb, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// Launch bound 12 waves (the launch size, kUnitsWaves): 168 VGPRs.  At the
+// 16-wave bound the compiler had 128 and spilled 5-7 VGPRs to scratch in every
+// instantiation (tools/kernel_meta.py).
+constexpr int kUnitsMaxWaves = 12;
+template <int G, int MODE, int VAR = 0>
+__global__ void __launch_bounds__(kUnitsMaxWaves * 64) crc32c_units_kernel(CrcParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
+  lds_fill_tables(lds, p.tab_main, p.tab_tree, kLevels * kTreeBytes / 16, nullptr, 0);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  uint32_t* wpre = reinterpret_cast<uint32_t*>(lds + kMainBytes + kLevels * kTreeBytes +
+                                               wave * kWaveScratch);
+
+  // Chunks of p.chunk (<= 16) blocks.  Workgroup w owns the interleaved chunks
+  // w, w+nwg, ... and its waves claim them from a per-workgroup counter (one
+  // relaxed device-scope atomic per chunk); a wave whose workgroup ran out
+  // steals from up to p.steal_limit other workgroups.  Wave k's first chunk is
+  // implicit.  (Static chunk assignment left the tail unbalanced, as measured
+  // for the streaming kernel in DESIGN.md 3.3.)
+  const uint32_t nwg = gridDim.x;
+  const uint32_t nwaves = blockDim.x >> 6;
+  uint32_t victim = blockIdx.x, tried = 0;
+  uint64_t chunk = (uint64_t)wave * nwg + blockIdx.x;
+  auto next_chunk = [&]() -> uint64_t {
+    for (;;) {
+      uint32_t idx = 0;
+      if (lane == 0)
+        idx = __hip_atomic_fetch_add(p.sched + victim * 16, 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+      idx = __builtin_amdgcn_readfirstlane(idx);
+      const uint64_t c = ((uint64_t)idx + nwaves) * nwg + victim;
+      if (c < p.n_chunks) return c;
+      if (++tried >= p.steal_limit + 1) return ~0ull;
+      victim = (victim + 1) % nwg;
+    }
+  };
+  if (chunk >= p.n_chunks) chunk = next_chunk();
+
+  for (; chunk != ~0ull; chunk = next_chunk()) {
+    units_chunk<G, MODE, VAR>(lds, p, chunk, wpre);
   }
   sched_release(p.sched);
 }

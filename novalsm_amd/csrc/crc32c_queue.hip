@@ -26,6 +26,11 @@
 // set each), so the next batch forms and launches while one runs.
 // Results are identical to the per-table calls: each block's checksum is
 // computed by the same kernels from the same bytes.
+//
+// Round 4: by default the queue entry points run on the persistent engine
+// (crc32c_engine.hip), which pays no launch per table; the
+// coalescing batches below serve NOVA_SST_ENGINE=0, and the plain call any
+// request the engine cannot run.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -68,13 +73,22 @@ __device__ __forceinline__ uint32_t qtable_of(const QBatch& b, uint64_t i) {
   return r;
 }
 
-__global__ void __launch_bounds__(256) qgather_kernel(QBatch b, uint64_t* offs, uint32_t* sizes) {
+// last[i] = 1 at every table's first and last block: the batched trailer
+// writer must not rewrite those blocks' whole 64-B trailer pieces, which may
+// reach past the end of the table's image (last block) or before its start (a
+// first block shorter than the piece) into memory of another caller (ADVICE
+// r03; the plain call never does: its image's edge blocks are never eligible).
+__global__ void __launch_bounds__(256) qgather_kernel(QBatch b, uint64_t* offs, uint32_t* sizes,
+                                                      uint8_t* last) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= b.n_blocks) return;
-  const QTable& T = b.t[qtable_of(b, i)];
+  const uint32_t r = qtable_of(b, i);
+  const QTable& T = b.t[r];
   const uint64_t j = i - T.start;
   offs[i] = T.base + T.offs[j];
   sizes[i] = T.sizes[j];
+  const bool end = r + 1 < b.n_tables ? i + 1 == b.t[r + 1].start : i + 1 == b.n_blocks;
+  last[i] = (end || j == 0) ? 1 : 0;
 }
 
 __global__ void __launch_bounds__(256) qscatter_kernel(QBatch b, const uint8_t* ok) {
@@ -107,6 +121,7 @@ struct Slot {
   uint64_t* offs = nullptr;
   uint32_t* sizes = nullptr;
   uint8_t* ok = nullptr;
+  uint8_t* last = nullptr;  // 1 at each table's first and last block (trailer writer)
   bool busy = false;
 };
 
@@ -116,16 +131,29 @@ struct Queue {
   Slot slot[kSlots];
   uint64_t batches = 0, requests = 0, max_tables = 0;
 
+  // A slot counts as set up only once every one of its allocations succeeded
+  // (ADVICE r03): a partial failure frees what it got and leaves the slot
+  // empty, so a later batch retries instead of gathering through null arrays.
   int init_slot(Slot& s) {
-    if (s.stream) return 0;
-    hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&s.offs, kMaxBlocks * 8);
-    if (e == hipSuccess) e = hipMalloc(&s.sizes, kMaxBlocks * 4);
-    if (e == hipSuccess) e = hipMalloc(&s.ok, kMaxBlocks);
+    if (s.stream && s.offs && s.sizes && s.ok && s.last) return 0;
+    Slot n{};
+    hipError_t e = hipStreamCreateWithFlags(&n.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&n.offs, kMaxBlocks * 8);
+    if (e == hipSuccess) e = hipMalloc(&n.sizes, kMaxBlocks * 4);
+    if (e == hipSuccess) e = hipMalloc(&n.ok, kMaxBlocks);
+    if (e == hipSuccess) e = hipMalloc(&n.last, kMaxBlocks);
     if (e != hipSuccess) {
+      (void)hipGetLastError();
+      if (n.last) (void)hipFree(n.last);
+      if (n.ok) (void)hipFree(n.ok);
+      if (n.sizes) (void)hipFree(n.sizes);
+      if (n.offs) (void)hipFree(n.offs);
+      if (n.stream) (void)hipStreamDestroy(n.stream);
       (void)hipGetLastError();
       return NOVA_E_NOMEM;
     }
+    n.busy = s.busy;
+    s = n;
     return 0;
   }
 
@@ -159,7 +187,8 @@ struct Queue {
     b.n_tables = (uint32_t)nr;
     b.n_blocks = total;
     const uint64_t wgs = (total + 255) / 256;
-    hipLaunchKernelGGL(qgather_kernel, dim3((uint32_t)wgs), dim3(256), 0, s.stream, b, s.offs, s.sizes);
+    hipLaunchKernelGGL(qgather_kernel, dim3((uint32_t)wgs), dim3(256), 0, s.stream, b, s.offs, s.sizes,
+                       s.last);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     CrcParams p{};
@@ -170,6 +199,7 @@ struct Queue {
     p.flags = rs[0]->flags;
     const int mode = rs[0]->mode;
     if (mode == kVerify) p.ok_out = s.ok;
+    if (mode == kTrailer) p.tr_last = s.last;
     rc = dispatch(mode, p, s.stream);
     if (rc) return rc;
     if (mode == kVerify) {
@@ -203,13 +233,13 @@ struct Queue {
 
   int submit(Req& r) {
     std::unique_lock<std::mutex> lk(mu);
-    const int ns = slots();
     q.push_back(&r);
     int si = -1;
     for (;;) {
       if (r.done) return r.rc;
-      // (a popped request waits for done; front() of an empty deque is undefined)
-      if (!q.empty() && q.front() == &r && (si = free_slot(ns)) >= 0) break;
+      // (a popped request waits for done; front() of an empty deque is undefined;
+      // the slot count is read on every wake: nova_sst_queue_set_slots may raise it)
+      if (!q.empty() && q.front() == &r && (si = free_slot(slots())) >= 0) break;
       r.cv.wait(lk);
     }
     // leader: take the compatible requests at the queue's front (r first)
@@ -260,7 +290,20 @@ int enqueue(Req& r, hipStream_t stream) {
   if (e == hipErrorNotReady) e = hipStreamSynchronize(stream);
   if (e != hipSuccess) return (int)e;
   r.stream = stream;
-  if (r.n > kMaxBlocks) {  // larger than one batch: the plain call (one launch is efficient)
+  bool plain = r.n > kMaxBlocks;  // larger than one batch: the plain call (one launch is efficient)
+  if (!plain && engine_enabled()) {
+    // the persistent engine (crc32c_engine.hip); if it cannot run the
+    // request, the plain call computes it (after zeroing a verify counter
+    // the engine may have added to)
+    if (engine_submit(r.mode, r.buf, r.offs, r.sizes, r.n, r.flags,
+                      r.mode == kVerify ? (void*)r.ok : nullptr, r.bad) == 0)
+      return 0;
+    engine_count_fallback();
+    if (r.mode == kVerify && r.bad && (e = hipMemsetAsync(r.bad, 0, sizeof(uint32_t), stream)) != hipSuccess)
+      return (int)e;
+    plain = true;
+  }
+  if (plain) {
     CrcParams p{};
     p.base = r.buf;
     p.offsets = r.offs;

@@ -19,6 +19,7 @@
 // reused): a stream per call would also leave one claim-counter slot per
 // stream address behind (crc32c_device.hip, sched_slot).
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -172,8 +173,14 @@ struct Streams {
 // end cannot unregister memory another call's DMA still reads; a call whose
 // range partly overlaps a live registration waits until that one is released
 // (hipHostRegister rejects overlapping ranges), then registers its own.
+// hipHostRegister pins whole pages, so every range is rounded out to pages
+// before it is compared: two calls on disjoint byte ranges that
+// share a page share (or wait for) one registration.  Otherwise the second
+// call found its pages pinned -- by the first call -- took them for
+// caller-pinned memory without a reference, and the first call's end could
+// unregister a page the second call's DMA still read.
 struct RegEntry {
-  uintptr_t lo, hi;
+  uintptr_t lo, hi;  // page-aligned
   int refs;
 };
 struct RegTable {
@@ -185,12 +192,21 @@ RegTable& reg_table() {
   static RegTable* t = new RegTable;  // never destroyed (exit order)
   return *t;
 }
+uintptr_t page_bytes() {
+  static const uintptr_t p = [] {
+    const long v = sysconf(_SC_PAGESIZE);
+    return v > 0 ? (uintptr_t)v : (uintptr_t)4096;
+  }();
+  return p;
+}
 
 struct HostReg {
   uintptr_t key = 0;  // lo of the entry this call holds a reference to (0: none)
   int reg(const void* base, size_t len) {
     if (!len) return 0;
-    const uintptr_t lo = (uintptr_t)base, hi = lo + len;
+    const uintptr_t pg = page_bytes();
+    const uintptr_t lo = (uintptr_t)base & ~(pg - 1);
+    const uintptr_t hi = ((uintptr_t)base + len + pg - 1) & ~(pg - 1);
     RegTable& t = reg_table();
     std::unique_lock<std::mutex> lk(t.mu);
     for (;;) {
@@ -206,8 +222,10 @@ struct HostReg {
       if (!overlap) break;
       t.cv.wait(lk);  // a partly overlapping registration is still in use
     }
-    if (is_pinned(base) && is_pinned((const uint8_t*)base + len - 1)) return 0;  // caller-pinned
-    if (hipHostRegister(const_cast<void*>(base), len, hipHostRegisterDefault) != hipSuccess) {
+    // No live registration of this library touches these pages, so pinned
+    // pages here were pinned by the caller.
+    if (is_pinned(base) && is_pinned((const uint8_t*)base + len - 1)) return 0;
+    if (hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault) != hipSuccess) {
       (void)hipGetLastError();
       return NOVA_E_NOMEM;
     }

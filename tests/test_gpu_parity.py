@@ -892,15 +892,25 @@ def test_concurrent_split_path(torch_gpu, oracle):
             assert np.array_equal(r, want), i
 
 
-def test_sst_queue_concurrent(torch_gpu, oracle):
-    """Coalescing queue (nova_sst_queue_*): 12 host threads,
+@pytest.fixture
+def sst_backend(request):
+    """Route the nova_sst_queue_* calls to the persistent engine (1) or the
+    round-3 coalescing queue (0) for one test."""
+    C.engine_set_enabled(request.param)
+    yield request.param
+    C.engine_set_enabled(-1)
+
+
+@pytest.mark.parametrize("sst_backend", [1, 0], indirect=True, ids=["engine", "queue"])
+def test_sst_queue_concurrent(torch_gpu, oracle, sst_backend):
+    """nova_sst_queue_* (DESIGN.md 3.5d, 3.5g): 12 host threads,
     each on its own stream with its own SSTable image (ragged layouts, 0 to 3000
     blocks, gaps between blocks, three trailer types, one with the TableBuilder
     quirk), write trailers then verify with corrupted blocks, many calls each.
     The image is filled asynchronously on the caller's stream right before the
-    first call (the batch must wait for it).  Every trailer equals the oracle's
-    and every verify flags exactly the corrupted blocks; the calls shared
-    launches (batches < requests)."""
+    first call (the request must wait for it).  Every trailer equals the oracle's
+    and every verify flags exactly the corrupted blocks.  Engine: every call ran
+    on it (no fallback).  Queue: the calls shared launches (batches < requests)."""
     torch = torch_gpu
     import threading
     T, R = 12, 12
@@ -919,6 +929,7 @@ def test_sst_queue_concurrent(torch_gpu, oracle):
         tabs.append(dict(n=n, sz=sz, offs=offs, total=total, bad=np.sort(bad), type=t % 3,
                          quirk=(t == 5)))
     before = C.queue_stats()
+    ebefore = C.engine_stats()
     results, errors = [None] * T, []
     # One batch in flight: while it runs, the other threads' calls queue up
     # behind it and the next leader takes them together.  (With 4 slots a fast
@@ -984,15 +995,21 @@ def test_sst_queue_concurrent(torch_gpu, oracle):
         for ok, nb in zip(oks, bads):
             assert np.array_equal(ok, expect), (t, np.nonzero(ok != expect)[0][:8])
             assert nb == int((expect == 0).sum()), (t, nb)
+    if sst_backend:
+        eafter = C.engine_stats()
+        assert eafter["requests"] - ebefore["requests"] == calls, (ebefore, eafter, calls)
+        assert eafter["fallbacks"] == ebefore["fallbacks"], (ebefore, eafter)
+        return
     after = C.queue_stats()
     served = after["requests"] - before["requests"]
     assert served == calls, (served, calls)
     assert after["batches"] - before["batches"] < served, (before, after)
 
 
+@pytest.mark.parametrize("sst_backend", [1, 0], indirect=True, ids=["engine", "queue"])
 @pytest.mark.parametrize("threads", [2, 4, 16])
-def test_sst_queue_stress(torch_gpu, oracle, threads):
-    """The coalescing queue under back-to-back calls (tools/concurrent_sst.py's
+def test_sst_queue_stress(torch_gpu, oracle, threads, sst_backend):
+    """nova_sst_queue_* under back-to-back calls (tools/concurrent_sst.py's
     shape): `threads` callers, each verifying its own 1024-block SSTable image
     (4096+U[0,255] B blocks) 60 times with no pause, every third call on a
     copy with one corrupted block; every call's flags and count are checked."""
@@ -1043,6 +1060,227 @@ def test_sst_queue_stress(torch_gpu, oracle, threads):
     for x in th:
         x.join()
     assert not errors, errors[:4]
+
+
+def _sst_tables(torch, oracle, ns, seed):
+    """SSTable images (4096+U[0,255] B blocks, 5-B trailers) with their oracle
+    trailer CRCs (type 0, TableBuilder ordering without the quirk)."""
+    from bench import sst4k_layout
+    out = []
+    for k, n in enumerate(ns):
+        offs_np, lens_np, total = sst4k_layout(n, seed + k)
+        img = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        C.fill_splitmix64(img, seed * 131 + k)
+        out.append(dict(n=n, offs_np=offs_np, lens_np=lens_np, img=img,
+                        offs=torch.from_numpy(offs_np.view(np.int64)).cuda(),
+                        lens=torch.from_numpy(lens_np.view(np.int32)).cuda()))
+    torch.cuda.synchronize()
+    return out
+
+
+def _trailer_words(oracle, host, offs_np, lens_np):
+    return oracle.batch(host, offs_np, lens_np, None, flags=C.APPEND_TYPE | C.MASK_OUTPUT | C.TYPE(0))
+
+
+def _check_trailers(host, offs_np, lens_np, want):
+    ends = offs_np.astype(np.int64) + lens_np.astype(np.int64)
+    got = np.stack([host[ends + i] for i in range(5)], axis=1)
+    assert np.all(got[:, 0] == 0)
+    words = got[:, 1].astype(np.uint32) | (got[:, 2].astype(np.uint32) << 8) | \
+        (got[:, 3].astype(np.uint32) << 16) | (got[:, 4].astype(np.uint32) << 24)
+    bad = np.nonzero(words != want)[0]
+    assert bad.size == 0, bad[:8]
+
+
+def test_engine_start_stop_restart(torch_gpu, oracle):
+    """The persistent engine through its whole life: started
+    explicitly, trailers then verify (with one corrupted block) on tables of
+    1, 5, 4096 and 20000 blocks, stopped, restarted by the next call, stopped
+    again; every result bit-exact, no request fell back to the plain call."""
+    torch = torch_gpu
+    C.engine_set_enabled(1)
+    try:
+        C.engine_stop()
+        s0 = C.engine_stats()
+        C.engine_start()
+        assert C.engine_stats()["running"]
+        tabs = _sst_tables(torch, oracle, [1, 5, 4096, 20000], 41)
+        for cycle in range(2):
+            for tb in tabs:
+                C.queue_write_trailers(tb["img"], tb["offs"], tb["lens"])
+                host = tb["img"].cpu().numpy()
+                want = _trailer_words(oracle, host, tb["offs_np"], tb["lens_np"])
+                _check_trailers(host, tb["offs_np"], tb["lens_np"], want)
+                j = (7 * tb["n"]) // 11
+                tb["img"][int(tb["offs_np"][j]) + 3] ^= 0x10
+                ok = torch.full((tb["n"],), 9, dtype=torch.uint8, device="cuda")
+                nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+                C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, nb)
+                exp = np.ones(tb["n"], np.uint8)
+                exp[j] = 0
+                assert np.array_equal(ok.cpu().numpy(), exp), (cycle, tb["n"])
+                assert int(nb.item()) == 1
+                tb["img"][int(tb["offs_np"][j]) + 3] ^= 0x10
+            C.engine_stop()
+            assert not C.engine_stats()["running"]
+        s1 = C.engine_stats()
+        assert s1["launches"] - s0["launches"] >= 2, (s0, s1)
+        assert s1["fallbacks"] == s0["fallbacks"], (s0, s1)
+        assert s1["requests"] - s0["requests"] == 16, (s0, s1)
+    finally:
+        C.engine_set_enabled(-1)
+
+
+def test_engine_idle_exit_and_buffer_rewrite(torch_gpu, oracle):
+    """Between requests the engine stays resident (or exits when idle and is
+    relaunched by the next call: both happen here, with a 300 us idle time).
+    A caller that rewrites its image and descriptors in place between calls --
+    new bytes, new block layout, on its own stream -- must get results for the
+    new contents: the engine's loads of caller memory bypass L1
+    (kVarEngine), so no line cached from an earlier request is used.  Two
+    threads keep the device unevenly loaded while the checked caller runs."""
+    torch = torch_gpu
+    import threading
+    import time
+    from bench import sst4k_layout
+    C.engine_set_enabled(1)
+    C.engine_stop()
+    C.engine_set_idle_us(300)
+    stop = threading.Event()
+    errors = []
+    noise = _sst_tables(torch, oracle, [3000, 700], 77)
+
+    def load(tb):
+        try:
+            s = torch.cuda.Stream()
+            ok = torch.empty(tb["n"], dtype=torch.uint8, device="cuda")
+            with torch.cuda.stream(s):
+                C.queue_write_trailers(tb["img"], tb["offs"], tb["lens"], stream=s)
+                while not stop.is_set():
+                    C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, stream=s)
+                    if not bool((ok == 1).all()):
+                        errors.append("noise verify")
+                        return
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=load, args=(tb,)) for tb in noise]
+    try:
+        for x in th:
+            x.start()
+        n = 2048
+        cap = n * (4096 + 255 + 5) + 64
+        img = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        offs = torch.empty(n, dtype=torch.int64, device="cuda")
+        lens = torch.empty(n, dtype=torch.int32, device="cuda")
+        ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+        s = torch.cuda.Stream()
+        for it in range(12):
+            offs_np, lens_np, total = sst4k_layout(n, 300 + it)
+            with torch.cuda.stream(s):
+                C.fill_splitmix64(img, 1000 + it, stream=s)
+                offs.copy_(torch.from_numpy(offs_np.view(np.int64)), non_blocking=False)
+                lens.copy_(torch.from_numpy(lens_np.view(np.int32)), non_blocking=False)
+                C.queue_write_trailers(img, offs, lens, stream=s)
+                host = img.cpu().numpy()
+            want = _trailer_words(oracle, host, offs_np, lens_np)
+            _check_trailers(host, offs_np, lens_np, want)
+            with torch.cuda.stream(s):
+                C.queue_verify_blocks(img, offs, lens, ok, stream=s)
+                got = ok.cpu().numpy()
+            assert np.all(got == 1), (it, np.nonzero(got != 1)[0][:8])
+            if it % 4 == 3:
+                stop.set()  # let the engine go idle and exit
+                for x in th:
+                    x.join()
+                time.sleep(0.01)
+                assert not C.engine_stats()["running"]
+                stop.clear()
+                th = [threading.Thread(target=load, args=(tb,)) for tb in noise]
+                for x in th:
+                    x.start()
+    finally:
+        stop.set()
+        for x in th:
+            x.join()
+        C.engine_set_idle_us(0)
+        C.engine_stop()
+        C.engine_set_enabled(-1)
+    assert not errors, errors[:4]
+    assert C.engine_stats()["fallbacks"] == 0
+
+
+def test_queue_batched_trailers_adjacent_tables(torch_gpu, oracle):
+    """the coalescing queue's batched trailer writer (more than
+    12288 blocks: the rounds kernel and the whole-piece second pass) on four
+    tables that are adjacent, unpadded slices of one buffer.  Every trailer
+    equals the oracle's, and no byte outside the tables' trailers changes --
+    in particular not the next table's first bytes, which the last block's
+    64-B trailer piece reaches when it is rewritten whole."""
+    torch = torch_gpu
+    import threading
+    from bench import sst4k_layout
+    ns = [5000, 4500, 5100, 4900]  # any three: more than 12288 blocks
+    lays = [sst4k_layout(n, 60 + k) for k, n in enumerate(ns)]
+    # table k starts where table k-1's last trailer ends, plus 0..40 bytes
+    starts, pos = [], 0
+    for k, (o, ln, total) in enumerate(lays):
+        starts.append(pos)
+        pos += total + (7 * k) % 41
+    buf = torch.empty(pos + 64, dtype=torch.uint8, device="cuda")
+    C.fill_splitmix64(buf, 4242)
+    torch.cuda.synchronize()
+    before = buf.cpu().numpy().copy()
+    C.engine_set_enabled(0)
+    C.queue_set_slots(1)
+    views = []
+    for k, (o, ln, total) in enumerate(lays):
+        views.append((buf[starts[k]:starts[k] + total],
+                      torch.from_numpy(o.view(np.int64)).cuda(), torch.from_numpy(ln.view(np.int32)).cuda()))
+    errors = []
+
+    def work(k, gate):
+        try:
+            v, o, ln = views[k]
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                gate.wait()
+                C.queue_write_trailers(v, o, ln, stream=s)
+            s.synchronize()
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    try:
+        for attempt in range(6):  # until the four calls shared a batch (timing)
+            buf.copy_(torch.from_numpy(before))
+            torch.cuda.synchronize()
+            qb = C.queue_stats()
+            gate = threading.Barrier(len(ns))
+            th = [threading.Thread(target=work, args=(k, gate)) for k in range(len(ns))]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            qa = C.queue_stats()
+            assert qa["requests"] - qb["requests"] == len(ns)
+            if qa["batches"] - qb["batches"] < len(ns):
+                break
+    finally:
+        C.queue_set_slots(0)
+        C.engine_set_enabled(-1)
+    assert not errors, errors
+    assert qa["batches"] - qb["batches"] < len(ns), "the calls never shared a batch"
+    after = buf.cpu().numpy()
+    expect = before.copy()
+    for k, (o, ln, total) in enumerate(lays):
+        base = starts[k]
+        want = _trailer_words(oracle, before[base:base + total], o, ln)
+        ends = base + o.astype(np.int64) + ln.astype(np.int64)
+        expect[ends] = 0
+        for b in range(4):
+            expect[ends + 1 + b] = ((want >> np.uint32(8 * b)) & np.uint32(0xFF)).astype(np.uint8)
+    diff = np.nonzero(after != expect)[0]
+    assert diff.size == 0, diff[:8]
 
 
 @pytest.mark.parametrize("kernel", ["default", "logstream"])

@@ -78,7 +78,7 @@ def test_product_kernels_use_no_scratch(lib):
 
 
 def test_abi_version(lib):
-    assert lib.nova_crc32c_abi_version() == C.ABI_VERSION == 2
+    assert lib.nova_crc32c_abi_version() == C.ABI_VERSION == 3
 
 
 def test_standard_results():

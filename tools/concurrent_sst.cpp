@@ -16,7 +16,8 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -o tools/bin/concurrent_sst
 //        tools/concurrent_sst.cpp -Lnovalsm_amd/lib -lnova_crc32c -Wl,-rpath,'$ORIGIN/../../novalsm_amd/lib' -lpthread
 // Run:   tools/bin/concurrent_sst <verify|trailers> <threads> <blocks per table> <seconds>
-//        [direct|queue]   (queue: nova_sst_queue_*, the coalescing queue)
+//        [direct|queue|engine]   (nova_sst_queue_*: queue = the coalescing queue,
+//        engine = the persistent engine)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -77,9 +78,11 @@ int main(int argc, char** argv) {
   const int T = atoi(argv[2]);
   const size_t n = strtoull(argv[3], nullptr, 10);
   const double secs = atof(argv[4]);
-  const bool queue = argc > 5 && !strcmp(argv[5], "queue");
+  const bool engine = argc > 5 && !strcmp(argv[5], "engine");
+  const bool queue = engine || (argc > 5 && !strcmp(argv[5], "queue"));
   if (T < 1 || T > 64 || n < 1 || n > (1u << 20) || secs <= 0) return 2;
   CKN(nova_device_init());
+  CKN(nova_sst_engine_set_enabled(engine ? 1 : 0));
 
   std::vector<Table> tabs(T);
   for (int t = 0; t < T; t++) {
@@ -177,15 +180,19 @@ int main(int argc, char** argv) {
   }
   std::sort(all.begin(), all.end());
   auto pct = [&](double p) { return all[std::min(all.size() - 1, (size_t)(p * all.size()))]; };
-  uint64_t qb = 0, qr = 0, qmax = 0;
+  uint64_t qb = 0, qr = 0, qmax = 0, er = 0, el = 0, ef = 0;
+  int erun = 0;
   CKN(nova_sst_queue_stats(&qb, &qr, &qmax));
+  CKN(nova_sst_engine_stats(&er, &el, &ef, &erun));
   printf("{\"op\": \"%s\", \"path\": \"%s\", \"queue_batches\": %llu, \"queue_requests\": %llu, "
-         "\"queue_max_tables\": %llu, \"threads\": %d, \"blocks_per_table\": %zu, \"table_bytes\": %llu, "
+         "\"queue_max_tables\": %llu, \"engine_requests\": %llu, \"engine_launches\": %llu, "
+         "\"engine_fallbacks\": %llu, \"threads\": %d, \"blocks_per_table\": %zu, \"table_bytes\": %llu, "
          "\"calls\": %zu, \"calls_per_thread_min\": %zu, \"calls_per_thread_max\": %zu, "
          "\"wall_s\": %.3f, \"aggregate_GBps\": %.1f, \"frac_of_8TBps\": %.4f, "
          "\"p50_us\": %.1f, \"p99_us\": %.1f, \"max_us\": %.1f, \"verified\": %s}\n",
-         verify ? "verify" : "trailers", queue ? "queue" : "direct", (unsigned long long)qb,
-         (unsigned long long)qr, (unsigned long long)qmax, T, n, (unsigned long long)tabs[0].algo_bytes, all.size(),
+         verify ? "verify" : "trailers", engine ? "engine" : queue ? "queue" : "direct", (unsigned long long)qb,
+         (unsigned long long)qr, (unsigned long long)qmax, (unsigned long long)er, (unsigned long long)el,
+         (unsigned long long)ef, T, n, (unsigned long long)tabs[0].algo_bytes, all.size(),
          min_calls, max_calls, wall, bytes / wall / 1e9, bytes / wall / 8e12, pct(0.50), pct(0.99),
          all.back(), good ? "true" : "false");
   for (auto& tb : tabs) {

@@ -5,8 +5,9 @@ Drives tools/bin/concurrent_sst (tools/concurrent_sst.cpp: native threads, one
 HIP stream and one device-resident SSTable image per thread, synchronous
 nova_sstable_verify_blocks / nova_sstable_write_trailers calls) over a matrix
 of thread counts and table sizes, one child process per point, and prints its
-JSON lines.  --paths direct,queue: each caller launching on its own stream,
-or every call through the coalescing queue (nova_sst_queue_*).  --hwq runs each point with GPU_MAX_HW_QUEUES set (the HIP
+JSON lines.  --paths direct,engine,queue: each caller launching on its own
+stream, or every call through nova_sst_queue_* on the persistent engine
+ or on the round-3 coalescing queue.  --hwq runs each point with GPU_MAX_HW_QUEUES set (the HIP
 runtime's hardware queues per process; 4 is the default on the box).
 
   python tools/concurrent_sst.py --build            # here, on the CPU
@@ -43,8 +44,9 @@ def main() -> int:
     ap.add_argument("--threads", default="1,2,4,8,16")
     ap.add_argument("--blocks", default="1024,4096", help="blocks per table (4 KiB blocks)")
     ap.add_argument("--seconds", type=float, default=1.0)
-    ap.add_argument("--paths", default="direct,queue",
-                    help="direct: nova_sstable_* on each caller's stream; queue: nova_sst_queue_*")
+    ap.add_argument("--paths", default="direct,engine",
+                    help="direct: nova_sstable_* on each caller's stream; engine / queue: "
+                         "nova_sst_queue_* on the persistent engine / the coalescing queue")
     ap.add_argument("--hwq", default="", help="comma list of GPU_MAX_HW_QUEUES values (<= 32)")
     args = ap.parse_args()
     if args.build:
