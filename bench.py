@@ -76,6 +76,9 @@ def config3_layout(n: int, seed: int = 3):
 
 
 SST_WORKLOADS = ("sst4k_trailers", "sst4k_verify")
+# SURVEY 8(f) rows 3-4 as driver-measured secondaries
+LOG_WORKLOADS = ("log4k_write", "log4k_verify", "log512_write", "log512_verify")
+OPS_WORKLOADS = LOG_WORKLOADS + ("parity",)
 
 
 def sst4k_layout(n: int, seed: int = 5):
@@ -91,7 +94,31 @@ def sst4k_layout(n: int, seed: int = 5):
     return offs, lens, total
 
 
+def log_bench_layout(pmax: int, total_target: int = 4 << 30, seed: int = 6):
+    """A ~4 GiB log file as log::Writer lays it out (db/log_writer.cc:53-97):
+    logical records of U[1,pmax] B payload from splitmix64(seed), fragmented at
+    32 KiB blocks.  (offsets u64, payload lengths u64, types u8, total bytes)."""
+    from novalsm_amd.synth import log_layout_fast, splitmix64_words
+    n = total_target // (7 + (pmax + 1) // 2)
+    r = splitmix64_words(seed, 0, n)
+    plens = ((r % np.uint64(pmax)) + np.uint64(1)).astype(np.int64)
+    offs, lens, types, _, total = log_layout_fast(plens)
+    return offs, lens.astype(np.uint64), types, total
+
+
 def workload(cfg):
+    if cfg in LOG_WORKLOADS:
+        pmax = 4096 if cfg.startswith("log4k") else 512
+        op = "write" if cfg.endswith("write") else "verify"
+        what = ("record CRC write (db/log_writer.cc:99-114)" if op == "write"
+                else "record verify (db/log_reader.cc:196-262)")
+        return {"workload": f"{cfg}: ~4 GiB log image per GPU, log::Writer layout of U[1,{pmax}] B payloads, "
+                            f"{what}", "n_blocks": None, "block_bytes": None, "kind": f"log_{op}",
+                "pmax": pmax}
+    if cfg == "parity":
+        return {"workload": "parity: XOR parity of 8 fragments x 512 MiB per GPU "
+                            "(ltc/stoc_file_client_impl.cpp:334-349)",
+                "n_blocks": 8, "block_bytes": 512 << 20, "kind": "parity"}
     if cfg == "sst4k_trailers":
         return {"workload": "sst4k_trailers: 1M x (4096+U[0,255]) B blocks + 5-B trailers per GPU, "
                             "trailer writer (TableBuilder ordering)",
@@ -260,6 +287,114 @@ def launch_ranks(n: int, argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
+# ---- same-run ceilings ------------------------------------------------------------
+
+def _events_avg_s(torch, fn, stream, warmup: int = 10, reps: int = 30) -> float:
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / reps / 1e3
+
+
+def parity_copy_ceiling(torch, C, buf, fo, plen, stream, args) -> dict:
+    """The XOR parity kernel's own bound, in the same run: a copy kernel of the
+    same traffic shape -- the 8 fragments read and the 512 MiB written, nothing
+    computed (copy_ceiling_kernel of the diagnostics library) --
+    at the chunks per lane that measured best in round 3, non-temporal loads and
+    stores, one-pass grid.  The faster of its forms is the ceiling."""
+    D = C.load_diag()
+    sink = torch.empty(256, dtype=torch.int32, device=buf.device)
+    tmp = torch.empty(plen, dtype=torch.uint8, device=buf.device)
+    best = None
+    for u in (1, 2, 4):
+        v = u | 1 << 4 | 1 << 5  # kind 0 (8 reads + 1 write), nt loads, nt stores
+
+        def f(v=v):
+            rc = D.nova_diag_copy_ceiling(buf.data_ptr(), fo.data_ptr(), plen, tmp.data_ptr(),
+                                          sink.data_ptr(), 0, v, stream.cuda_stream)
+            assert rc == 0, rc
+        sec = _events_avg_s(torch, f, stream)
+        gbs = 9 * plen / sec / 1e9
+        if best is None or gbs > best["achieved"]:
+            best = {"kind": "8-read + 1-write copy, no XOR (copy_ceiling_kernel, diagnostics library)",
+                    "chunks_per_lane": u, "achieved": round(gbs, 1), "unit": "GB/s",
+                    "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+    del tmp, sink
+    return best
+
+
+def h2d_ceiling(torch, host, dev_tmp, chunk: int, n_streams: int = 3) -> dict:
+    """Config 5's own bound, in the same run: pinned-host -> HBM copies of the
+    same bytes with hipMemcpyAsync (torch copy_, non_blocking), as one copy and
+    as chunk-sized copies over n_streams streams; the faster is the ceiling."""
+    total = host.numel()
+    res = {}
+
+    def one():
+        dev_tmp.copy_(host, non_blocking=True)
+
+    streams = [torch.cuda.Stream() for _ in range(n_streams)]
+
+    def chunked():
+        for i, o in enumerate(range(0, total, chunk)):
+            with torch.cuda.stream(streams[i % n_streams]):
+                dev_tmp[o:o + chunk].copy_(host[o:o + chunk], non_blocking=True)
+
+    for name, fn in (("one_copy", one), (f"chunks_{chunk >> 20}MiB_x{n_streams}_streams", chunked)):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        res[name] = total * reps / (time.perf_counter() - t0) / 1e9
+    best = max(res, key=res.get)
+    return {"kind": "pinned H2D hipMemcpyAsync of the same bytes", "form": best,
+            "achieved": round(res[best], 2), "unit": "GB/s",
+            "forms": {k: round(v, 2) for k, v in res.items()}}
+
+
+# ---- HBM preflight -----------------------------------------------------------------
+
+def hbm_need(wl) -> int:
+    """Device bytes a workload allocates (its image, descriptors and outputs)."""
+    n = wl["n_blocks"]
+    if wl["kind"] == "strided":
+        return n * wl["block_bytes"] + 4 * n
+    if wl["kind"] in ("sst_trailers", "sst_verify"):
+        return n * (4096 + 128 + 5) + 17 * n
+    if wl["kind"] == "variable":
+        return n * (28 << 10) + 16 * n
+    if wl["kind"] in ("log_write", "log_verify"):
+        return (4 << 30) + (4 << 30) // (7 + (wl["pmax"] + 1) // 2) * 26
+    if wl["kind"] == "parity":
+        return 9 * wl["block_bytes"]
+    if wl["kind"] == "host":
+        return 2 * (4096 * wl["block_bytes"]) * 4
+    return 0
+
+
+def hbm_preflight(cfg, wl, ctx) -> None:
+    """Fail loudly, on every rank, when this GPU cannot hold the workload (a
+    shape the driver's first 8-GPU run may meet untried), instead of a late
+    out-of-memory inside a kernel launch or a silent partial run."""
+    import torch
+    free, total = torch.cuda.mem_get_info(ctx.dev)
+    need = hbm_need(wl)
+    if need + (512 << 20) > free:
+        msg = {"error": "HBM preflight", "config": cfg, "rank": ctx.rank, "need_bytes": need,
+               "free_bytes": free, "total_bytes": total}
+        print(json.dumps(msg), file=sys.stderr, flush=True)
+        raise SystemExit(4)
+
+
 # ---- one device-resident config ------------------------------------------------
 
 class Ctx:
@@ -288,10 +423,56 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
     import torch
     from novalsm_amd import crc32c as C
     wl = workload(cfg)
+    hbm_preflight(cfg, wl, ctx)
     stream = torch.cuda.current_stream()
     n = wl["n_blocks"]
     seed = cfg
-    if wl["kind"] == "strided":
+    ceiling = None
+    if wl["kind"] in ("log_write", "log_verify"):
+        offs_np, lens_np, types_np, total = log_bench_layout(wl["pmax"])
+        n = len(offs_np)
+        buf = torch.empty(total + 64, dtype=torch.uint8, device=ctx.dev)
+        C.fill_splitmix64(buf, 41, first_word=ctx.rank * (total // 8))
+        offs = torch.from_numpy(offs_np.view(np.int64)).to(ctx.dev)
+        ln_t = torch.from_numpy(lens_np.view(np.int64)).to(ctx.dev)
+        buf[offs + 4] = (ln_t & 0xFF).to(torch.uint8)  # header length (LE16) and type
+        buf[offs + 5] = (ln_t >> 8).to(torch.uint8)
+        buf[offs + 6] = torch.from_numpy(types_np).to(ctx.dev)
+        del ln_t
+        sum_rec = int(lens_np.sum()) + 7 * n
+        if wl["kind"] == "log_write":
+            def step():
+                C.log_write_crcs(buf, offs, stream=stream, buf_len=total)
+            bytes_step = sum_rec  # type + payload + length/type header read, CRC field written
+            out = None
+        else:
+            C.log_write_crcs(buf, offs, stream=stream, buf_len=total)
+            out = torch.empty(n, dtype=torch.uint8, device=ctx.dev)
+            bad = torch.zeros(1, dtype=torch.int32, device=ctx.dev)
+
+            def step():
+                C.log_verify_records(buf, offs, stream=stream, ok=out, bad=bad, buf_len=total)
+            bytes_step = sum_rec + n  # the whole records read, one status byte written
+        dispatch = C.describe(n, total // n, 0, log=True, log_verify=wl["kind"] == "log_verify")
+        dispatch["op"] = "nova_log_write_crcs" if wl["kind"] == "log_write" else "nova_log_verify_records"
+        dispatch["records"] = n
+        dispatch["mean_record_span"] = round(total / n, 1)
+        lens_np = None
+    elif wl["kind"] == "parity":
+        k, plen = wl["n_blocks"], wl["block_bytes"]
+        buf = torch.empty(k * plen, dtype=torch.uint8, device=ctx.dev)
+        C.fill_splitmix64(buf, 51, first_word=ctx.rank * (k * plen // 8))
+        fo = torch.arange(k, dtype=torch.int64, device=ctx.dev) * plen
+        out = torch.empty(plen, dtype=torch.uint8, device=ctx.dev)
+
+        def step():
+            C.xor_parity(buf, fo, plen, out=out, stream=stream)
+        bytes_step = (k + 1) * plen  # k fragments read, the parity written
+        dispatch = {"op": "nova_xor_parity", "kernel": "xor_parity_kernel<8, 1>", "fragments": k,
+                    "fragment_bytes": plen}
+        offs_np = lens_np = None
+        ceiling = parity_copy_ceiling(torch, C, buf, fo, plen, stream, args)
+    elif wl["kind"] == "strided":
         L = wl["block_bytes"]
         total = n * L
         buf = torch.empty(total, dtype=torch.uint8, device=ctx.dev)
@@ -390,7 +571,25 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
         orc = load_oracle()
         idx = np.linspace(0, n - 1, 257).astype(np.int64)
         ok = True
-        if wl["kind"] == "sst_trailers":
+        if wl["kind"] == "log_write":
+            idx = np.linspace(0, n - 1, 257).astype(np.int64)
+            offs_h = offs.cpu().numpy().view(np.uint64)
+            for i in idx:
+                a = int(offs_h[i])
+                L_ = int(buf[a + 4].item()) | (int(buf[a + 5].item()) << 8)
+                rec = buf[a:a + 7 + L_].cpu().numpy()
+                want = orc.mask(orc.value(rec[6:].tobytes()))  # type byte + payload
+                ok &= int.from_bytes(rec[:4].tobytes(), "little") == want
+        elif wl["kind"] == "log_verify":
+            ok = int(bad.item()) == 0 and bool((out.cpu().numpy() == C.LOG_OK).all())
+        elif wl["kind"] == "parity":
+            k, plen = wl["n_blocks"], wl["block_bytes"]
+            for i in np.linspace(0, plen - 4097, 33).astype(np.int64):
+                want = np.zeros(4096, np.uint8)
+                for f in range(k):
+                    want ^= buf[f * plen + i:f * plen + i + 4096].cpu().numpy()
+                ok &= bool(np.array_equal(out[i:i + 4096].cpu().numpy(), want))
+        elif wl["kind"] == "sst_trailers":
             for i in idx:
                 o, ln = int(offs_np[i]), int(lens_np[i])
                 blk = buf[o:o + ln + 5].cpu().numpy().tobytes()
@@ -413,6 +612,9 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4)}
     roof.update(traffic_of(cfg, dispatch))
+    if ceiling:
+        roof["ceiling"] = ceiling
+        roof["frac_of_ceiling"] = round(achieved / ceiling["achieved"], 4)
     roof.update({"kernel_ms_avg": round(avg_launch_s * 1e3, 4),
                  "kernel_ms_min": round(min(kernel_ms), 4),
                  "kernel_ms_median": round(sorted(kernel_ms)[len(kernel_ms) // 2], 4)})
@@ -426,6 +628,12 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
         res_wl["algorithmic_bytes"] = ("sum(len) read + 5 B trailer written per block"
                                        if wl["kind"] == "sst_trailers"
                                        else "sum(len + 5) read + 1 B flag written per block")
+    elif wl["kind"] == "log_write":
+        res_wl["algorithmic_bytes"] = "sum(7 + len) per record: header length/type and payload read, CRC written"
+    elif wl["kind"] == "log_verify":
+        res_wl["algorithmic_bytes"] = "sum(7 + len) read + 1 B status written per record"
+    elif wl["kind"] == "parity":
+        res_wl["algorithmic_bytes"] = "8 fragments read + the parity written"
     return {
         "config": cfg,
         "value": round(ctx.world * bytes_step * args.steps / dt_max / 2**30, 2),
@@ -478,25 +686,51 @@ def traffic_of(cfg, dispatch: dict) -> dict:
     return {"traffic": pmc.get("hbm_bytes_per_launch"), "traffic_source": src + ")"}
 
 
-def run_host_config(args, ctx: Ctx) -> int:
+def host_config_measure(args, ctx: Ctx, steps: int, warmup: int) -> dict:
+    """Config 5: 4 GiB of pinned 16 KiB blocks streamed H2D -> CRC -> D2H
+    (nova_crc32c_stream_host), its rate against the same-run pinned H2D copy
+    ceiling, every block's CRC checked against the device-resident path."""
     import torch
     from novalsm_amd import crc32c as C
     wl = workload(5)
+    hbm_preflight(5, wl, ctx)
     L, n = wl["block_bytes"], wl["n_blocks"]
     host = torch.empty(n * L, dtype=torch.uint8).pin_memory()
     tmp = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
     C.fill_splitmix64(tmp, 5, first_word=ctx.rank * (n * L // 8))
     host.copy_(tmp.cpu())
+    want = C.batch_strided(tmp, L, L, n).cpu()
+    ceiling = h2d_ceiling(torch, host, tmp, 4096 * L)
     del tmp
-    for _ in range(max(1, args.warmup)):
-        C.stream_host(host, L, L, n)
+    torch.cuda.empty_cache()
+    out = None
+    for _ in range(max(1, warmup)):
+        out = C.stream_host(host, L, L, n)
     ctx.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        C.stream_host(host, L, L, n)
+    for _ in range(steps):
+        out = C.stream_host(host, L, L, n)
     ctx.barrier()
     dt = max(ctx.all_gather_f64(time.perf_counter() - t0))
-    value = ctx.world * n * L * args.steps / dt / 2**30
+    verified = bool(np.array_equal(np.asarray(out).view(np.uint32), want.numpy().view(np.uint32)))
+    gbs = n * L * steps / dt / 1e9
+    return {"value": round(ctx.world * n * L * steps / dt / 2**30, 3), "unit": "GiB/s",
+            "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "workload": {"workload": wl["workload"], "n_blocks": n, "block_bytes": L,
+                         "bytes_per_gpu": n * L, "op": "nova_crc32c_stream_host",
+                         "chunk_blocks": 4096, "streams": 3},
+            "roofline": {"bound": "pcie_h2d", "achieved": round(gbs, 2), "peak": ceiling["achieved"],
+                         "unit": "GB/s", "frac": round(gbs / ceiling["achieved"], 4),
+                         "ceiling": ceiling, "pcie_gen5_x16_spec_GBps": 63.0,
+                         "traffic": None, "traffic_source": "host-link bound: no HBM PMC pass"},
+            "verified_sample": verified}
+
+
+def run_host_config(args, ctx: Ctx) -> int:
+    r = host_config_measure(args, ctx, args.steps, args.warmup)
+    value, dt = r["value"], r["ms_per_step"] * args.steps / 1e3
+    wl = workload(5)
+    L, n = wl["block_bytes"], wl["n_blocks"]
     if ctx.rank == 0:
         print(json.dumps({"metric": "GiB/s pinned-host streamed CRC32C (H2D->CRC->D2H), 16 KiB",
                           "value": round(value, 3), "unit": "GiB/s", "n_gpus": ctx.world,
@@ -505,8 +739,9 @@ def run_host_config(args, ctx: Ctx) -> int:
                           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                           "dtype": "u8", "data": "synthetic (splitmix64)",
                           "config": {"workload": wl["workload"], "n_blocks": n,
-                                     "block_bytes": L}}), flush=True)
-    return 0
+                                     "block_bytes": L}, "roofline": r["roofline"],
+                          "verified_sample": r["verified_sample"]}), flush=True)
+    return 0 if r["verified_sample"] else 3
 
 
 def harness_check(args, world: int, rank: int) -> int:
@@ -522,11 +757,19 @@ def harness_check(args, world: int, rank: int) -> int:
     crc = C.Value(data)
     import torch
     t = torch.tensor([float(rank)], dtype=torch.float64)
+    ranks = [rank]
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        parts = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(parts, torch.tensor([rank, int(os.environ.get("LOCAL_RANK", "0"))]))
+        ranks = sorted(int(x[0]) for x in parts)
+        local = sorted(int(x[1]) for x in parts)
+    else:
+        local = [0]
     if rank == 0:
         print(json.dumps({"harness_check": True, "n_gpus": world, "backend": "gloo",
-                          "max_rank": int(t.item()), "crc": f"0x{crc:08x}"}), flush=True)
+                          "max_rank": int(t.item()), "ranks": ranks, "local_ranks": local,
+                          "crc": f"0x{crc:08x}"}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -538,10 +781,11 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="2", choices=["2", "3", "4", "5", *SST_WORKLOADS])
+    ap.add_argument("--config", default="2", choices=["2", "3", "4", "5", *SST_WORKLOADS, *OPS_WORKLOADS])
     ap.add_argument("--secondary", default="auto",
-                    help="configs measured after the primary one in the same run "
-                         "(comma list, 'none'; auto: 3,4 when the primary is 2)")
+                    help="configs measured after the primary one in the same run (comma list, "
+                         "'none'; auto, when the primary is 2: 3, 4, the SSTable, log and parity "
+                         "workloads, and 5 -- pinned host, one GPU only)")
     ap.add_argument("--settle-ms", type=float, default=400.0,
                     help="time-based settle of back-to-back launches before the warmup")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per unit override (tuning)")
@@ -592,7 +836,7 @@ def main() -> int:
 
     prim = run_device_config(args.config, args, ctx)
     if args.secondary == "auto":
-        sec_cfgs = [3, 4, *SST_WORKLOADS] if args.config == 2 else []
+        sec_cfgs = [3, 4, *SST_WORKLOADS, *OPS_WORKLOADS, 5] if args.config == 2 else []
     elif args.secondary in ("", "none"):
         sec_cfgs = []
     else:
@@ -601,6 +845,12 @@ def main() -> int:
     secondary = []
     for c in sec_cfgs:
         if c == 5:
+            # the host link is per GPU and 4 GiB of pinned memory per rank is
+            # the node's, not the GPU's: measured at N = 1 only
+            if world == 1:
+                r = host_config_measure(args, ctx, max(3, args.steps // 20), max(1, args.warmup // 20))
+                secondary.append({"metric": "GiB/s pinned-host streamed CRC32C (H2D->CRC->D2H), 16 KiB; "
+                                            "% of the same-run H2D copy ceiling", "config": 5, **r})
             continue
         r = run_device_config(c, args, ctx)
         secondary.append({"metric": METRIC, **r})

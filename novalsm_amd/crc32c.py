@@ -619,10 +619,12 @@ def plan(n_blocks: int, bytes_per_block: int):
 
 
 def describe(n_blocks: int, length: int, stride: int, variable: bool = False,
-             large: bool = False, log: bool = False) -> dict:
+             large: bool = False, log: bool = False, log_verify: bool = False) -> dict:
+    """The product's plan for a batch (nova_crc32c_describe); log / log_verify:
+    n_blocks log records of mean span `length` written / verified."""
     import json
     buf = ctypes.create_string_buffer(512)
-    v = 3 if log else ((2 if large else 1) if variable else 0)
+    v = 4 if log_verify else 3 if log else ((2 if large else 1) if variable else 0)
     _L().nova_crc32c_describe(n_blocks, length, stride, v, buf, 512)
     return json.loads(buf.value.decode())
 

@@ -1305,13 +1305,24 @@ int nova_crc32c_describe(size_t n_blocks, uint64_t len, uint64_t stride, int var
                  sg, sg, stream_bpg(sg, (uint32_t)len),
                  g_tune_static_pct.load() < 0 ? 8 : g_tune_static_pct.load());
   } else {
-    const bool log = variable == 3;
-    const int mode = log ? kLogWrite : kStore;
+    // variable 3 / 4: log records (len = mean record span) written / verified
+    const bool log = variable == 3 || variable == 4;
+    const int mode = variable == 4 ? kLogVerify : log ? kLogWrite : kStore;
     const Plan pl = plan(n_blocks, len, !variable, mode, variable == 2, cus_hint());
     const int g = pl.G < 2 ? 2 : pl.G;
     // the chunk launch_rounds() runs when plan() leaves it to the default
     const uint32_t def_chunk = log ? 64u : 4u * (64u / (uint32_t)g);
-    if (pl.kernel == kRoundsK)
+    // log verify of large logs: windowed pre-sort by line count (run())
+    const bool presort = mode == kLogVerify && g == 8 && n_blocks >= kLogSortMin && g_tune_sort.load() >= 2;
+    if (pl.kernel == kRoundsK && presort)
+      n = snprintf(buf, buflen,
+                   "{\"kernel\": \"crc32c_rounds_kernel<%d, %d>\", \"lanes_per_block\": %d, "
+                   "\"sort\": %d, \"waves_per_wg\": %d, \"chunk_blocks\": %u, "
+                   "\"kernels\": [\"log_sort_kernel\", \"crc32c_rounds_kernel<%d, %d>\", "
+                   "\"log_unperm_kernel\"], \"sort_window\": %u}", g, mode, g, g_tune_sort.load(),
+                   (int)flat_waves(), pl.chunk ? pl.chunk : def_chunk, g, mode,
+                   log_sort_window(n_blocks, (uint64_t)n_blocks * len));
+    else if (pl.kernel == kRoundsK)
       n = snprintf(buf, buflen,
                    "{\"kernel\": \"crc32c_rounds_kernel<%d, %d>\", \"lanes_per_block\": %d, "
                    "\"sort\": %d, \"waves_per_wg\": %d, \"chunk_blocks\": %u}", g, mode,

@@ -94,3 +94,117 @@ def log_image(seed: int, payload_lens, block_offset: int = 0):
     for a, b in pads:
         img[a:b] = 0
     return img, offs, lens, types
+
+
+def big_string(partial: bytes, n: int) -> bytes:
+    """BigString (db/log_test.cc:19-26): `partial` repeated, cut to n bytes."""
+    reps = n // len(partial) + 1
+    return (partial * reps)[:n]
+
+
+def log_case_image(writes, mutations, crc_of):
+    """The file a log::Writer leaves after AddRecord of each payload in
+    `writes` (db/log_writer.cc:53-114: log_layout above, header CRC
+    Mask(Value(type || payload)) from `crc_of(bytes) -> masked u32`), then the
+    edits a reader test makes to it (db/log_test.cc:76-97):
+      ("inc", offset, delta)   IncrementByte: byte += delta (mod 256)
+      ("set", offset, value)   SetByte
+      ("shrink", nbytes)       ShrinkSize: drop the file's last nbytes
+      ("fixcrc", offset, len)  FixChecksum: the CRC of the header at offset
+                               over its type byte and len payload bytes
+    Returns (image u8, physical record offsets u64)."""
+    offs, lens, types, pads, total = log_layout([len(w) for w in writes])
+    img = np.zeros(total, np.uint8)
+    k = 0
+    for w in writes:  # the fragments of each logical record, in order
+        done = 0
+        while True:
+            o, ln = int(offs[k]), int(lens[k])
+            img[o + 4] = ln & 0xFF
+            img[o + 5] = ln >> 8
+            img[o + 6] = types[k]
+            img[o + 7:o + 7 + ln] = np.frombuffer(w[done:done + ln], np.uint8)
+            c = crc_of(bytes([int(types[k])]) + w[done:done + ln])
+            img[o:o + 4] = np.frombuffer(int(c).to_bytes(4, "little"), np.uint8)
+            done += ln
+            k += 1
+            if done >= len(w):
+                break
+    for m in mutations:
+        if m[0] == "inc":
+            img[m[1]] = (int(img[m[1]]) + m[2]) & 0xFF
+        elif m[0] == "set":
+            img[m[1]] = m[2] & 0xFF
+        elif m[0] == "shrink":
+            img = img[:img.size - m[1]].copy()
+        elif m[0] == "fixcrc":
+            o, ln = m[1], m[2]
+            c = crc_of(img[o + 6:o + 7 + ln].tobytes())
+            img[o:o + 4] = np.frombuffer(int(c).to_bytes(4, "little"), np.uint8)
+        else:
+            raise ValueError(m)
+    return img, offs
+
+
+def log_layout_fast(payload_lens):
+    """log_layout(payload_lens) for a file starting at a block boundary, with the
+    records that fit a block whole placed by one numpy step per 32 KiB block
+    (log_layout walks them one by one: ~25 s for a 4 GiB image of 263-B
+    records).  Same result (tests/test_host_api.py checks them equal)."""
+    pl = np.asarray(payload_lens, dtype=np.int64)
+    n = pl.size
+    O, L, T, pads = [], [], [], []
+    i, bo, pos = 0, 0, 0  # next logical record, offset in the block, block start
+    rem, begin = 0, True
+    win = 256
+    while i < n:
+        leftover = LOG_BLOCK - bo
+        if leftover < LOG_HEADER:  # db/log_writer.cc:64-73
+            if leftover > 0:
+                pads.append((pos + bo, pos + LOG_BLOCK))
+            pos += LOG_BLOCK
+            bo = 0
+            continue
+        if not begin:  # the rest of record i: MIDDLE or LAST fragments
+            frag = min(rem, LOG_BLOCK - bo - LOG_HEADER)
+            end = frag == rem
+            O.append(np.array([pos + bo], np.int64))
+            L.append(np.array([frag], np.int64))
+            T.append(np.array([LAST if end else MIDDLE], np.uint8))
+            bo += LOG_HEADER + frag
+            rem -= frag
+            if end:
+                i += 1
+                begin = True
+            continue
+        # records i.. that fit this block whole: FULL
+        while True:
+            k = min(n - i, win)
+            cs = np.cumsum(LOG_HEADER + pl[i:i + k])
+            m = int(np.searchsorted(cs, leftover, side="right"))
+            if m < k or i + k == n:
+                break
+            win *= 2
+        if m:
+            starts = cs[:m] - (LOG_HEADER + pl[i:i + m])
+            O.append(pos + bo + starts)
+            L.append(pl[i:i + m].copy())
+            T.append(np.full(m, FULL, np.uint8))
+            bo += int(cs[m - 1])
+            i += m
+            if m > 64:
+                win = max(256, 2 * m)
+            continue
+        # record i begins here as a FIRST fragment (possibly empty)
+        frag = leftover - LOG_HEADER
+        O.append(np.array([pos + bo], np.int64))
+        L.append(np.array([frag], np.int64))
+        T.append(np.array([FIRST], np.uint8))
+        bo += LOG_HEADER + frag
+        rem = int(pl[i]) - frag
+        begin = False
+    total = pos + bo
+    offs = np.concatenate(O).astype(np.uint64) if O else np.zeros(0, np.uint64)
+    lens = np.concatenate(L).astype(np.uint32) if L else np.zeros(0, np.uint32)
+    types = np.concatenate(T) if T else np.zeros(0, np.uint8)
+    return offs, lens, types, pads, total

@@ -169,3 +169,30 @@ def load_oracle() -> Oracle:
         build_oracle()
         _cache = Oracle(ctypes.CDLL(ORACLE_SO))
     return _cache
+
+
+def log_reader_case(oracle, case):
+    """A tests/golden/log_reader_cases.json case rebuilt with the ORACLE's CRC
+    (oracle/gen_log_cases.py used the reference's): (image, offsets, expected
+    statuses).  The image must hash to the fixture's SHA-256."""
+    import hashlib
+    from novalsm_amd.synth import big_string, log_case_image
+
+    writes = []
+    for w in case["writes"]:
+        if w[0] == "lit":
+            writes.append(w[1].encode())
+        elif w[0] == "big":
+            writes.append(big_string(w[1].encode(), w[2]))
+        else:  # "numbers": NumberString(i), db/log_test.cc:29-33
+            writes.extend(f"{i}.".encode() for i in range(w[1]))
+    img, offs = log_case_image(writes, case["edits"],
+                               lambda b: oracle.mask(oracle.value(b)))
+    assert hashlib.sha256(img.tobytes()).hexdigest() == case["sha256"], case["name"]
+    assert img.size == case["buf_len"], case["name"]
+    offsets = [int(x) for x in offs] + [int(x) for x in case["probes"]]
+    if case["offsets"] is not None:
+        assert offsets == case["offsets"], case["name"]
+    expect = case["expect"] if case["expect"] is not None else [case["expect_all"]] * len(offsets)
+    assert len(expect) == case["n_records"] == len(offsets)
+    return img, np.array(offsets, np.uint64), np.array(expect, np.uint8)

@@ -1319,6 +1319,43 @@ def _golden_log_checks(torch, golden, oracle):
     assert np.array_equal(ok.cpu().numpy(), oracle.log_check(buf.cpu().numpy(), offs))
 
 
+def _log_reader_cases():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "log_reader_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("kernel", ["default", "units"])
+@pytest.mark.parametrize("case", _log_reader_cases(), ids=lambda c: c["name"])
+def test_log_reader_cases_device(torch_gpu, oracle, case, kernel):
+    """nova_log_verify_records on the files the reference's
+    own reader tests write and edit (db/log_test.cc, tests/golden/
+    log_reader_cases.json; MarginalTrailer, ShortTrailer, AlignedEof,
+    TruncatedTrailingRecordIsIgnored, BadLength, BadLengthAtEndIsIgnored,
+    ChecksumMismatch, MissingLast/PartialLastIsIgnored, ...): every record's
+    status and n_bad equal what that test asserts.  The buffer extends past
+    buf_len (the bytes there must not matter); "units" forces the units
+    kernel's log path."""
+    torch = torch_gpu
+    from tests.oracle_lib import log_reader_case
+    host, offs, expect = log_reader_case(oracle, case)
+    buf = dev(torch, np.concatenate([host, np.full(512, 0x5A, np.uint8)]))
+    doffs = dev(torch, offs, torch.int64)
+    ctx = C.diagnostics() if kernel != "default" else None
+    if ctx:
+        ctx.__enter__()
+        C.set_tuning(16, 4096)  # forced segments: the units kernel's log path
+    try:
+        st, bad = C.log_verify_records(buf, doffs, buf_len=case["buf_len"])
+        got = st.cpu().numpy()
+        assert np.array_equal(got, expect), (case["name"], np.nonzero(got != expect)[0][:8])
+        assert int(bad.item()) == case["n_bad"]
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+
+
 @pytest.mark.parametrize("kernel", ["default", "units", "logstream"])
 def test_log_record_bounds(torch_gpu, golden, oracle, kernel):
     """ADVICE r01 / db/log_reader.cc:196-247: a record whose length field runs

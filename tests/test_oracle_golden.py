@@ -208,3 +208,25 @@ def test_xor_parity_oracle():
     par = orc.xor_parity(buf, offs, 3000)
     want = buf[0:3000] ^ buf[1003:4003] ^ buf[5001:8001]
     assert np.array_equal(par, want)
+
+
+def _log_cases():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "log_reader_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", _log_cases(), ids=lambda c: c["name"])
+def test_log_reader_cases_oracle(oracle, case):
+    """the reference's own reader tests (db/log_test.cc,
+    cited per case) as golden data -- the file each test writes and edits,
+    rebuilt here with the oracle's CRC to the fixture's hash (whose CRCs came
+    from the reference util/crc32c.cc), and the per-record statuses that test's
+    assertions imply (oracle/gen_log_cases.py).  The oracle's ReadPhysicalRecord
+    restatement must give exactly those statuses."""
+    from tests.oracle_lib import log_reader_case
+    img, offs, expect = log_reader_case(oracle, case)
+    got = oracle.log_check(img, offs, buf_len=case["buf_len"])
+    assert np.array_equal(got, expect), (case["name"], got[:16], expect[:16])
+    assert int(np.isin(got, [0, 2]).sum()) == case["n_bad"]
