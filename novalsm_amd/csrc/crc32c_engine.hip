@@ -280,16 +280,29 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wp
     // r + kRing only after request r is done, and a live request's seq is
     // above (newest written seq) - kRing, so a slot found holding a newer
     // seq s1 - 1 moves the cursor to s1 - kRing (still at or below it).
-    EngSlot* S = nullptr;
+    // All of a slot's fields are read at once (one round trip); a slot that
+    // turns out not to hold ticket t is passed over and the next one read.
+    uint64_t cstart = 0, cend = 0, base = 0, offs = 0, sizes = 0, out = 0, bad = 0, n = 0;
+    uint32_t mode = 0, flags = 0, cb = 0;
     for (;;) {
-      S = &d->slot[r % kRing];
-      uint64_t s1 = 0, ce = 0;
+      const EngSlot* S = &d->slot[r % kRing];
+      uint64_t s1 = 0;
       if (lane == 0) {
         s1 = ld_agent(&S->seq1);
-        ce = ld_agent(&S->cend);
+        cstart = ld_agent(&S->cstart);
+        cend = ld_agent(&S->cend);
+        base = ld_agent(&S->base);
+        offs = ld_agent(&S->offs);
+        sizes = ld_agent(&S->sizes);
+        out = ld_agent(&S->out);
+        bad = ld_agent(&S->bad);
+        n = ld_agent(&S->n);
+        mode = ld_agent(&S->mode);
+        flags = ld_agent(&S->flags);
+        cb = ld_agent(&S->cb);
       }
       s1 = uni64(s1);
-      ce = uni64(ce);
+      const uint64_t ce = uni64(cend);
       if (s1 > r + 1) {
         r = s1 - kRing > r + 1 ? s1 - kRing : r + 1;
         continue;
@@ -301,21 +314,6 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wp
       if (s1 == r + 1) break;
       if (lane == 0) st_sys(&e.ctl->error, 2u);  // published tickets with no slot: cannot happen
       return;
-    }
-    uint64_t cstart = 0, cend = 0, base = 0, offs = 0, sizes = 0, out = 0, bad = 0, n = 0;
-    uint32_t mode = 0, flags = 0, cb = 0;
-    if (lane == 0) {
-      cstart = ld_agent(&S->cstart);
-      cend = ld_agent(&S->cend);
-      base = ld_agent(&S->base);
-      offs = ld_agent(&S->offs);
-      sizes = ld_agent(&S->sizes);
-      out = ld_agent(&S->out);
-      bad = ld_agent(&S->bad);
-      n = ld_agent(&S->n);
-      mode = ld_agent(&S->mode);
-      flags = ld_agent(&S->flags);
-      cb = ld_agent(&S->cb);
     }
     cstart = uni64(cstart);
     cend = uni64(cend);

@@ -1289,7 +1289,8 @@ def test_log_records_write_verify(torch_gpu, golden, oracle, kernel):
     db/log_reader.cc:196-262) against the reference-generated log fixture (a
     log::Writer layout with FULL/FIRST/MIDDLE/LAST fragments over ~20 blocks),
     then the reader's per-record statuses against the oracle.  "logstream"
-    forces the whole-image kernel (the product picks it for logs >= 64 MiB)."""
+    forces the whole-image log-stream experiment (diagnostics build only,
+    DESIGN.md 3.5e; the product always runs the rounds kernel)."""
     if kernel == "logstream":
         with C.diagnostics() as L:
             L.nova_diag_set_variable_kernel(4)
