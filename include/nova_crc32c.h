@@ -187,6 +187,14 @@ int nova_sst_engine_set_idle_us(uint32_t us);
 /* Route the nova_sst_queue_* calls of this process: 1 the engine, 0 the
  * coalescing queue, -1 back to NOVA_SST_ENGINE (default: the engine). */
 int nova_sst_engine_set_enabled(int on);
+/* Engine tracing (from the next instance; resets the sums): per request, the
+ * dispatcher's, first chunk's and last chunk's s_memrealtime stamps.
+ * nova_sst_engine_trace_stats: requests traced and averages in us of
+ * [submit -> completion seen (host clock), dispatched -> first chunk started,
+ * first chunk started -> last chunk done, dispatched -> last chunk done (GPU
+ * clock)], then the largest host span. */
+int nova_sst_engine_set_trace(int on);
+int nova_sst_engine_trace_stats(uint64_t* n, double* out5);
 
 /* ---- MANIFEST / write-ahead log records ----------
  * buf holds buf_len bytes of a log file image starting at a 32 KiB log-block

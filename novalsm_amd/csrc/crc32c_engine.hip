@@ -103,6 +103,7 @@ struct EngDev {  // device memory, zeroed before every launch
   uint32_t head[kXcds][32];  // per-XCD ticket heads, one 128-B line each
   uint32_t cdone[kRing];     // chunks finished, per slot
   EngSlot slot[kRing];
+  uint64_t tr[kRing][4];     // trace: dispatched, first chunk started, last chunk done (s_memrealtime)
 };
 struct EngParams {
   const EngHostReq* hring;
@@ -112,6 +113,7 @@ struct EngParams {
   uint64_t first_seq;
   uint64_t idle_ticks;     // s_memrealtime ticks (100 MHz) without a request before exiting
   uint64_t give_up_ticks;  // no new ticket (worker) / an unfinished request (dispatcher) this long: exit
+  uint64_t* htrace;        // trace (or null): per request, the tr words copied to pinned memory
   CrcParams tab;           // tables and zero line for every chunk
 };
 
@@ -144,6 +146,22 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 __device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// LDS words at absolute byte addresses (the dynamic LDS region starts at 0).
+__device__ __forceinline__ __attribute__((address_space(3))) uint64_t* lds64(uint32_t a) {
+  return reinterpret_cast<__attribute__((address_space(3))) uint64_t*>(a);
+}
+__device__ __forceinline__ __attribute__((address_space(3))) uint32_t* lds32(uint32_t a) {
+  return reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(a);
+}
+// Per workgroup: [the end word as last read][stop][poll lock], after the tables
+// and every wave's scratch.  One waiting wave per CU at a time reads the
+// device's end and stop words and copies them here; the others spin on
+// these LDS words -- 256 pollers of the end word's line instead of ~2800.
+template <int G>
+constexpr uint32_t poll_off() {
+  return kMainBytes + (2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16)) * kTreeBytes + kEngMaxWaves * kWaveScratch;
+}
 
 // Wave 0 of workgroup 0: host ring -> device slots, tickets published.
 __device__ void engine_dispatch(const EngParams& e) {
@@ -196,6 +214,11 @@ __device__ void engine_dispatch(const EngParams& e) {
         st_agent(&S->mode, r.mode);
         st_agent(&S->flags, r.flags);
         st_agent(&S->cb, r.cb);
+        if (e.htrace) {
+          st_agent(&d->tr[seq % kRing][0], now_ticks());
+          st_agent(&d->tr[seq % kRing][1], ~(uint64_t)0);
+          st_agent(&d->tr[seq % kRing][2], (uint64_t)0);
+        }
         st_agent(&S->seq1, seq + 1);
       }
       const uint64_t total = uni64(((uint64_t)(uint32_t)__shfl((int)(uint32_t)(inc >> 32), 63) << 32) |
@@ -249,20 +272,44 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wp
   uint64_t t = claim();
   for (;;) {
     if (t >= dend) {  // wait for the ticket to be published, or for the stop
+      constexpr uint32_t kPoll = poll_off<G>();
       uint64_t t0 = now_ticks();
       for (uint32_t spin = 0;; spin++) {
-        uint64_t x = 0;
-        uint32_t stop = 0;
-        if (lane == 0) {
-          x = ld_agent(&d->dend);
-          stop = ld_agent(&d->dstop);
+        // the workgroup's copy first; then, if no other wave of this CU is
+        // reading them, the device's words (published into the copy)
+        // (atomic loads: other waves write these words; a plain load could be hoisted)
+        uint64_t x = __hip_atomic_load(lds64(kPoll), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        uint32_t stop = __hip_atomic_load(lds32(kPoll + 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        uint32_t got = 0;
+        if (t >= x && !stop && lane == 0) {
+          uint32_t expect = 0;
+          got = __hip_atomic_compare_exchange_strong(lds32(kPoll + 12), &expect, 1u, __ATOMIC_RELAXED,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                    ? 1u : 0u;
         }
-        x = uni64(x);
+        if (uni32(got)) {
+          uint64_t g = 0;
+          uint32_t gs = 0;
+          if (lane == 0) {
+            g = ld_agent(&d->dend);
+            gs = ld_agent(&d->dstop);
+            // only the lock holder writes them, so a plain compare is enough
+            if (g > __hip_atomic_load(lds64(kPoll), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+              __hip_atomic_store(lds64(kPoll), g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (gs) __hip_atomic_store(lds32(kPoll + 8), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(lds32(kPoll + 12), 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          x = uni64(g);
+          stop = uni32(gs);
+        } else {
+          x = uni64(x);
+          stop = uni32(stop);
+        }
         if (t < x) {
           dend = x;
           break;
         }
-        if (uni32(stop)) return;
+        if (stop) return;
         if (x != dend) {  // progress: restart the give-up clock
           dend = x;
           t0 = now_ticks();
@@ -270,10 +317,10 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wp
           if (lane == 0) st_sys(&e.ctl->error, 1u);
           return;
         }
-        if (spin < 32)
-          __builtin_amdgcn_s_sleep(2);
+        if (spin < 64)
+          __builtin_amdgcn_s_sleep(1);
         else
-          __builtin_amdgcn_s_sleep(12);
+          __builtin_amdgcn_s_sleep(6);
       }
     }
     // The request holding ticket t.  Slot r % kRing is reused for seq
@@ -327,6 +374,8 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wp
     mode = uni32(mode);
     const uint64_t nt = claim();  // the next ticket, in flight during this chunk
     const uint64_t c = t - cstart;
+    if (e.htrace && lane == 0)
+      __hip_atomic_fetch_min((g64*)&d->tr[r % kRing][1], now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (mode == kVerify) {
       p.ok_out = (uint8_t*)uni64(out);
       p.n_bad = (uint32_t*)uni64(bad);
@@ -341,10 +390,19 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wp
     // once drained they are in memory, so the count needs no release fence
     drain_vm();
     if (lane == 0) {
+      if (e.htrace) {
+        __hip_atomic_fetch_max((g64*)&d->tr[r % kRing][2], now_ticks(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        drain_vm();
+      }
       const uint32_t prev = __hip_atomic_fetch_add((g32*)&d->cdone[r % kRing], 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
       if ((uint64_t)prev + 1 == cend - cstart) {  // the request's last chunk: every other
         // chunk's wave drained its results before its add, this one before its own
+        if (e.htrace) {
+          for (int k = 0; k < 3; k++) st_sys(&e.htrace[(r % kRing) * 4 + k], ld_agent(&d->tr[r % kRing][k]));
+          drain_vm();
+        }
         st_sys(&e.hdone[r % kRing], r + 1);
         __hip_atomic_fetch_add((g64*)&d->reqs_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -358,6 +416,11 @@ __global__ void __launch_bounds__(kEngMaxWaves * 64) crc32c_engine_kernel(EngPar
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
   lds_fill_tables(lds, e.tab.tab_main, e.tab.tab_tree, kLevels * kTreeBytes / 16, nullptr, 0);
+  if (threadIdx.x == 0) {  // the workgroup's copy of the end / stop words, and the poll lock
+    *lds64(poll_off<G>()) = 0;
+    *lds32(poll_off<G>() + 8) = 0;
+    *lds32(poll_off<G>() + 12) = 0;
+  }
   __syncthreads();
   const int wave = threadIdx.x >> 6;
   if (blockIdx.x == 0 && wave == 0) {
@@ -370,7 +433,8 @@ __global__ void __launch_bounds__(kEngMaxWaves * 64) crc32c_engine_kernel(EngPar
 
 template <int G>
 constexpr size_t engine_lds(int waves) {
-  return kMainBytes + (2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16)) * kTreeBytes + waves * kWaveScratch;
+  (void)waves;  // the poll words sit after the largest launch's wave scratch
+  return poll_off<G>() + 16;
 }
 
 // ---- host side --------------------------------------------------------------
@@ -398,6 +462,12 @@ struct Engine {
   std::atomic<uint64_t> inflight{0};
   uint64_t requests = 0, relaunches = 0, fallbacks = 0;
   uint32_t idle_us = 0, waves = 0;
+  // trace (nova_sst_engine_set_trace): per-request spans, summed under tmu
+  uint64_t* htrace = nullptr;  // pinned, kRing x 4
+  bool trace = false;
+  std::mutex tmu;
+  uint64_t tr_n = 0;
+  double tr_host_us = 0, tr_wait_us = 0, tr_run_us = 0, tr_gpu_us = 0, tr_host_max = 0;
 
   int init_locked(int d) {
     if (ready) return 0;
@@ -413,6 +483,8 @@ struct Engine {
       e = hipHostMalloc((void**)&hdone, sizeof(uint64_t) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&ctl, sizeof(EngCtl), hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess)
+      e = hipHostMalloc((void**)&htrace, sizeof(uint64_t) * 4 * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess) e = hipMalloc((void**)&ddev, sizeof(EngDev));
     if (e == hipSuccess)
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG>),
@@ -459,6 +531,7 @@ struct Engine {
     p.first_seq = first;
     p.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
     p.give_up_ticks = 20ull * 100000000ull;  // 20 s (every spin of the engine is bounded)
+    p.htrace = trace ? htrace : nullptr;
     p.tab.tab_main = t->main[gindex(kEngG)];
     p.tab.tab_tree = t->tree;
     p.tab.tab_ft = t->ft;
@@ -601,6 +674,7 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   }
   // wait for the completion word; relaunch if the instance exited without
   // taking this request
+  const auto t_submit = std::chrono::steady_clock::now();
   const volatile uint64_t* hd = g.hdone + seq % kRing;
   const volatile EngCtl* c = g.ctl;
   const auto t0 = std::chrono::steady_clock::now();
@@ -632,6 +706,21 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   }
   std::atomic_thread_fence(std::memory_order_acquire);
   g.inflight.fetch_sub(1);
+  if (g.trace) {  // this request's spans (the stamps were stored before its completion word)
+    const double host_us =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_submit).count();
+    const volatile uint64_t* tr = g.htrace + (seq % kRing) * 4;
+    const uint64_t t0 = tr[0], t1 = tr[1], t2 = tr[2];
+    std::lock_guard<std::mutex> lk(g.tmu);
+    g.tr_n++;
+    g.tr_host_us += host_us;
+    g.tr_host_max = host_us > g.tr_host_max ? host_us : g.tr_host_max;
+    if (t1 >= t0 && t2 >= t1) {  // s_memrealtime: 100 MHz
+      g.tr_wait_us += (double)(t1 - t0) / 100.0;
+      g.tr_run_us += (double)(t2 - t1) / 100.0;
+      g.tr_gpu_us += (double)(t2 - t0) / 100.0;
+    }
+  }
   return 0;
 }
 
@@ -683,6 +772,35 @@ int nova_sst_engine_stats(uint64_t* requests, uint64_t* launches, uint64_t* fall
   if (launches) *launches = gp->gen;
   if (fallbacks) *fallbacks = gp->fallbacks;
   if (running) *running = gp->running && gp->ctl && !((volatile EngCtl*)gp->ctl)->exited ? 1 : 0;
+  return 0;
+}
+
+int nova_sst_engine_set_trace(int on) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<std::mutex> lk(gp->mu);
+  gp->trace = on != 0;  // from the next instance
+  std::lock_guard<std::mutex> lt(gp->tmu);
+  gp->tr_n = 0;
+  gp->tr_host_us = gp->tr_wait_us = gp->tr_run_us = gp->tr_gpu_us = gp->tr_host_max = 0;
+  return 0;
+}
+
+int nova_sst_engine_trace_stats(uint64_t* n, double* out5) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<std::mutex> lt(gp->tmu);
+  const double k = gp->tr_n ? 1.0 / (double)gp->tr_n : 0.0;
+  if (n) *n = gp->tr_n;
+  if (out5) {
+    out5[0] = gp->tr_host_us * k;  // submit -> completion seen, host clock
+    out5[1] = gp->tr_wait_us * k;  // dispatched -> first chunk started, GPU clock
+    out5[2] = gp->tr_run_us * k;   // first chunk started -> last chunk done
+    out5[3] = gp->tr_gpu_us * k;   // dispatched -> last chunk done
+    out5[4] = gp->tr_host_max;
+  }
   return 0;
 }
 

@@ -1250,26 +1250,48 @@ def test_queue_batched_trailers_adjacent_tables(torch_gpu, oracle):
         except Exception as e:  # pragma: no cover
             errors.append(e)
 
+    # a long call holds the queue's one batch slot while the four callers
+    # enqueue behind it; the next leader then takes all four in one batch
+    nb_blk = 1 << 19
+    b_offs, b_lens, b_total = sst4k_layout(nb_blk, 7)
+    bimg = torch.empty(b_total + 64, dtype=torch.uint8, device="cuda")
+    C.fill_splitmix64(bimg, 77)
+    b_o = torch.from_numpy(b_offs.view(np.int64)).cuda()
+    b_l = torch.from_numpy(b_lens.view(np.int32)).cuda()
+    b_ok = torch.empty(nb_blk, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+
+    def blocker(gate):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                gate.wait()
+                for _ in range(4):
+                    C.queue_verify_blocks(bimg, b_o, b_l, b_ok, stream=s)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
     try:
         for attempt in range(6):  # until the four calls shared a batch (timing)
             buf.copy_(torch.from_numpy(before))
             torch.cuda.synchronize()
             qb = C.queue_stats()
-            gate = threading.Barrier(len(ns))
-            th = [threading.Thread(target=work, args=(k, gate)) for k in range(len(ns))]
+            gate = threading.Barrier(len(ns) + 1)
+            th = [threading.Thread(target=blocker, args=(gate,))]
+            th += [threading.Thread(target=work, args=(k, gate)) for k in range(len(ns))]
             for x in th:
                 x.start()
             for x in th:
                 x.join()
             qa = C.queue_stats()
-            assert qa["requests"] - qb["requests"] == len(ns)
-            if qa["batches"] - qb["batches"] < len(ns):
+            assert qa["requests"] - qb["requests"] == len(ns) + 4
+            if qa["batches"] - qb["batches"] < len(ns) + 4:
                 break
     finally:
         C.queue_set_slots(0)
         C.engine_set_enabled(-1)
     assert not errors, errors
-    assert qa["batches"] - qb["batches"] < len(ns), "the calls never shared a batch"
+    assert qa["batches"] - qb["batches"] < len(ns) + 4, "the calls never shared a batch"
     after = buf.cpu().numpy()
     expect = before.copy()
     for k, (o, ln, total) in enumerate(lays):

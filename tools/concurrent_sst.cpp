@@ -16,8 +16,9 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -o tools/bin/concurrent_sst
 //        tools/concurrent_sst.cpp -Lnovalsm_amd/lib -lnova_crc32c -Wl,-rpath,'$ORIGIN/../../novalsm_amd/lib' -lpthread
 // Run:   tools/bin/concurrent_sst <verify|trailers> <threads> <blocks per table> <seconds>
-//        [direct|queue|engine]   (nova_sst_queue_*: queue = the coalescing queue,
-//        engine = the persistent engine)
+//        [direct|queue|engine|engine_trace]   (nova_sst_queue_*: queue = the coalescing
+//        queue, engine = the persistent engine; engine_trace: with its
+//        per-request spans, nova_sst_engine_set_trace, printed as a second JSON line)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -78,11 +79,13 @@ int main(int argc, char** argv) {
   const int T = atoi(argv[2]);
   const size_t n = strtoull(argv[3], nullptr, 10);
   const double secs = atof(argv[4]);
-  const bool engine = argc > 5 && !strcmp(argv[5], "engine");
+  const bool trace = argc > 5 && !strcmp(argv[5], "engine_trace");
+  const bool engine = trace || (argc > 5 && !strcmp(argv[5], "engine"));
   const bool queue = engine || (argc > 5 && !strcmp(argv[5], "queue"));
   if (T < 1 || T > 64 || n < 1 || n > (1u << 20) || secs <= 0) return 2;
   CKN(nova_device_init());
   CKN(nova_sst_engine_set_enabled(engine ? 1 : 0));
+  CKN(nova_sst_engine_set_trace(trace ? 1 : 0));
 
   std::vector<Table> tabs(T);
   for (int t = 0; t < T; t++) {
@@ -184,13 +187,21 @@ int main(int argc, char** argv) {
   int erun = 0;
   CKN(nova_sst_queue_stats(&qb, &qr, &qmax));
   CKN(nova_sst_engine_stats(&er, &el, &ef, &erun));
+  uint64_t tn = 0;
+  double ts[5] = {0, 0, 0, 0, 0};
+  CKN(nova_sst_engine_trace_stats(&tn, ts));
+  if (trace)
+    printf("{\"trace_requests\": %llu, \"host_submit_to_done_us\": %.2f, \"gpu_dispatch_to_first_chunk_us\": %.2f, "
+           "\"gpu_first_to_last_chunk_us\": %.2f, \"gpu_dispatch_to_last_us\": %.2f, \"host_max_us\": %.1f}\n",
+           (unsigned long long)tn, ts[0], ts[1], ts[2], ts[3], ts[4]);
   printf("{\"op\": \"%s\", \"path\": \"%s\", \"queue_batches\": %llu, \"queue_requests\": %llu, "
          "\"queue_max_tables\": %llu, \"engine_requests\": %llu, \"engine_launches\": %llu, "
          "\"engine_fallbacks\": %llu, \"threads\": %d, \"blocks_per_table\": %zu, \"table_bytes\": %llu, "
          "\"calls\": %zu, \"calls_per_thread_min\": %zu, \"calls_per_thread_max\": %zu, "
          "\"wall_s\": %.3f, \"aggregate_GBps\": %.1f, \"frac_of_8TBps\": %.4f, "
          "\"p50_us\": %.1f, \"p99_us\": %.1f, \"max_us\": %.1f, \"verified\": %s}\n",
-         verify ? "verify" : "trailers", engine ? "engine" : queue ? "queue" : "direct", (unsigned long long)qb,
+         verify ? "verify" : "trailers", trace ? "engine_trace" : engine ? "engine" : queue ? "queue" : "direct",
+         (unsigned long long)qb,
          (unsigned long long)qr, (unsigned long long)qmax, (unsigned long long)er, (unsigned long long)el,
          (unsigned long long)ef, T, n, (unsigned long long)tabs[0].algo_bytes, all.size(),
          min_calls, max_calls, wall, bytes / wall / 1e9, bytes / wall / 8e12, pct(0.50), pct(0.99),

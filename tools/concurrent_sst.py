@@ -70,7 +70,9 @@ def main() -> int:
                     if r.returncode != 0 or not line:
                         print(r.stdout, r.stderr, file=sys.stderr)
                         return r.returncode or 1
-                    row = json.loads(line[0])
+                    row = json.loads(line[-1])
+                    for extra in line[:-1]:  # engine_trace: the spans
+                        row.update(json.loads(extra))
                     row["hw_queues"] = hwq if hwq is not None else env.get("GPU_MAX_HW_QUEUES", "default")
                     print(json.dumps(row), flush=True)
     return 0
