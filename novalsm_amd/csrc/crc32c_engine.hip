@@ -66,7 +66,7 @@ using namespace nova_dev;
 
 constexpr uint32_t kRing = 1024;  // requests in flight (host ring and device slots)
 constexpr int kEngG = 16;         // lanes per block (units kernel: G = 16)
-constexpr int kEngMaxWaves = 12;  // launch bound (the units kernel's: 168 VGPRs)
+constexpr int kEngMaxWaves = 8;   // launch bound: 256 VGPRs (18 swaths of a block in flight per group)
 constexpr uint32_t kXcds = 8;
 
 struct EngHostReq {  // a host ring entry (64 B), written by its submitter
@@ -155,13 +155,15 @@ __device__ __forceinline__ __attribute__((address_space(3))) uint32_t* lds32(uin
   return reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(a);
 }
 // Per workgroup: [the end word as last read][stop][poll lock], after the tables
-// and every wave's scratch.  One waiting wave per CU at a time reads the
+// (main image, tree levels, byte table).  One waiting wave per CU at a time reads the
 // device's end and stop words and copies them here; the others spin on
 // these LDS words -- 256 pollers of the end word's line instead of ~2800.
 template <int G>
-constexpr uint32_t poll_off() {
-  return kMainBytes + (2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16)) * kTreeBytes + kEngMaxWaves * kWaveScratch;
-}
+constexpr uint32_t tree_levels() { return 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16); }
+template <int G>
+constexpr uint32_t byte_tab_off() { return kMainBytes + tree_levels<G>() * kTreeBytes; }
+template <int G>
+constexpr uint32_t poll_off() { return byte_tab_off<G>() + 1024u; }
 
 // Wave 0 of workgroup 0: host ring -> device slots, tickets published.
 __device__ void engine_dispatch(const EngParams& e) {
@@ -255,9 +257,142 @@ __device__ void engine_dispatch(const EngParams& e) {
   }
 }
 
-// Every other wave: tickets -> chunks of the units kernel's body.
+// One chunk of a request: blocks [c * cb, (c + 1) * cb) of it, in rounds of
+// kGroups = 4 blocks, one per 16-lane group -- the burst kernel's shape
+// (crc32c_burst_kernel) on the rounds kernel's bank-replicated
+// M_256 tables:
+//   * a group issues ALL of its block's loads at once (up to kEK swaths of
+//     256 B: a 4 KiB SSTable block in one pass; longer blocks take more
+//     passes) with the tail line(s) -- the bytes [E, u1) and, for verify, the
+//     stored CRC -- so a round is one memory round trip, not one per step;
+//   * the wave's groups run the wave's largest swath count, each block's
+//     region end-aligned (shorter blocks start on zero pieces);
+//   * in-lane M4/M8 and cross-lane M16..M128 fold, then finish_block (tail
+//     bytes from LDS, the n < 4 init fix, the mode's epilogue);
+//   * the next round's descriptors are loaded before this round folds.
+// Every load of caller memory is non-temporal and every result store is
+// write-through (the engine outlives the caller's writes and reads).
+constexpr int kEK = 18;  // swaths per pass: 4.5 KiB (4096 + 255 + 5 B blocks: one pass)
+
+template <int MODE>
+__device__ __forceinline__ void engine_chunk(const uint8_t* lds, const CrcParams& p, uint64_t c) {
+  constexpr int G = kEngG;
+  constexpr uint64_t kS = 16ull * G;
+  constexpr uint32_t kGroups = 64 / G;
+  constexpr bool kTail2 = MODE == kVerify;
+  const int lane = threadIdx.x & 63;
+  const int q = lane & (G - 1);
+  const int grp = lane / G;
+  const uint32_t rep = (uint32_t)(lane & 31) << 2;
+  const uint32_t lo0 = rep, lo1 = rep | 128u, lo2 = rep | 0x10000u, lo3 = rep | 0x10080u;
+  const uint8_t* tree = lds + kMainBytes;  // level l: M_{4 * 2^l}
+  const bool raw = (p.flags & NOVA_CRC32C_RAW) != 0;
+  const uint32_t extra = MODE == kVerify ? 1u : 0u;  // verify covers block + type byte
+  const uint64_t zl = (uint64_t)p.zline;
+  const uint64_t base = (uint64_t)p.base;
+  const uint64_t b_lo = c * p.chunk;
+  const uint64_t b_hi = b_lo + p.chunk < p.n_blocks ? b_lo + p.chunk : p.n_blocks;
+  uint32_t nbad = 0;
+  // this round's descriptors (and, loaded during its fold, the next round's)
+  auto desc = [&](uint64_t b0, uint64_t& o, uint32_t& ln) {
+    const uint64_t b = b0 + grp;
+    const uint64_t bb = b < b_hi ? b : b_lo;  // clamped: valid memory, result unused
+    o = ld_nt<true>(p.offsets + bb);
+    ln = ld_nt<true>(p.lengths + bb);
+  };
+  uint64_t o_cur = 0, o_nxt = 0;
+  uint32_t l_cur = 0, l_nxt = 0;
+  desc(b_lo, o_cur, l_cur);
+  for (uint64_t b0 = b_lo; b0 < b_hi; b0 += kGroups) {
+    const uint64_t b = b0 + grp;
+    const bool valid = b < b_hi;
+    const uint64_t u0 = base + o_cur;
+    const uint32_t n = l_cur + extra;
+    const uint64_t u1 = u0 + n;
+    const uint64_t E = u1 & ~15ull;
+    const uint64_t A0 = u0 & ~15ull;
+    const uint32_t K = valid && E > A0 ? (uint32_t)((E - A0 + kS - 1) / kS) : 0u;
+    const uint32_t Kw = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max(K));
+    uint64_t first = E - (uint64_t)Kw * kS + 16ull * q;
+    FlatSet Y;
+    Y.u0 = u0;
+    Y.u1 = u1;
+    Y.rec = b;
+    Y.ninit = (raw || n < 4) ? 0u : ~0u;  // init 0 (table/format.cc, table_builder.cc)
+    Y.st = 0;
+    Y.valid = valid;
+    // tail line(s): [E, E+16) holds the tail bytes (verify: the start of the
+    // stored CRC), [E+16, E+32) the rest of a stored CRC
+    Y.t = gload16((valid && (kTail2 || (u1 & 15) != 0)) ? E : zl);
+    if constexpr (kTail2) Y.t2 = gload16(valid && u1 + 4 > E + 16 ? E + 16 : zl);
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    // 32-bit positions relative to the lane's first piece: the block's first
+    // byte (head masking) and its first line (pieces before it read zeros)
+    const int64_t ur = (int64_t)(u0 - first), ar = (int64_t)(A0 - first);
+    int32_t urel = ur < -(1 << 20) ? -(1 << 20) : (ur > (1 << 30) ? (1 << 30) : (int32_t)ur);
+    int32_t arel = ar < -(1 << 20) ? -(1 << 20) : (ar > (1 << 30) ? (1 << 30) : (int32_t)ar);
+    for (uint32_t k0 = 0; k0 < Kw; k0 += kEK) {
+      uint4 d[kEK];
+#pragma unroll
+      for (int i = 0; i < kEK; i++) {
+        const bool in = valid && k0 + i < Kw && (int32_t)(kS * i) >= arel;
+        d[i] = gload16(in ? first + (uint64_t)i * kS : zl);
+      }
+      if (k0 == 0 && b0 + kGroups < b_hi) desc(b0 + kGroups, o_nxt, l_nxt);  // under the data loads
+#pragma unroll
+      for (int i = 0; i < kEK; i++) {
+        if (k0 + i < Kw) {  // wave-uniform
+          const int32_t hr = urel - (int32_t)(kS * i);
+          const int32_t h = hr < -4 ? -4 : (hr > 32 ? 32 : hr);
+          const uint4 w = is_head(h) ? head_piece(d[i], h, Y.ninit) : d[i];
+          swath4<0>(lds, c0, c1, c2, c3, w, lo0, lo1, lo2, lo3);
+        }
+      }
+      first += (uint64_t)kEK * kS;  // the next pass
+      urel -= (int32_t)(kEK * kS);
+      arel -= (int32_t)(kEK * kS);
+    }
+    // fold the group's stream words: in-lane M4/M8, then M16 .. M128 across the group
+    uint32_t v = lapply(tree + kTreeBytes, lapply(tree, c0) ^ c1) ^ (lapply(tree, c2) ^ c3);
+    auto level = [&](int k, uint32_t o) {  // o: v of lane q ^ 2^k
+      const bool right = (q >> k) & 1;
+      v = lapply(tree + (2 + k) * kTreeBytes, right ? o : v) ^ (right ? v : o);
+    };
+    level(0, lane_xor<1>(v));
+    level(1, lane_xor<2>(v));
+    level(2, lane_xor<4>(v));
+    level(3, lane_xor<8>(v));
+    uint64_t wb_a = 0;
+    uint32_t wb_v = 0;
+    finish_block<MODE, kMainBytes>(lds, byte_tab_off<G>(), p, raw, v, Y, wb_a, wb_v);
+    if (q == 0 && valid) {
+      if constexpr (MODE == kVerify) {
+        st_through((uint8_t*)wb_a, (uint8_t)wb_v);
+        nbad += wb_v ? 0u : 1u;
+      } else if constexpr (MODE == kTrailer) {
+        store_trailer_through((uint8_t*)wb_a, (p.flags >> 8) & 0xffu, wb_v, (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
+      } else {
+        st_through((uint32_t*)wb_a, wb_v);
+      }
+    }
+    o_cur = o_nxt;
+    l_cur = l_nxt;
+  }
+  if constexpr (MODE == kVerify) {  // one add per chunk, performed in memory (system scope)
+    const uint32_t nb = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(__builtin_popcountll(__builtin_amdgcn_ballot_w64(nbad & 1)) +
+              2 * __builtin_popcountll(__builtin_amdgcn_ballot_w64((nbad >> 1) & 1)) +
+              4 * __builtin_popcountll(__builtin_amdgcn_ballot_w64((nbad >> 2) & 1)) +
+              8 * __builtin_popcountll(__builtin_amdgcn_ballot_w64((nbad >> 3) & 1)) +
+              16 * __builtin_popcountll(__builtin_amdgcn_ballot_w64((nbad >> 4) & 1))));
+    if (lane == 0 && nb && p.n_bad)
+      __hip_atomic_fetch_add((g32*)p.n_bad, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Every other wave: tickets -> chunks (engine_chunk).
 template <int G>
-__device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wpre) {
+__device__ void engine_work(const EngParams& e, const uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   EngDev* d = e.dev;
   const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & (kXcds - 1);
@@ -379,12 +514,12 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wp
     if (mode == kVerify) {
       p.ok_out = (uint8_t*)uni64(out);
       p.n_bad = (uint32_t*)uni64(bad);
-      units_chunk<G, kVerify, kVarEngine>(lds, p, c, wpre);
+      engine_chunk<kVerify>(lds, p, c);
     } else if (mode == kTrailer) {
-      units_chunk<G, kTrailer, kVarEngine>(lds, p, c, wpre);
+      engine_chunk<kTrailer>(lds, p, c);
     } else {
       p.out = (uint32_t*)uni64(out);
-      units_chunk<G, kStore, kVarEngine>(lds, p, c, wpre);
+      engine_chunk<kStore>(lds, p, c);
     }
     // publish the chunk: its results were stored write-through (st_through);
     // once drained they are in memory, so the count needs no release fence
@@ -414,8 +549,7 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds, uint32_t* wp
 template <int G>
 __global__ void __launch_bounds__(kEngMaxWaves * 64) crc32c_engine_kernel(EngParams e) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int kLevels = 2 + (G >= 2) + (G >= 4) + (G >= 8) + (G >= 16);
-  lds_fill_tables(lds, e.tab.tab_main, e.tab.tab_tree, kLevels * kTreeBytes / 16, nullptr, 0);
+  lds_fill_tables(lds, e.tab.tab_main, e.tab.tab_tree, tree_levels<G>() * kTreeBytes / 16, e.tab.tab_byte, 64);
   if (threadIdx.x == 0) {  // the workgroup's copy of the end / stop words, and the poll lock
     *lds64(poll_off<G>()) = 0;
     *lds32(poll_off<G>() + 8) = 0;
@@ -427,8 +561,7 @@ __global__ void __launch_bounds__(kEngMaxWaves * 64) crc32c_engine_kernel(EngPar
     engine_dispatch(e);
     return;
   }
-  uint32_t* wpre = reinterpret_cast<uint32_t*>(lds + kMainBytes + kLevels * kTreeBytes + wave * kWaveScratch);
-  engine_work<G>(e, lds, wpre);
+  engine_work<G>(e, lds);
 }
 
 template <int G>
@@ -536,8 +669,8 @@ struct Engine {
     p.tab.tab_tree = t->tree;
     p.tab.tab_ft = t->ft;
     p.tab.tab_sh16 = t->sh16;
+    p.tab.tab_byte = t->byte8;  // M_1 byte table (tail bytes)
     p.tab.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
-    p.tab.seg = 0;  // whole blocks are units
     hipLaunchKernelGGL((crc32c_engine_kernel<kEngG>), dim3((uint32_t)cus), dim3(64 * waves),
                        engine_lds<kEngG>((int)waves), stream, p);
     e = hipGetLastError();
