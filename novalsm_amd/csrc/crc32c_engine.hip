@@ -50,6 +50,7 @@
 //     word (system scope).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -66,8 +67,17 @@ using namespace nova_dev;
 
 constexpr uint32_t kRing = 1024;  // requests in flight (host ring and device slots)
 constexpr int kEngG = 16;         // lanes per block (units kernel: G = 16)
-constexpr int kEngMaxWaves = 8;   // launch bound: 256 VGPRs (18 swaths of a block in flight per group)
-constexpr uint32_t kXcds = 8;
+// Launch bound: 8 waves per CU (182 VGPRs).  A 12-wave build (168 VGPRs)
+// spilled and measured 5-20 % slower (profiles/r04_engine_conc_v4.log).
+constexpr int kEngMaxWaves = 8;
+constexpr int kEngWaves = 8;
+constexpr uint32_t kCntGroups = 8;
+// Ticket pages: page[p] = the request holding ticket kPage * p (a hint: checked
+// against the slot's ticket range), so a wave finds its ticket's request in
+// one or two round trips instead of walking its cursor forward one slot per
+// round trip (an idle wave's cursor lags by every request it sat out).
+constexpr uint32_t kPageShift = 4;
+constexpr uint32_t kPages = 1u << 14;  // 256K tickets covered (wraps: hints only)
 
 struct EngHostReq {  // a host ring entry (64 B), written by its submitter
   uint64_t base, offs, sizes, out, bad, n;
@@ -100,10 +110,17 @@ struct EngDev {  // device memory, zeroed before every launch
   uint32_t p1[31];
   uint64_t reqs_done;
   uint64_t p2[15];
-  uint32_t head[kXcds][32];  // per-XCD ticket heads, one 128-B line each
-  uint32_t cdone[kRing];     // chunks finished, per slot
+  // Chunks finished, per slot: one counter per ticket group t % 8 (1/8 of the
+  // request's adds per address), then a top counter of the groups whose
+  // chunks are all done.  Same-address atomics
+  // serialize in memory; one counter for all of a 1024-chunk request put
+  // ~1024 of them on the request's critical path.
+  uint32_t head[kCntGroups][32];  // per-XCD ticket heads, one 128-B line each
+  uint32_t cgrp[kRing][kCntGroups][32];  // 128-B line each
+  uint32_t ctop[kRing][32];
   EngSlot slot[kRing];
   uint64_t tr[kRing][4];     // trace: dispatched, first chunk started, last chunk done (s_memrealtime)
+  uint64_t page[kPages];     // ticket page -> request seq + 1 (hint)
 };
 struct EngParams {
   const EngHostReq* hring;
@@ -204,7 +221,9 @@ __device__ void engine_dispatch(const EngParams& e) {
       if ((uint32_t)lane < m) {
         const uint64_t seq = seen + lane;
         EngSlot* S = &d->slot[seq % kRing];
-        st_agent(&d->cdone[seq % kRing], 0u);  // the slot's previous request (seq - kRing) is done
+        // the slot's previous request (seq - kRing) is done: its counters are free
+        for (uint32_t x = 0; x < kCntGroups; x++) st_agent(&d->cgrp[seq % kRing][x][0], 0u);
+        st_agent(&d->ctop[seq % kRing][0], 0u);
         st_agent(&S->cstart, cend + inc - nch);
         st_agent(&S->cend, cend + inc);
         st_agent(&S->base, r.base);
@@ -218,14 +237,25 @@ __device__ void engine_dispatch(const EngParams& e) {
         st_agent(&S->cb, r.cb);
         if (e.htrace) {
           st_agent(&d->tr[seq % kRing][0], now_ticks());
-          st_agent(&d->tr[seq % kRing][1], ~(uint64_t)0);
+          st_agent(&d->tr[seq % kRing][1], (uint64_t)0);
           st_agent(&d->tr[seq % kRing][2], (uint64_t)0);
         }
         st_agent(&S->seq1, seq + 1);
       }
       const uint64_t total = uni64(((uint64_t)(uint32_t)__shfl((int)(uint32_t)(inc >> 32), 63) << 32) |
                                    (uint32_t)__shfl((int)(uint32_t)inc, 63));
-      drain_vm();  // every lane's slot stores are written through before the end moves
+      // ticket pages: every page whose first ticket a request holds names it
+      // (the wave's 64 lanes write one request's pages at a time)
+      for (uint32_t k = 0; k < m; k++) {
+        const uint64_t cs = cend + uni64(((uint64_t)(uint32_t)__shfl((int)(uint32_t)((inc - nch) >> 32), (int)k) << 32) |
+                                         (uint32_t)__shfl((int)(uint32_t)(inc - nch), (int)k));
+        const uint64_t ce = cend + uni64(((uint64_t)(uint32_t)__shfl((int)(uint32_t)(inc >> 32), (int)k) << 32) |
+                                         (uint32_t)__shfl((int)(uint32_t)inc, (int)k));
+        const uint64_t p0 = (cs + (1u << kPageShift) - 1) >> kPageShift, p1 = (ce + (1u << kPageShift) - 1) >> kPageShift;
+        const uint64_t np = p1 - p0 < kPages ? p1 - p0 : kPages;
+        for (uint64_t j = lane; j < np; j += 64) st_agent(&d->page[(p0 + j) & (kPages - 1)], seen + k + 1);
+      }
+      drain_vm();  // every lane's slot and page stores are written through before the end moves
       cend += total;
       if (lane == 0) st_agent(&d->dend, cend);
       seen += m;
@@ -395,12 +425,16 @@ template <int G>
 __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   EngDev* d = e.dev;
-  const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & (kXcds - 1);
+  // Tickets t with t % 8 == x go to XCD x's waves, each taking the next from
+  // its XCD's head (dynamic: a request's chunks go to whichever waves are
+  // free; one queue per CU instead made every request wait for the slowest
+  // of 256 queues -- 35 % less at 16 callers).
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & (kCntGroups - 1);
   auto claim = [&]() -> uint64_t {
     uint32_t k = 0;
     if (lane == 0)
       k = __hip_atomic_fetch_add((g32*)&d->head[xcc][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return xcc + (uint64_t)kXcds * uni32(k);
+    return xcc + (uint64_t)kCntGroups * uni32(k);
   };
   uint64_t r = e.first_seq;  // request cursor (the wave's tickets only grow)
   uint64_t dend = 0;
@@ -462,14 +496,18 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
     // r + kRing only after request r is done, and a live request's seq is
     // above (newest written seq) - kRing, so a slot found holding a newer
     // seq s1 - 1 moves the cursor to s1 - kRing (still at or below it).
-    // All of a slot's fields are read at once (one round trip); a slot that
-    // turns out not to hold ticket t is passed over and the next one read.
+    // All of a slot's fields are read at once (one round trip), together with
+    // t's ticket page; when the cursor's slot does not hold t the page's
+    // request is tried next, then slots are walked forward one at a time.
     uint64_t cstart = 0, cend = 0, base = 0, offs = 0, sizes = 0, out = 0, bad = 0, n = 0;
     uint32_t mode = 0, flags = 0, cb = 0;
+    bool hinted = false;
+    const uint64_t r0 = r;  // the cursor is never past t's request; a hint may be (it wraps)
     for (;;) {
       const EngSlot* S = &d->slot[r % kRing];
-      uint64_t s1 = 0;
+      uint64_t s1 = 0, hint = 0;
       if (lane == 0) {
+        if (!hinted) hint = ld_agent(&d->page[(t >> kPageShift) & (kPages - 1)]);
         s1 = ld_agent(&S->seq1);
         cstart = ld_agent(&S->cstart);
         cend = ld_agent(&S->cend);
@@ -485,12 +523,26 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
       }
       s1 = uni64(s1);
       const uint64_t ce = uni64(cend);
+      if (!hinted) {
+        // the page of t names the request holding its first ticket: t's request
+        // or an earlier one (pages hold hints, checked below like the cursor)
+        hinted = true;
+        hint = uni64(hint);
+        if (!(s1 == r + 1 && t >= uni64(cstart) && t < ce) && hint > r + 1) {
+          r = hint - 1;
+          continue;
+        }
+      }
       if (s1 > r + 1) {
         r = s1 - kRing > r + 1 ? s1 - kRing : r + 1;
         continue;
       }
       if (s1 == r + 1 && t >= ce) {
         r++;
+        continue;
+      }
+      if (s1 == r + 1 && t < uni64(cstart)) {  // a stale (wrapped) hint overshot: walk from the cursor
+        r = r0;
         continue;
       }
       if (s1 == r + 1) break;
@@ -507,10 +559,8 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
     p.flags = uni32(flags);
     p.chunk = uni32(cb);
     mode = uni32(mode);
-    const uint64_t nt = claim();  // the next ticket, in flight during this chunk
     const uint64_t c = t - cstart;
-    if (e.htrace && lane == 0)
-      __hip_atomic_fetch_min((g64*)&d->tr[r % kRing][1], now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e.htrace && lane == 0 && c == 0) st_agent(&d->tr[r % kRing][1], now_ticks());  // request's first chunk
     if (mode == kVerify) {
       p.ok_out = (uint8_t*)uni64(out);
       p.n_bad = (uint32_t*)uni64(bad);
@@ -525,16 +575,21 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
     // once drained they are in memory, so the count needs no release fence
     drain_vm();
     if (lane == 0) {
-      if (e.htrace) {
-        __hip_atomic_fetch_max((g64*)&d->tr[r % kRing][2], now_ticks(), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        drain_vm();
-      }
-      const uint32_t prev = __hip_atomic_fetch_add((g32*)&d->cdone[r % kRing], 1u, __ATOMIC_RELAXED,
+      // the request's tickets are counted per XCD (t % 8), one line each;
+      // this XCD's share: t' in [cstart, cend), t' % 8 == grp
+      const uint32_t grp = xcc;
+      auto below = [&](uint64_t n) -> uint64_t { return n > grp ? (n - grp + kCntGroups - 1) / kCntGroups : 0; };
+      const uint64_t mine = below(cend) - below(cstart);
+      const uint64_t groups = cend - cstart < kCntGroups ? cend - cstart : kCntGroups;
+      const uint32_t prev = __hip_atomic_fetch_add((g32*)&d->cgrp[r % kRing][grp][0], 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
-      if ((uint64_t)prev + 1 == cend - cstart) {  // the request's last chunk: every other
-        // chunk's wave drained its results before its add, this one before its own
+      if ((uint64_t)prev + 1 == mine &&
+          (uint64_t)__hip_atomic_fetch_add((g32*)&d->ctop[r % kRing][0], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) + 1 == groups) {
+        // the request's last chunk: every other chunk's wave drained its
+        // results before its add, this one before its own
         if (e.htrace) {
+          st_agent(&d->tr[r % kRing][2], now_ticks());
           for (int k = 0; k < 3; k++) st_sys(&e.htrace[(r % kRing) * 4 + k], ld_agent(&d->tr[r % kRing][k]));
           drain_vm();
         }
@@ -542,12 +597,15 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
         __hip_atomic_fetch_add((g64*)&d->reqs_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    t = nt;
+    // the next ticket: claimed after this chunk is counted (the claim's add
+    // is contended; issued before the chunk, every load of the chunk waited
+    // for it: in-order vmcnt)
+    t = claim();
   }
 }
 
-template <int G>
-__global__ void __launch_bounds__(kEngMaxWaves * 64) crc32c_engine_kernel(EngParams e) {
+template <int G, int W>
+__global__ void __launch_bounds__(W * 64) crc32c_engine_kernel(EngParams e) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   lds_fill_tables(lds, e.tab.tab_main, e.tab.tab_tree, tree_levels<G>() * kTreeBytes / 16, e.tab.tab_byte, 64);
   if (threadIdx.x == 0) {  // the workgroup's copy of the end / stop words, and the poll lock
@@ -592,7 +650,8 @@ struct Engine {
   uint64_t next_seq = 0;     // the next request's seq
   uint64_t inst_first = 0;   // the running instance's first seq
   uint64_t gen = 0;          // instances launched
-  std::atomic<uint64_t> inflight{0};
+  std::atomic<uint64_t> inflight{0};         // requests submitted and not yet returned
+  std::atomic<uint64_t> inflight_blocks{0};  // their blocks
   uint64_t requests = 0, relaunches = 0, fallbacks = 0;
   uint32_t idle_us = 0, waves = 0;
   // trace (nova_sst_engine_set_trace): per-request spans, summed under tmu
@@ -620,8 +679,9 @@ struct Engine {
       e = hipHostMalloc((void**)&htrace, sizeof(uint64_t) * 4 * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess) e = hipMalloc((void**)&ddev, sizeof(EngDev));
     if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG>),
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG, kEngMaxWaves>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)engine_lds<kEngG>(kEngMaxWaves));
+
     if (e != hipSuccess) {
       (void)hipGetLastError();
       broken = true;
@@ -631,8 +691,8 @@ struct Engine {
     memset(hdone, 0, sizeof(uint64_t) * kRing);
     memset(ctl, 0, sizeof(EngCtl));
     if (!idle_us) idle_us = (uint32_t)env_u64("NOVA_SST_ENGINE_IDLE_US", 1000);
-    waves = (uint32_t)env_u64("NOVA_SST_ENGINE_WAVES", kEngMaxWaves);
-    if (waves < 2 || waves > (uint32_t)kEngMaxWaves) waves = kEngMaxWaves;
+    waves = (uint32_t)env_u64("NOVA_SST_ENGINE_WAVES", kEngWaves);
+    if (waves < 2 || waves > (uint32_t)kEngMaxWaves) waves = kEngWaves;
     ready = true;
     return 0;
   }
@@ -671,7 +731,7 @@ struct Engine {
     p.tab.tab_sh16 = t->sh16;
     p.tab.tab_byte = t->byte8;  // M_1 byte table (tail bytes)
     p.tab.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
-    hipLaunchKernelGGL((crc32c_engine_kernel<kEngG>), dim3((uint32_t)cus), dim3(64 * waves),
+    hipLaunchKernelGGL((crc32c_engine_kernel<kEngG, kEngMaxWaves>), dim3((uint32_t)cus), dim3(64 * waves),
                        engine_lds<kEngG>((int)waves), stream, p);
     e = hipGetLastError();
     if (e != hipSuccess) {
@@ -698,7 +758,7 @@ struct Engine {
   bool ring_slot_free(uint64_t seq) const {
     if (seq < kRing) return true;
     const volatile uint64_t* h = hdone;
-    return h[seq % kRing] == seq - kRing + 1;
+    return h[seq % kRing] >= seq - kRing + 1;  // monotone per slot
   }
 };
 
@@ -758,6 +818,8 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   if (!gp) return err;
   Engine& g = *gp;
   static const uint64_t timeout_ms = env_u64("NOVA_SST_ENGINE_TIMEOUT_MS", 10000);
+  // blocks per chunk fixed at 1..16 (0: adaptive, below)
+  static const uint32_t cb_fixed = (uint32_t)std::min<uint64_t>(16, env_u64("NOVA_SST_ENGINE_CB", 0));
   uint64_t seq = 0;
   {
     std::unique_lock<std::mutex> lk(g.mu);
@@ -775,7 +837,8 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
     g.next_seq = seq + 1;
     // blocks per chunk: one round per wave when the request is alone (latency),
     // four rounds when others are in flight (fewer tickets, longer streams)
-    const uint64_t others = g.inflight.fetch_add(1);
+    g.inflight.fetch_add(1);
+    const uint64_t blocks = g.inflight_blocks.fetch_add(n) + n;
     EngHostReq r{};
     r.base = (uint64_t)base;
     r.offs = (uint64_t)offs;
@@ -785,7 +848,10 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
     r.n = n;
     r.mode = (uint32_t)mode;
     r.flags = flags;
-    r.cb = others ? 16u : (uint32_t)(64 / kEngG);
+    // blocks per chunk: 4 (one round of the chunk body) per 16K blocks in
+    // flight -- short chunks (latency) when the engine is quiet, longer ones
+    // (fewer tickets per block) when it is busy (tools/concurrent_sst.py sweep)
+    r.cb = cb_fixed ? cb_fixed : (uint32_t)std::min<uint64_t>(16, 4 * ((blocks + 16383) / 16384));
     volatile EngHostReq* h = g.ring + seq % kRing;
     h->base = r.base;
     h->offs = r.offs;
@@ -802,6 +868,7 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
     g.requests++;
     if ((err = g.relaunch_if_exited_locked())) {
       g.inflight.fetch_sub(1);
+      g.inflight_blocks.fetch_sub(n);
       return err;
     }
   }
@@ -811,19 +878,24 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   const volatile uint64_t* hd = g.hdone + seq % kRing;
   const volatile EngCtl* c = g.ctl;
   const auto t0 = std::chrono::steady_clock::now();
+  // The word only grows (seq + 1, then seq + 1 + kRing once this request is
+  // done and its ring slot reused), so a waiter descheduled past a full ring
+  // turn still sees its request done.
   for (uint64_t spin = 0;; spin++) {
-    if (*hd == seq + 1) break;
+    if (*hd >= seq + 1) break;
     if ((spin & 255) == 255) {
       if (c->error) {
         std::lock_guard<std::mutex> lk(g.mu);
         g.broken = true;
         g.inflight.fetch_sub(1);
+        g.inflight_blocks.fetch_sub(n);
         return NOVA_E_NODEV;
       }
       if (c->exited) {
         std::lock_guard<std::mutex> lk(g.mu);
-        if (*hd != seq + 1 && (err = g.relaunch_if_exited_locked())) {
+        if (*hd < seq + 1 && (err = g.relaunch_if_exited_locked())) {
           g.inflight.fetch_sub(1);
+          g.inflight_blocks.fetch_sub(n);
           return err;
         }
       }
@@ -831,6 +903,7 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
         std::lock_guard<std::mutex> lk(g.mu);
         g.broken = true;  // later requests take the plain path
         g.inflight.fetch_sub(1);
+        g.inflight_blocks.fetch_sub(n);
         return NOVA_E_NODEV;
       }
       if (spin > (1u << 16)) std::this_thread::yield();
@@ -839,6 +912,7 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   }
   std::atomic_thread_fence(std::memory_order_acquire);
   g.inflight.fetch_sub(1);
+  g.inflight_blocks.fetch_sub(n);
   if (g.trace) {  // this request's spans (the stamps were stored before its completion word)
     const double host_us =
         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_submit).count();
