@@ -195,6 +195,13 @@ int nova_sst_engine_set_enabled(int on);
  * clock)], then the largest host span. */
 int nova_sst_engine_set_trace(int on);
 int nova_sst_engine_trace_stats(uint64_t* n, double* out5);
+/* Where a traced request's GPU time goes: requests with every stamp, and the
+ * average us after its dispatch at which chunk 0's wave saw its ticket, found
+ * the slot, finished the blocks, drained the stores, counted the chunk; then
+ * when the last chunk was done; then the same five for the last chunk's wave
+ * (out11 = [slot0, last_done, seen0, body0, drain0, count0, seenL, slotL,
+ * bodyL, drainL, countL]). */
+int nova_sst_engine_trace_detail(uint64_t* n, double* out11);
 
 /* ---- MANIFEST / write-ahead log records ----------
  * buf holds buf_len bytes of a log file image starting at a 32 KiB log-block

@@ -69,6 +69,7 @@ _SIG = {
     "nova_sst_engine_set_enabled": (_i32, [ctypes.c_int]),
     "nova_sst_engine_set_trace": (_i32, [ctypes.c_int]),
     "nova_sst_engine_trace_stats": (_i32, [_vp, _vp]),
+    "nova_sst_engine_trace_detail": (_i32, [_vp, _vp]),
     "nova_crc32c_stream_host": (_i32, [_vp, _u64, _u32, _sz, _vp, _u32, _sz, _i32]),
     "nova_crc32c_batch_host": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _sz, _i32]),
     "nova_sstable_write_trailers_host": (_i32, [_vp, _vp, _vp, _sz, _u32, _sz, _i32]),

@@ -72,6 +72,7 @@ constexpr int kEngG = 16;         // lanes per block (units kernel: G = 16)
 constexpr int kEngMaxWaves = 8;
 constexpr int kEngWaves = 8;
 constexpr uint32_t kCntGroups = 8;
+constexpr uint32_t kTrWords = 16;
 // Ticket pages: page[p] = the request holding ticket kPage * p (a hint: checked
 // against the slot's ticket range), so a wave finds its ticket's request in
 // one or two round trips instead of walking its cursor forward one slot per
@@ -119,7 +120,10 @@ struct EngDev {  // device memory, zeroed before every launch
   uint32_t cgrp[kRing][kCntGroups][32];  // 128-B line each
   uint32_t ctop[kRing][32];
   EngSlot slot[kRing];
-  uint64_t tr[kRing][4];     // trace: dispatched, first chunk started, last chunk done (s_memrealtime)
+  // trace (s_memrealtime): 0 dispatched, 2 last chunk done; chunk 0's wave:
+  // 3 ticket seen, 1 slot found, 4 body done, 5 drained, 6 counted; the last
+  // chunk's wave: 7 ticket seen, 8 slot found, 9 body done, 10 drained, 11 counted
+  uint64_t tr[kRing][kTrWords];
   uint64_t page[kPages];     // ticket page -> request seq + 1 (hint)
 };
 struct EngParams {
@@ -237,8 +241,7 @@ __device__ void engine_dispatch(const EngParams& e) {
         st_agent(&S->cb, r.cb);
         if (e.htrace) {
           st_agent(&d->tr[seq % kRing][0], now_ticks());
-          st_agent(&d->tr[seq % kRing][1], (uint64_t)0);
-          st_agent(&d->tr[seq % kRing][2], (uint64_t)0);
+          for (uint32_t k = 1; k < 12; k++) st_agent(&d->tr[seq % kRing][k], (uint64_t)0);
         }
         st_agent(&S->seq1, seq + 1);
       }
@@ -492,6 +495,7 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
           __builtin_amdgcn_s_sleep(6);
       }
     }
+    const uint64_t ts_seen = e.htrace ? now_ticks() : 0;
     // The request holding ticket t.  Slot r % kRing is reused for seq
     // r + kRing only after request r is done, and a live request's seq is
     // above (newest written seq) - kRing, so a slot found holding a newer
@@ -560,7 +564,7 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
     p.chunk = uni32(cb);
     mode = uni32(mode);
     const uint64_t c = t - cstart;
-    if (e.htrace && lane == 0 && c == 0) st_agent(&d->tr[r % kRing][1], now_ticks());  // request's first chunk
+    const uint64_t ts_slot = e.htrace ? now_ticks() : 0;
     if (mode == kVerify) {
       p.ok_out = (uint8_t*)uni64(out);
       p.n_bad = (uint32_t*)uni64(bad);
@@ -573,7 +577,9 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
     }
     // publish the chunk: its results were stored write-through (st_through);
     // once drained they are in memory, so the count needs no release fence
+    const uint64_t ts_body = e.htrace ? now_ticks() : 0;
     drain_vm();
+    const uint64_t ts_drain = e.htrace ? now_ticks() : 0;
     if (lane == 0) {
       // the request's tickets are counted per XCD (t % 8), one line each;
       // this XCD's share: t' in [cstart, cend), t' % 8 == grp
@@ -583,14 +589,30 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
       const uint64_t groups = cend - cstart < kCntGroups ? cend - cstart : kCntGroups;
       const uint32_t prev = __hip_atomic_fetch_add((g32*)&d->cgrp[r % kRing][grp][0], 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t ts_count = e.htrace ? now_ticks() : 0;
+      if (e.htrace && c == 0) {
+        uint64_t* w = d->tr[r % kRing];
+        st_agent(&w[3], ts_seen);
+        st_agent(&w[1], ts_slot);
+        st_agent(&w[4], ts_body);
+        st_agent(&w[5], ts_drain);
+        st_agent(&w[6], ts_count);
+      }
       if ((uint64_t)prev + 1 == mine &&
           (uint64_t)__hip_atomic_fetch_add((g32*)&d->ctop[r % kRing][0], 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT) + 1 == groups) {
         // the request's last chunk: every other chunk's wave drained its
         // results before its add, this one before its own
         if (e.htrace) {
-          st_agent(&d->tr[r % kRing][2], now_ticks());
-          for (int k = 0; k < 3; k++) st_sys(&e.htrace[(r % kRing) * 4 + k], ld_agent(&d->tr[r % kRing][k]));
+          uint64_t* w = d->tr[r % kRing];
+          st_agent(&w[2], now_ticks());
+          st_agent(&w[7], ts_seen);
+          st_agent(&w[8], ts_slot);
+          st_agent(&w[9], ts_body);
+          st_agent(&w[10], ts_drain);
+          st_agent(&w[11], ts_count);
+          drain_vm();
+          for (uint32_t k = 0; k < 12; k++) st_sys(&e.htrace[(r % kRing) * kTrWords + k], ld_agent(&w[k]));
           drain_vm();
         }
         st_sys(&e.hdone[r % kRing], r + 1);
@@ -655,11 +677,13 @@ struct Engine {
   uint64_t requests = 0, relaunches = 0, fallbacks = 0;
   uint32_t idle_us = 0, waves = 0;
   // trace (nova_sst_engine_set_trace): per-request spans, summed under tmu
-  uint64_t* htrace = nullptr;  // pinned, kRing x 4
+  uint64_t* htrace = nullptr;  // pinned, kRing x kTrWords
   bool trace = false;
   std::mutex tmu;
   uint64_t tr_n = 0;
   double tr_host_us = 0, tr_wait_us = 0, tr_run_us = 0, tr_gpu_us = 0, tr_host_max = 0;
+  uint64_t tr_dn = 0;
+  double tr_detail[11] = {};  // words 1..11 - word 0, summed (us)
 
   int init_locked(int d) {
     if (ready) return 0;
@@ -676,7 +700,7 @@ struct Engine {
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&ctl, sizeof(EngCtl), hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
-      e = hipHostMalloc((void**)&htrace, sizeof(uint64_t) * 4 * kRing, hipHostMallocCoherent | hipHostMallocMapped);
+      e = hipHostMalloc((void**)&htrace, sizeof(uint64_t) * kTrWords * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess) e = hipMalloc((void**)&ddev, sizeof(EngDev));
     if (e == hipSuccess)
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG, kEngMaxWaves>),
@@ -916,8 +940,14 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   if (g.trace) {  // this request's spans (the stamps were stored before its completion word)
     const double host_us =
         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_submit).count();
-    const volatile uint64_t* tr = g.htrace + (seq % kRing) * 4;
+    const volatile uint64_t* tr = g.htrace + (seq % kRing) * kTrWords;
     const uint64_t t0 = tr[0], t1 = tr[1], t2 = tr[2];
+    uint64_t w[12];
+    bool all = true;
+    for (int k = 0; k < 12; k++) {
+      w[k] = tr[k];
+      all = all && w[k] >= t0 && w[k] - t0 < 100000000ull;  // stamped, within a second
+    }
     std::lock_guard<std::mutex> lk(g.tmu);
     g.tr_n++;
     g.tr_host_us += host_us;
@@ -926,6 +956,10 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
       g.tr_wait_us += (double)(t1 - t0) / 100.0;
       g.tr_run_us += (double)(t2 - t1) / 100.0;
       g.tr_gpu_us += (double)(t2 - t0) / 100.0;
+    }
+    if (all) {
+      g.tr_dn++;
+      for (int k = 1; k < 12; k++) g.tr_detail[k - 1] += (double)(w[k] - t0) / 100.0;
     }
   }
   return 0;
@@ -991,6 +1025,20 @@ int nova_sst_engine_set_trace(int on) {
   std::lock_guard<std::mutex> lt(gp->tmu);
   gp->tr_n = 0;
   gp->tr_host_us = gp->tr_wait_us = gp->tr_run_us = gp->tr_gpu_us = gp->tr_host_max = 0;
+  gp->tr_dn = 0;
+  for (double& x : gp->tr_detail) x = 0;
+  return 0;
+}
+
+int nova_sst_engine_trace_detail(uint64_t* n, double* out11) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<std::mutex> lt(gp->tmu);
+  const double k = gp->tr_dn ? 1.0 / (double)gp->tr_dn : 0.0;
+  if (n) *n = gp->tr_dn;
+  if (out11)
+    for (int i = 0; i < 11; i++) out11[i] = gp->tr_detail[i] * k;
   return 0;
 }
 

@@ -190,10 +190,17 @@ int main(int argc, char** argv) {
   uint64_t tn = 0;
   double ts[5] = {0, 0, 0, 0, 0};
   CKN(nova_sst_engine_trace_stats(&tn, ts));
+  uint64_t dn = 0;
+  double td[11] = {};
+  CKN(nova_sst_engine_trace_detail(&dn, td));
   if (trace)
     printf("{\"trace_requests\": %llu, \"host_submit_to_done_us\": %.2f, \"gpu_dispatch_to_first_chunk_us\": %.2f, "
-           "\"gpu_first_to_last_chunk_us\": %.2f, \"gpu_dispatch_to_last_us\": %.2f, \"host_max_us\": %.1f}\n",
-           (unsigned long long)tn, ts[0], ts[1], ts[2], ts[3], ts[4]);
+           "\"gpu_first_to_last_chunk_us\": %.2f, \"gpu_dispatch_to_last_us\": %.2f, \"host_max_us\": %.1f, "
+           "\"detail_requests\": %llu, \"chunk0_us\": {\"seen\": %.2f, \"slot\": %.2f, \"body\": %.2f, "
+           "\"drained\": %.2f, \"counted\": %.2f}, \"last_us\": {\"seen\": %.2f, \"slot\": %.2f, "
+           "\"body\": %.2f, \"drained\": %.2f, \"counted\": %.2f, \"done\": %.2f}}\n",
+           (unsigned long long)tn, ts[0], ts[1], ts[2], ts[3], ts[4], (unsigned long long)dn, td[2], td[0], td[3],
+           td[4], td[5], td[6], td[7], td[8], td[9], td[10], td[1]);
   printf("{\"op\": \"%s\", \"path\": \"%s\", \"queue_batches\": %llu, \"queue_requests\": %llu, "
          "\"queue_max_tables\": %llu, \"engine_requests\": %llu, \"engine_launches\": %llu, "
          "\"engine_fallbacks\": %llu, \"threads\": %d, \"blocks_per_table\": %zu, \"table_bytes\": %llu, "
