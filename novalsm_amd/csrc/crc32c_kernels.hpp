@@ -1516,11 +1516,22 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
       const uint64_t s64 = (Le - (n_u0 & ~(kL - 1))) / kL;
       S = s64 == 0 ? 1u : (s64 > 0xffffffffull ? 0xffffffffu : (uint32_t)s64);
     }
-    uint32_t rank = 0;
-    for (int j = 0; j < 64; j++) {
-      // lane j's key as a wave-uniform scalar (v_readlane: no LDS round trip)
-      const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)S, j);
-      rank += (sj > S || (sj == S && j < lane)) ? 1u : 0u;
+    // Rank by bucket, largest first: key = lines above the chunk's shortest
+    // slot, clamped to kBk - 1 (exact for the spreads that matter: SSTable
+    // blocks differ by 1-2 lines, short log records span < 16 lines at G = 4).
+    // One ballot + mbcnt per bucket instead of a 64-iteration readlane
+    // compare loop (~300 VALU per chunk; 4-5 per log record).
+    constexpr uint32_t kBk = G >= 8 ? 32u : 16u;
+    const uint32_t mn = wave_min(t_ok ? S : 0xffffffffu);
+    const uint32_t bk = t_ok ? min(kBk - 1u, S - mn) : 0u;  // invalid slots: bucket 0, sorted last
+    uint32_t rank = 0, base = 0;
+    for (int k = (int)kBk - 1; k >= 0; k--) {
+      // (invalid slots -- the chunk's highest lanes -- rank after bucket 0's valid ones)
+      const uint64_t m = __builtin_amdgcn_ballot_w64(bk == (uint32_t)k);
+      if (m == 0) continue;  // (scalar branch)
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (bk == (uint32_t)k) rank = base + below;
+      base += (uint32_t)__builtin_popcountll(m);
     }
     sortbuf[rank] = (uint32_t)lane;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

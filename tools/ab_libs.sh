@@ -6,7 +6,8 @@
 # tools/bench_ops.py (OPS, default log_write,log_verify,trailers,verify on the
 # SSTable-like image) and appends them to gpurun_out/ab_ops.log; with LAT=1 each
 # leg also runs tools/latency_burst.py (burst-kernel launch times, default lanes)
-# into gpurun_out/ab_lat.log; with LATR=1 tools/latency.py's mid-size batches
+# into gpurun_out/ab_lat.log; with LOG512=1 the log ops also on a U[1,512] B
+# payload image; with LATR=1 tools/latency.py's mid-size batches
 # (rounds kernel, default plan) into gpurun_out/ab_latr.log.  Every step has
 # its own time limit and the script stops at the first failure.
 set -u
@@ -24,6 +25,11 @@ for leg in new old new old; do
   echo "== $leg"
   timeout -k 10 300 python -u tools/bench_ops.py --ops "$OPS" --images sst4k > gpurun_out/ops_$leg.log 2>&1 || exit 3
   grep '"op"' gpurun_out/ops_$leg.log | sed "s/^/$leg /" >> gpurun_out/ab_ops.log
+  if [ "${LOG512:-0}" = 1 ]; then  # the short-record log image (payloads U[1,512] B)
+    timeout -k 10 300 python -u tools/bench_ops.py --ops log_write,log_verify --no-ablations --log-payload-max 512 \
+      > gpurun_out/ops512_$leg.log 2>&1 || exit 3
+    grep '"op"' gpurun_out/ops512_$leg.log | sed "s/^/$leg 512 /" >> gpurun_out/ab_ops.log
+  fi
   if [ "${LATR:-0}" = 1 ]; then  # mid-size batches, default dispatch (rounds kernel), events
     timeout -k 10 200 python -u tools/latency.py --sizes 16384,32768,65536,262144 --variants auto > gpurun_out/latr_$leg.log 2>&1 || exit 3
     grep '^{' gpurun_out/latr_$leg.log | sed "s/^/$leg /" >> gpurun_out/ab_latr.log

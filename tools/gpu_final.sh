@@ -1,8 +1,9 @@
 #!/bin/bash
 # End-of-round measurement on one box: smoke, the whole GPU suite, the driver's
 # bench line, rocprof kernel stats of the same command, PMC traffic passes for
-# every workload of the line (summarised on the host afterwards:
-# python tools/pmc_summary.py <cfg>), the composite ops.  Stops at the first
+# every workload of the line (PMC_CFGS; SQ=1 adds the SQ issue/wait passes;
+# summarised on the host afterwards: python tools/pmc_summary.py <cfg>), the
+# composite ops.  Stops at the first
 # failing step.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -24,7 +25,7 @@ STEPS=${STEPS:-smoke,pytest,bench,prof,pmc,ops}
 [[ $STEPS == *bench* ]] && step final_bench 600 python bench.py
 [[ $STEPS == *prof* ]] && step final_rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final_prof -o run -- python3 bench.py --no-cpu-baseline
 if [[ $STEPS == *pmc* ]]; then
-  for cfg in 2 3 4 sst4k_trailers sst4k_verify; do
+  for cfg in ${PMC_CFGS:-2 3 4 sst4k_trailers sst4k_verify log4k_write log4k_verify log512_write log512_verify parity}; do
     rm -rf gpurun_out/pmc$cfg
     step final_pmc_$cfg 400 bash tools/pmc.sh $cfg
   done

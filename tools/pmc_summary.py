@@ -34,17 +34,26 @@ STEP_KERNELS = {
     "4": ["crc32c_stream_kernel<16, 0>"],
     "sst4k_trailers": ["crc32c_rounds_kernel<8, 0>", "trailer_layout_kernel", "trailer_rmw_kernel"],
     "sst4k_verify": ["crc32c_rounds_kernel<8, 2>"],
+    "log4k_write": ["crc32c_rounds_kernel<8, 3>"],
+    "log4k_verify": ["crc32c_rounds_kernel<8, 4>", "log_sort_kernel", "log_unperm_kernel"],
+    "log512_write": ["crc32c_rounds_kernel<4, 3>"],
+    "log512_verify": ["crc32c_rounds_kernel<4, 4>"],
+    "parity": ["xor_parity_kernel"],
 }
+SQ_COUNTERS = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+               "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD",
+               "SQ_INSTS_VMEM_WR", "SQ_WAIT_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
+               "SQ_INSTS_SMEM", "SQ_ACTIVE_INST_VALU"]
 
 
 def label(name: str) -> str:
-    m = re.search(r"(trailer_\w+_kernel|log_\w+_kernel)", name)
+    m = re.search(r"(trailer_\w+_kernel|log_\w+_kernel|xor_parity_kernel)", name)
     return m.group(1) if m and "crc32c_" not in name else kernel_label(name)
 
 
 def per_kernel(ctr, cfg):
     vals = collections.defaultdict(list)
-    for path in glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc{cfg}", ctr, "**", "*counter_collection.csv"),
+    for path in glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc{cfg}", "**", "*counter_collection.csv"),
                           recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
@@ -77,6 +86,12 @@ def algorithmic(cfg):
     if cfg in ("sst4k_trailers", "sst4k_verify"):
         s = int(bench.sst4k_layout(n, 5)[1].astype(np.uint64).sum())
         return s + 5 * n if cfg == "sst4k_trailers" else s + 6 * n
+    # the others: the bytes the bench line of the same pass reports
+    path = os.path.join(ROOT, "gpurun_out", f"pmc{cfg}", "FETCH_SIZE.log")
+    if os.path.exists(path):
+        for line in reversed(open(path).read().splitlines()):
+            if line.startswith("{"):
+                return int(json.loads(line)["config"]["bytes_per_gpu"])
     return None
 
 
@@ -111,6 +126,24 @@ def main():
     }
     if algo:
         res["read_over_algorithmic"] = res["hbm_read_bytes_per_launch"] / algo
+    sq = {}
+    for ctr in SQ_COUNTERS:  # the main kernel's median per dispatch
+        v = sorted(per_kernel(ctr, cfg).get(kernels[0], []))
+        if v:
+            sq[ctr] = v[len(v) // 2]
+    if sq:
+        res["sq"] = sq
+        kib = (algo or 0) / 1024.0
+        if kib and "SQ_INSTS_VALU" in sq:
+            res["valu_per_kib"] = sq["SQ_INSTS_VALU"] / kib
+        if kib and "SQ_INSTS_LDS" in sq:
+            res["lds_per_kib"] = sq["SQ_INSTS_LDS"] / kib
+        if kib and "SQ_INSTS_SALU" in sq:
+            res["salu_per_kib"] = sq["SQ_INSTS_SALU"] / kib
+        if sq.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in sq:
+            res["wait_over_wave_cycles"] = sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]
+        if sq.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in sq:
+            res["lds_conflict_over_active"] = sq["SQ_LDS_BANK_CONFLICT"] / sq["SQ_LDS_IDX_ACTIVE"]
     out = os.path.join(ROOT, os.environ.get("PMC_OUT_DIR", "profiles"), f"pmc_config{cfg}.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
