@@ -306,13 +306,13 @@ def parity_copy_ceiling(torch, C, buf, fo, plen, stream, args) -> dict:
     """The XOR parity kernel's own bound, in the same run: a copy kernel of the
     same traffic shape -- the 8 fragments read and the 512 MiB written, nothing
     computed (copy_ceiling_kernel of the diagnostics library) --
-    at the chunks per lane that measured best in round 3, non-temporal loads and
-    stores, one-pass grid.  The faster of its forms is the ceiling."""
+    at 1-8 chunks per lane (8: the product's own shape), non-temporal loads
+    and stores, one-pass grid.  The fastest of its forms is the ceiling."""
     D = C.load_diag()
     sink = torch.empty(256, dtype=torch.int32, device=buf.device)
     tmp = torch.empty(plen, dtype=torch.uint8, device=buf.device)
     best = None
-    for u in (1, 2, 4):
+    for u in (1, 2, 4, 8):
         v = u | 1 << 4 | 1 << 5  # kind 0 (8 reads + 1 write), nt loads, nt stores
 
         def f(v=v):

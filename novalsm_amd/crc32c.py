@@ -106,6 +106,7 @@ _DIAG_SIG = {
     "nova_diag_set_burst_lanes": (None, [_i32]),
     "nova_diag_set_split": (None, [_i32]),
     "nova_diag_read_stream": (_i32, [_vp, _sz, _vp, _i32, _vp]),
+    "nova_diag_log_field_scatter": (_i32, [_vp, _vp, _u64, _vp]),
     "nova_diag_read_ceiling": (_i32, [_vp, _sz, _vp, _i32, _i32, _vp]),
 }
 ABI_VERSION = 3

@@ -961,6 +961,14 @@ __global__ void __launch_bounds__(kLsWaves * 64) crc32c_logstream_kernel(CrcPara
 }
 
 
+// Diagnostic: the log writer's CRC-field stores alone (VERDICT r03 item 2's
+// composite bound): one unaligned 4-B store per record at its header, as the
+// product's chunk epilogue issues them (store_u32_unaligned), value = index.
+__global__ void __launch_bounds__(256) log_field_scatter_kernel(uint8_t* base, const uint64_t* off, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) store_u32_unaligned(base + off[i], (uint32_t)i);
+}
+
 // Diagnostic: plain coalesced streaming read (grid-stride, 4 x 16 B per lane
 // in flight), the chip's read ceiling for comparison with the CRC kernels.
 __global__ void __launch_bounds__(256) read_stream_kernel(const uint8_t* base, uint64_t n16,
@@ -1656,11 +1664,20 @@ void nova_diag_set_trailer_single_pass(int on) { g_tune_trailer_1pass.store(on);
 void nova_diag_set_burst_lanes(int lanes) { g_tune_burst.store(lanes); }
 void nova_diag_set_split(int on) { g_tune_split.store(on); }
 
+// out_dev: wgs * 256 words (one per thread).
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream) {
   if (!base || !out_dev || wgs <= 0) return NOVA_E_INVAL;
   hipLaunchKernelGGL(read_stream_kernel, dim3(wgs), dim3(256), 0, (hipStream_t)stream,
                      (const uint8_t*)base, (uint64_t)(bytes / 16), out_dev);
+  return (int)hipGetLastError();
+}
+
+int nova_diag_log_field_scatter(void* base, const uint64_t* offsets_dev, uint64_t n, void* stream) {
+  if (!base || !offsets_dev) return NOVA_E_INVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(log_field_scatter_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (uint8_t*)base, offsets_dev, n);
   return (int)hipGetLastError();
 }
 

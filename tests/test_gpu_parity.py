@@ -313,6 +313,40 @@ def test_stream_host_matches_device(torch_gpu, oracle):
     assert np.array_equal(got2, got[:300])
 
 
+def test_pageable_adjacent_subpage_ranges_two_threads(torch_gpu, oracle):
+    """hipHostRegister pins whole pages, so two callers on
+    disjoint byte ranges of one pageable slab that share a page must not see
+    each other's registration as caller-pinned memory (HostReg rounds ranges
+    out to pages and counts references, crc32c_stream.cpp).  Two threads
+    checksum adjacent sub-page ranges back to back; every result is checked."""
+    import threading
+    L, n = 256, 8  # 2 KiB per range
+    slab = splitmix64_bytes(21, 5 * 4096)
+    a0 = (-slab.ctypes.data) % 4096 + 512  # 512 B into the slab's first whole page
+    ranges = [slab[a0:a0 + L * n], slab[a0 + L * n:a0 + 2 * L * n]]  # that page | it and the next
+    want = [np.array([oracle.value(r[i * L:(i + 1) * L].tobytes()) for i in range(n)], np.uint32)
+            for r in ranges]
+    errors = []
+    start = threading.Barrier(2)
+
+    def work(k):
+        try:
+            start.wait()
+            for it in range(150):
+                got = C.stream_host(ranges[k], L, L, n, chunk_blocks=4, n_streams=2)
+                if not np.array_equal(got, want[k]):
+                    errors.append((k, it, got, want[k]))
+                    return
+        except Exception as e:  # pragma: no cover
+            errors.append((k, e))
+    th = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:2]
+
+
 def test_lane_xor(torch_gpu):
     """the kernels' lane_xor<K> (DPP for K <= 8, the gfx950
     v_permlane16/32_swap for 16 and 32) equals __shfl_xor on every lane of a
@@ -1924,18 +1958,23 @@ def test_log_plan_by_record_size(torch_gpu, oracle, pmax):
     plen = rng.integers(1, pmax + 1, n)
     host, offs, _, _ = log_image(31, plen)
     assert len(offs) >= 1 << 16
-    buf = dev(torch, host)
+    # plus a probe at the end of the file: TRUNCATED, so nothing may be stored
+    # for it (its header bytes read as a length past the block)
+    offs = np.append(offs, np.uint64(host.size))
+    buf = dev(torch, np.append(host, np.full(64, 0xA5, np.uint8)))
     doffs = dev(torch, offs, torch.int64)
     want = host.copy()
-    oracle.log_write(want, offs)
+    oracle.log_write(want, offs[:-1])  # (the oracle writes at every offset it is given)
     C.log_write_crcs(buf, doffs)
-    assert np.array_equal(buf.cpu().numpy(), want)
-    ok, bad = C.log_verify_records(buf, doffs)
-    assert (ok.cpu().numpy() == C.LOG_OK).all() and int(bad.item()) == 0
-    victims = rng.choice(len(offs), 50, replace=False)
+    got = buf.cpu().numpy()
+    assert np.array_equal(got[:host.size], want) and (got[host.size:] == 0xA5).all()
+    ok, bad = C.log_verify_records(buf[:host.size], doffs)
+    okh = ok.cpu().numpy()
+    assert (okh[:-1] == C.LOG_OK).all() and okh[-1] == C.LOG_TRUNCATED and int(bad.item()) == 0
+    victims = rng.choice(len(offs) - 1, 50, replace=False)
     for v in victims:
         buf[int(offs[v]) + 6] ^= 0x02  # the type byte is CRC input
-    ok, bad = C.log_verify_records(buf, doffs)
+    ok, bad = C.log_verify_records(buf[:host.size], doffs)
     okh = ok.cpu().numpy()
     assert sorted(np.nonzero(okh == C.LOG_CHECKSUM_MISMATCH)[0].tolist()) == sorted(victims.tolist())
     assert int(bad.item()) == len(victims)

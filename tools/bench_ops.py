@@ -79,6 +79,8 @@ def main() -> int:
     ap.add_argument("--chunk-sweep", default="",
                     help="comma list of rounds-kernel chunk sizes (nova_diag_set_chunk_blocks), log ops")
     ap.add_argument("--no-ablations", action="store_true", help="skip the diagnostics ablations")
+    ap.add_argument("--log-bound", action="store_true",
+                    help="log write: time its composite bound (no-store pass + isolated CRC-field stores)")
     args = ap.parse_args()
     import torch
     from novalsm_amd import crc32c as C
@@ -123,6 +125,42 @@ def main() -> int:
                               "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}),
                   flush=True)
         C.set_tuning(0, 0)
+
+    def log_write_bound(buf, o, n, total, sum_rec, sec_product):
+        """log write's composite bound, all in this run --
+        the same launch without its result stores (diagnostics ablation 6) plus
+        the CRC-field stores alone (one unaligned 4-B store per record at its
+        header, nova_diag_log_field_scatter), each timed right after a read of
+        the whole image so they find the image out of the caches, as the
+        product's stores do."""
+        with C.diagnostics() as D:
+            D.nova_diag_set_trailer_single_pass(6)
+            t_ns = timed(torch, lambda: C.log_write_crcs(buf, o, stream=stream), args.steps, args.warmup, stream)
+            D.nova_diag_set_trailer_single_pass(0)
+        D = C.load_diag()
+        wgs = 4096
+        sink = torch.zeros(wgs * 256, dtype=torch.int32, device="cuda")  # read_stream: one word per thread
+        sp = stream.cuda_stream
+        ms = []
+        for it in range(args.warmup + args.steps):
+            assert D.nova_diag_read_stream(buf.data_ptr(), total, sink.data_ptr(), wgs, sp) == 0
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            assert D.nova_diag_log_field_scatter(buf.data_ptr(), o.data_ptr(), n, sp) == 0
+            e1.record(stream)
+            e1.synchronize()
+            if it >= args.warmup:
+                ms.append(e0.elapsed_time(e1))
+        ms.sort()
+        t_sc = ms[len(ms) // 2] / 1e3
+        C.log_write_crcs(buf, o, stream=stream)  # the CRC fields again
+        torch.cuda.synchronize()
+        bound = t_ns + t_sc
+        print(json.dumps({"sweep": "log_write_bound", "records": n, "no_store_ms": round(t_ns * 1e3, 4),
+                          "field_scatter_ms": round(t_sc * 1e3, 4), "bound_ms": round(bound * 1e3, 4),
+                          "product_ms": round(sec_product * 1e3, 4),
+                          "bound_frac": round(sum_rec / bound / 1e9 / HBM_PEAK_GBS, 4),
+                          "product_over_bound": round(sec_product / bound, 4)}), flush=True)
 
     def emit(op, workload, alg_bytes, sec, ok, extra=None):
         gbs = alg_bytes / sec / 1e9
@@ -264,6 +302,8 @@ def main() -> int:
                 gbs1 = sum_rec / sec1 / 1e9
                 print(json.dumps({"sweep": name, "GBps": round(gbs1, 1),
                                   "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
+            if args.log_bound:
+                log_write_bound(buf, o, n, total, sum_rec, sec)
         if "log_verify" in ops:
             C.log_write_crcs(buf, o, stream=stream)
             okb = torch.empty(n, dtype=torch.uint8, device="cuda")
