@@ -307,11 +307,13 @@ def parity_copy_ceiling(torch, C, buf, fo, plen, stream, args) -> dict:
     same traffic shape -- the 8 fragments read and the 512 MiB written, nothing
     computed (copy_ceiling_kernel of the diagnostics library) --
     at 1-8 chunks per lane (8: the product's own shape), non-temporal loads
-    and stores, one-pass grid.  The fastest of its forms is the ceiling."""
+    and stores, one-pass grid -- and the runtime's device-to-device copy of
+    one fragment.  The fastest form is the ceiling."""
     D = C.load_diag()
     sink = torch.empty(256, dtype=torch.int32, device=buf.device)
     tmp = torch.empty(plen, dtype=torch.uint8, device=buf.device)
     best = None
+    forms = {}
     for u in (1, 2, 4, 8):
         v = u | 1 << 4 | 1 << 5  # kind 0 (8 reads + 1 write), nt loads, nt stores
 
@@ -321,10 +323,21 @@ def parity_copy_ceiling(torch, C, buf, fo, plen, stream, args) -> dict:
             assert rc == 0, rc
         sec = _events_avg_s(torch, f, stream)
         gbs = 9 * plen / sec / 1e9
+        forms[f"copy_kernel_{u}_chunks"] = round(gbs, 1)
         if best is None or gbs > best["achieved"]:
             best = {"kind": "8-read + 1-write copy, no XOR (copy_ceiling_kernel, diagnostics library)",
                     "chunks_per_lane": u, "achieved": round(gbs, 1), "unit": "GB/s",
                     "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+    # the runtime's own device-to-device copy of one fragment (1 read + 1 write:
+    # HBM's mixed read/write rate as the driver's copy engine-free path reaches it)
+    src = buf[int(fo[0].item()):int(fo[0].item()) + plen]
+    sec = _events_avg_s(torch, lambda: tmp.copy_(src), stream)
+    gbs = 2 * plen / sec / 1e9
+    forms["hip_d2d_copy"] = round(gbs, 1)
+    if gbs > best["achieved"]:
+        best = {"kind": "hipMemcpyAsync device-to-device copy of one fragment (torch copy_)",
+                "achieved": round(gbs, 1), "unit": "GB/s", "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+    best["forms_GBps"] = forms
     del tmp, sink
     return best
 
