@@ -1466,6 +1466,10 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
   uint64_t n_u0 = 0, c_u0 = 0;
   uint32_t n_n = 0, n_rec = 0, n_aux = 0, c_n = 0, c_rec = 0, c_aux = 0;
   uint32_t t_ok = 0, n_ok = 0, c_ok = 0;  // slot holds a block of the batch
+  // sorted chunks: each slot's line count, and whether the sort was exact (no
+  // bucket clamped), so a round's longest block is its first slot
+  uint32_t n_S = 0, c_S = 0;
+  bool n_exact = false, c_exact = false;
   uint32_t n_chunk = kNone, c_chunk = kNone, t_chunk = kNone;
   // wave-uniform state packed in one word (fewer scalar registers)
   constexpr uint32_t fReady = 1, fRefill = 2, fDry = 4, fDone = 8, fRoundDone = 16, fClaim = 32;
@@ -1507,6 +1511,7 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
   };
   auto sort_nxt = [&]() {
     n_ok = t_ok;
+    n_exact = false;
     if (!p.sort_local) return;
     uint32_t S = 0;
     if (t_ok) {  // key: lines on the group's line grid (a round costs its longest block's lines)
@@ -1524,6 +1529,8 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
     constexpr uint32_t kBk = G >= 8 ? 32u : 16u;
     const uint32_t mn = wave_min(t_ok ? S : 0xffffffffu);
     const uint32_t bk = t_ok ? min(kBk - 1u, S - mn) : 0u;  // invalid slots: bucket 0, sorted last
+    // exact: no key clamped (invalid slots have S = 0, below every valid one)
+    n_exact = __builtin_amdgcn_ballot_w64(t_ok && S - mn > kBk - 1u) == 0;
     uint32_t rank = 0, base = 0;
     for (int k = (int)kBk - 1; k >= 0; k--) {
       // (invalid slots -- the chunk's highest lanes -- rank after bucket 0's valid ones)
@@ -1545,6 +1552,7 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
     n_aux = __shfl(n_aux, src);
     if constexpr (kBatch) n_tr = __shfl(n_tr, src);
     n_ok = __shfl(t_ok, src);
+    n_S = __shfl(S, src);
   };
   auto pipe = [&](uint32_t st) {  // run stage st (its inputs are complete or waited for)
     if (st == 1) {
@@ -1663,6 +1671,8 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
         c_rec = n_rec;
         c_aux = n_aux;
         c_ok = n_ok;
+        c_S = n_S;
+        c_exact = n_exact;
         c_chunk = n_chunk;
         fl &= ~fReady;
         r_idx = 0;
@@ -1704,8 +1714,18 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
       // the shortest non-empty region: its first line is the latest one, so
       // from step r_fast on every lane's four pieces are region pieces
       uint32_t mn = (ok && n > 0) ? nl : 0xffffffffu;
-      m = wave_max(m);
-      mn = wave_min(mn);
+      if (c_exact) {
+        // an exactly sorted chunk (largest first, invalid slots last): the
+        // round's first slot holds its longest block (m is then exact, as it
+        // must be), its last slot a lower bound of the shortest (a smaller mn
+        // only takes fewer fast steps)
+        const int s0 = __builtin_amdgcn_readfirstlane((int)(slot - (uint32_t)grp));
+        m = (uint32_t)__builtin_amdgcn_readlane((int)c_S, s0);
+        mn = (uint32_t)__builtin_amdgcn_readlane((int)c_S, s0 + (int)kGroups - 1);  // 0: an invalid slot
+      } else {
+        m = wave_max(m);
+        mn = wave_min(mn);
+      }
       r_S = (uint32_t)__builtin_amdgcn_readfirstlane((int)((m + 3) >> 2));  // wave-uniform: scalar control flow
       r_sk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(4 * r_S - m));
       {
