@@ -11,19 +11,25 @@
 // 14-29 % of the HBM roofline.
 //
 // The engine pays the launch and the table fill once per burst of requests:
-//   * one workgroup per CU stays resident with the units kernel's LDS tables
-//     (crc32c_units_kernel, whole blocks as units, G lanes per block);
+//   * one workgroup per CU (8 waves) stays resident with the M_256 tables in
+//     LDS (G = 16 lanes per block);
 //   * a submitting thread writes its request (image, descriptor arrays,
-//     outputs, op) into a ring in pinned host memory and bumps a tail word;
+//     outputs, op, blocks per chunk) into a ring in pinned host memory and
+//     bumps a tail word;
 //   * wave 0 of workgroup 0 -- the dispatcher -- polls the tail, copies new
-//     requests into device-memory slots and publishes their chunk tickets
-//     (chunks of cb blocks) by advancing one end word;
-//   * every other wave takes tickets from its XCD's head (eight heads: one
-//     device-scope atomic per ticket, MI355X_MICROARCH.md "dequeue"), claims
-//     the next ticket while it checksums the current chunk with the units
-//     kernel's chunk body (units_chunk), and counts the chunk done; the wave
-//     that finishes a request's last chunk writes the request's completion
-//     word in pinned host memory, on which its submitter spins.
+//     requests into device-memory slots, maps their ticket pages to them and
+//     publishes their chunk tickets by advancing one end word;
+//   * one poller wave per CU reads the end word and shares it through LDS;
+//     every other wave takes tickets from its XCD's head (eight heads,
+//     MI355X_MICROARCH.md "dequeue"), finds the ticket's request (its cursor
+//     slot and the ticket's page, one round trip), runs the chunk
+//     (engine_chunk: rounds of 4 blocks, all of a block's loads at once),
+//     counts it on its XCD's counter line and only then claims its next
+//     ticket (the claim's add is contended; before the chunk, every load of
+//     the chunk would wait for it);
+//   * the last chunk of an XCD bumps the request's top counter; the last of
+//     those writes the request's completion word in pinned host memory, on
+//     which its submitter spins (a test for >=: the word only grows).
 // Once no request arrives for the idle time (default 1 ms) and every taken
 // request is done, the dispatcher stops the workers and the kernel exits,
 // recording the first request it did not take; a submitter that finds its
@@ -41,8 +47,8 @@
 //     loaded with agent-scope atomics (write-through, L1-bypassing), drained
 //     before the end word is advanced;
 //   * caller memory: the chunk body loads descriptors, block bytes and stored
-//     CRCs non-temporally (kVarEngine), so no L1 line of a buffer rewritten
-//     since an earlier request is used;
+//     CRCs non-temporally, so no L1 line of a buffer rewritten since an earlier
+//     request is used;
 //   * results: stored write-through (agent-scope atomic stores) and drained
 //     (s_waitcnt vmcnt(0)) before the chunk's done count is added -- no L2
 //     write-back fence, which at one per chunk serialised the engine at
