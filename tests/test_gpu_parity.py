@@ -1165,6 +1165,90 @@ def test_engine_start_stop_restart(torch_gpu, oracle):
         C.engine_set_enabled(-1)
 
 
+_ENGINE_WRAP_CHILD = r"""
+import sys, threading
+sys.path.insert(0, %r)
+import numpy as np, torch
+from novalsm_amd import crc32c as C
+from tests.oracle_lib import load_oracle
+orc = load_oracle()
+C.engine_set_enabled(1)
+
+def table(n, seed, lo, hi):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(5))
+    total = int(offs[-1]) + int(lens[-1]) + 5
+    img = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    C.fill_splitmix64(img, seed)
+    torch.cuda.synchronize()
+    return dict(n=n, img=img, offs_np=offs, lens_np=lens,
+                offs=torch.from_numpy(offs.view(np.int64)).cuda(),
+                lens=torch.from_numpy(lens.view(np.int32)).cuda())
+
+def check(tb, errs, tag):
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        C.queue_write_trailers(tb["img"], tb["offs"], tb["lens"], stream=s)
+        host = tb["img"].cpu().numpy()
+        want = orc.batch(host, tb["offs_np"], tb["lens_np"], None,
+                         flags=C.APPEND_TYPE | C.MASK_OUTPUT | C.TYPE(0))
+        ends = tb["offs_np"].astype(np.int64) + tb["lens_np"].astype(np.int64)
+        w = sum(host[ends + 1 + i].astype(np.uint32) << (8 * i) for i in range(4))
+        if not (np.array_equal(w, want) and (host[ends] == 0).all()):
+            errs.append((tag, "trailers", int(np.count_nonzero(w != want))))
+            return
+        vic = [tb["n"] // 3, tb["n"] - 1]
+        for v in vic:
+            tb["img"][int(tb["offs_np"][v])] ^= 0x40
+        ok = torch.full((tb["n"],), 9, dtype=torch.uint8, device="cuda")
+        nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+        C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, nb, stream=s)
+        okh = ok.cpu().numpy()
+        if sorted(np.nonzero(okh != 1)[0].tolist()) != vic or int(nb.item()) != 2:
+            errs.append((tag, "verify", np.nonzero(okh != 1)[0][:4].tolist(), int(nb.item())))
+        for v in vic:
+            tb["img"][int(tb["offs_np"][v])] ^= 0x40
+
+big = [table(1 << 20, 71 + k, 8, 72) for k in range(2)]   # 1M blocks: 2^18 tickets at 4 per chunk
+small = [table(n, 90 + n, 4000, 4300) for n in (3, 700, 4096)]
+errs = []
+def big_caller():
+    for it in range(3):
+        for k, tb in enumerate(big):
+            check(tb, errs, ("big", it, k))
+def small_caller():
+    for it in range(40):
+        check(small[it %% 3], errs, ("small", it))
+th = [threading.Thread(target=big_caller), threading.Thread(target=small_caller)]
+for t in th: t.start()
+for t in th: t.join()
+st = C.engine_stats()
+print("ERRS", errs[:4], "FALLBACKS", st["fallbacks"], "REQUESTS", st["requests"])
+sys.exit(1 if errs or st["fallbacks"] else 0)
+"""
+
+
+def test_engine_ticket_pages_wrap(torch_gpu):
+    """The engine maps ticket pages (16 tickets) to requests as hints, in a
+    table of 2^18 tickets -- exactly one 1M-block request at 4 blocks per
+    chunk (NOVA_SST_ENGINE_CB=4, read once per process: a child process).
+    With a second caller's small tables in flight, later requests' pages
+    overwrite a running request's pages, so its waves read hints past their
+    own request and must fall back to their cursor (crc32c_engine.hip).  Both
+    callers' trailers and verify results (two corrupted blocks per call) are
+    checked against the oracle; no request may fall back to the plain call."""
+    import os
+    import subprocess
+    import sys
+    root = str(__import__("pathlib").Path(__file__).resolve().parents[1])
+    env = dict(os.environ, NOVA_SST_ENGINE_CB="4")
+    r = subprocess.run([sys.executable, "-c", _ENGINE_WRAP_CHILD % root], env=env, capture_output=True,
+                       text=True, timeout=240, cwd=root)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+
+
 def test_engine_idle_exit_and_buffer_rewrite(torch_gpu, oracle):
     """Between requests the engine stays resident (or exits when idle and is
     relaunched by the next call: both happen here, with a 300 us idle time).
