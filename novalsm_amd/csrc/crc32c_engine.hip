@@ -313,6 +313,18 @@ __device__ void engine_dispatch(const EngParams& e) {
 // write-through (the engine outlives the caller's writes and reads).
 constexpr int kEK = 18;  // swaths per pass: 4.5 KiB (4096 + 255 + 5 B blocks: one pass)
 
+// A trailer [type][LE32 masked crc] written through (sc1, as st_through's
+// agent-scope stores compile): the type byte, then the CRC as one unaligned
+// dword store (the hardware splits one that crosses a line) -- two partial
+// writes at the memory instead of five byte stores.  The dword store is
+// inline asm (an atomic store must be aligned); the chunk's vmcnt(0) drain
+// before its count covers it like every other result store.
+__device__ __forceinline__ void engine_store_trailer(uint8_t* d, uint32_t type, uint32_t m, bool quirk) {
+  const uint32_t w = quirk ? ((m & 0x00ffffffu) | ((uint32_t)'!' << 24)) : m;
+  st_through(d, (uint8_t)type);
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(d + 1), "v"(w) : "memory");
+}
+
 template <int MODE>
 __device__ __forceinline__ void engine_chunk(const uint8_t* lds, const CrcParams& p, uint64_t c) {
   constexpr int G = kEngG;
@@ -409,7 +421,7 @@ __device__ __forceinline__ void engine_chunk(const uint8_t* lds, const CrcParams
         st_through((uint8_t*)wb_a, (uint8_t)wb_v);
         nbad += wb_v ? 0u : 1u;
       } else if constexpr (MODE == kTrailer) {
-        store_trailer_through((uint8_t*)wb_a, (p.flags >> 8) & 0xffu, wb_v, (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
+        engine_store_trailer((uint8_t*)wb_a, (p.flags >> 8) & 0xffu, wb_v, (p.flags & NOVA_TRAILER_TB_QUIRK) != 0);
       } else {
         st_through((uint32_t*)wb_a, wb_v);
       }
