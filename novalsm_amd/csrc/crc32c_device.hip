@@ -525,6 +525,21 @@ void init_device(int dev, DevTables* t) {
   hipError_t e = hipGetDeviceProperties(&prop, dev);
   if (e != hipSuccess) { t->err = (int)e; return; }
   t->cus = prop.multiProcessorCount;
+  {  // the scratch pool (DevTables::pool); without it scratch uses hipMallocAsync
+    hipMemPoolProps pp{};
+    pp.allocType = hipMemAllocationTypePinned;
+    pp.handleTypes = hipMemHandleTypeNone;
+    pp.location.type = hipMemLocationTypeDevice;
+    pp.location.id = dev;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &pp) == hipSuccess) {
+      uint64_t keep = 512ull << 20;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      t->pool = pool;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
   using namespace nova::gf2;
   const Lin m1 = zero_byte();
   std::vector<uint32_t> img;
@@ -800,6 +815,7 @@ int launch_burst_g(int V, CrcParams& p, DevTables* t, hipStream_t stream) {
 
 
 constexpr uint64_t kLogSortMin = 1u << 16;  // records: the log_sort_kernel pre-pass from here
+constexpr uint64_t kTrailerTwoPassMin = 1u << 18;  // blocks: the trailer writer's two passes from here
 // Records per sort window: the power of two nearest to ~512 KiB of log.  A wider
 // window cuts more round padding but spreads a chunk's reads over more of the
 // image; measured over payloads U[1,512] .. U[1,16384] B the best window spanned
@@ -1036,7 +1052,13 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
                        p.offsets, n, perm, st_pos, crc_pos, mode == kLogWrite ? nullptr : status_out, win);
     return (int)hipGetLastError();
   }
-  if (pl.kernel == kRoundsK && mode == kTrailer) return trailer_two_pass(p, G, pl.chunk, t, stream);
+  // The trailer writer's two passes (CRC array, then whole-piece rewrite)
+  // win from ~2^18 blocks; below, the CRC kernel's own trailer stores save two
+  // launches and the scratch (a call waited on, sst4k blocks, events:
+  // 16K blocks 33 vs 49 us, 64K 75 vs 90 us, 256K 238 vs 240 us, 1M 851 vs
+  // 770 us; profiles/r04_trailer_forms_sizes_pool.log).
+  if (pl.kernel == kRoundsK && mode == kTrailer && p.n_blocks >= kTrailerTwoPassMin)
+    return trailer_two_pass(p, G, pl.chunk, t, stream);
   if (pl.kernel == kRoundsK) {
     switch (mode) {
       case kStore: return launch_rounds<kStore>(G, p, t, stream, pl.chunk);

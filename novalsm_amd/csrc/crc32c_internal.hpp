@@ -136,6 +136,12 @@ struct DevTables {
   uint32_t* ls_tabs = nullptr;    // diagnostics: log-stream kernel LDS tail (M4, M16, prefix masks)
   int cus = 0;
   int err = 0;
+  // Stream-ordered scratch pool (StreamScratch): keeps up to 512 MiB mapped
+  // between calls.  With the default pool's release threshold (0) every sync
+  // handed the scratch back to the driver and the next call mapped it again:
+  // a trailer writer waited on per table paid ~20-200 us for it
+  // (profiles/r04_trailer_forms_sizes*.log).  Null: hipMallocAsync.
+  hipMemPool_t pool = nullptr;
   // Claim counters, one 16 KiB slot per HIP stream (256 workgroups x 64 B).
   // Launches on one stream run in order, so no two running launches share a
   // slot; each launch leaves its slot zeroed (sched_release).  A slot lives
@@ -202,6 +208,10 @@ struct StreamScratch {
   hipStream_t s = nullptr;
   int alloc(size_t bytes, hipStream_t stream) {
     s = stream;
+    int err = 0;
+    DevTables* t = tables(&err);
+    if (t && t->pool && hipMallocFromPoolAsync(&p, bytes, t->pool, stream) == hipSuccess) return 0;
+    (void)hipGetLastError();
     if (hipMallocAsync(&p, bytes, stream) == hipSuccess) return 0;
     p = nullptr;
     (void)hipGetLastError();  // not sticky for the caller's next launch check

@@ -1328,17 +1328,19 @@ def test_engine_idle_exit_and_buffer_rewrite(torch_gpu, oracle):
     assert C.engine_stats()["fallbacks"] == 0
 
 
-def test_queue_batched_trailers_adjacent_tables(torch_gpu, oracle):
-    """the coalescing queue's batched trailer writer (more than
-    12288 blocks: the rounds kernel and the whole-piece second pass) on four
-    tables that are adjacent, unpadded slices of one buffer.  Every trailer
-    equals the oracle's, and no byte outside the tables' trailers changes --
-    in particular not the next table's first bytes, which the last block's
-    64-B trailer piece reaches when it is rewritten whole."""
+@pytest.mark.parametrize("size", ["one_pass", "two_pass"])
+def test_queue_batched_trailers_adjacent_tables(torch_gpu, oracle, size):
+    """the coalescing queue's batched trailer writer on four tables
+    that are adjacent, unpadded slices of one buffer: above 12288 blocks the
+    rounds kernel, and from 2^18 blocks (kTrailerTwoPassMin) the whole-piece
+    second pass.  Every trailer equals the oracle's, and no byte outside the
+    tables' trailers changes -- in particular not the next table's first
+    bytes, which the last block's 64-B trailer piece reaches when it is
+    rewritten whole."""
     torch = torch_gpu
     import threading
     from bench import sst4k_layout
-    ns = [5000, 4500, 5100, 4900]  # any three: more than 12288 blocks
+    ns = [5000, 4500, 5100, 4900] if size == "one_pass" else [70000, 66000, 68000, 65000]
     lays = [sst4k_layout(n, 60 + k) for k, n in enumerate(ns)]
     # table k starts where table k-1's last trailer ends, plus 0..40 bytes
     starts, pos = [], 0
