@@ -710,6 +710,14 @@ struct Engine {
     DevTables* t = tables(&err);
     if (!t) return err;
     cus = t->cus;
+    {
+      // NOVA_SST_ENGINE_CUS: run on fewer CUs (one workgroup each, whose LDS
+      // tables keep any other kernel off that CU while the engine is
+      // resident); workgroups go round-robin over the XCDs, so every XCD
+      // still gets its share.  Rounded down to a multiple of 8.
+      const uint64_t want = env_u64("NOVA_SST_ENGINE_CUS", 0);
+      if (want >= 8 && want < (uint64_t)cus) cus = (int)(want & ~7ull);
+    }
     hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&ring, sizeof(EngHostReq) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
