@@ -152,19 +152,31 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
  * too little work for a launch of its own.  These calls run on a persistent
  * kernel (crc32c_engine.hip) that stays resident while
  * requests arrive -- one workgroup per CU, tables loaded once -- and exits
- * after NOVA_SST_ENGINE_IDLE_US (default 1000) without one; the next call
- * starts it again.  While it is resident it holds every CU's LDS, so this
- * process's other kernels (plain calls included) wait for its idle exit.
+ * after NOVA_SST_ENGINE_IDLE_US (default 1000, at most 1 s) without one; the
+ * next call starts it again.
+ * Sharing the GPU: while resident the engine holds every CU's LDS.  Every
+ * other launch of this library (plain batches, composites, log, parity,
+ * host-streamed paths, the hook) makes it yield: it takes no new request,
+ * finishes the ones it took and exits, and its next instance starts only
+ * after those launches have finished; so a plain call waits at most for the
+ * requests already taken.  Kernels of OTHER libraries are
+ * not seen: call nova_sst_engine_yield(stream) after enqueuing them on
+ * `stream` (or keep the engine off with nova_sst_engine_set_enabled(0)).
  * Work queued on `stream` before the call (the image, its descriptors)
  * completes first: the call synchronises `stream` when it is busy.  A table
  * of more than 2^20 blocks runs as the plain call on `stream`, and so does a
- * request the engine cannot run (no device memory, an engine error, or
- * NOVA_SST_ENGINE_TIMEOUT_MS, default 10000, without a result; the engine is
- * then not used again by this process; a verify counter is zeroed before the
- * plain call recomputes it).  NOVA_SST_ENGINE=0: the round-3 coalescing
- * queue instead (concurrent calls grouped into shared launches,
- * NOVA_SST_QUEUE_SLOTS 1..4 batches in flight, nova_sst_queue_set_slots;
- * DESIGN.md 3.5d). */
+ * request the engine did not run: no device memory, an engine error, or
+ * NOVA_SST_ENGINE_TIMEOUT_MS (default 10000; nova_sst_engine_set_timeout_ms)
+ * without a result.  The plain call runs only once the engine can no longer
+ * touch the request (it is taken back: never started, skipped, or the
+ * instance stopped and ended); the engine then backs off (100 ms, doubling to
+ * 12.8 s, reset by a success) and is tried again.  If it cannot be taken back
+ * within max(timeout, 30 s) the call returns NOVA_E_NODEV WITHOUT the plain
+ * call -- the outputs may still be written -- and the engine is not used
+ * again by this process.  A verify counter is zeroed before the plain call
+ * recomputes it.  NOVA_SST_ENGINE=0: the round-3 coalescing queue instead
+ * (concurrent calls grouped into shared launches, NOVA_SST_QUEUE_SLOTS 1..4
+ * batches in flight, nova_sst_queue_set_slots). */
 int nova_sst_queue_write_trailers(void* buf, const uint64_t* offsets, const uint32_t* sizes,
                                   size_t n_blocks, uint32_t flags, void* stream);
 int nova_sst_queue_verify_blocks(const void* buf, const uint64_t* offsets, const uint32_t* sizes,
@@ -184,6 +196,24 @@ int nova_sst_engine_start(void);
 int nova_sst_engine_stop(void);
 int nova_sst_engine_stats(uint64_t* requests, uint64_t* launches, uint64_t* fallbacks, int* running);
 int nova_sst_engine_set_idle_us(uint32_t us);
+/* Counters of this device's engine, out[0..n) (n <= NOVA_ENGINE_COUNTERS):
+ * requests, instances launched, plain-call fallbacks, resident now; instance
+ * exits after the idle time, for a yield, for a stop, giving up on a request;
+ * requests timed out, engine errors, requests taken back, requests that could
+ * not be taken back; relaunches that waited for a yielded launch, yield bumps;
+ * disabled for good, backing off now. */
+#define NOVA_ENGINE_COUNTERS 16
+int nova_sst_engine_counters(uint64_t* out, size_t n);
+/* Host timeout for one engine request (0: NOVA_SST_ENGINE_TIMEOUT_MS). */
+int nova_sst_engine_set_timeout_ms(uint32_t ms);
+/* Make the resident engine yield to work the caller enqueued on `stream`
+ * (its next instance waits for that work); for kernels of other libraries. */
+int nova_sst_engine_yield(void* stream);
+/* End a backoff now (the next request tries the engine). */
+int nova_sst_engine_reset(void);
+/* Test hook, calling thread only: wait `us` after submitting a request before
+ * waiting for it (a waiter descheduled past a whole ring turn). */
+void nova_sst_engine_set_wait_delay_us(uint32_t us);
 /* Route the nova_sst_queue_* calls of this process: 1 the engine, 0 the
  * coalescing queue, -1 back to NOVA_SST_ENGINE (default: the engine). */
 int nova_sst_engine_set_enabled(int on);
@@ -313,14 +343,18 @@ void nova_crc32c_set_tuning(int lanes_per_unit, uint32_t seg_bytes);
 const char* nova_error_string(int err);
 /* ABI version: bump on any signature or result-meaning change (2: log entry
  * points take buf_len; 3: log verify status NOVA_LOG_BLOCK_TRAILER (5), not
- * counted in n_bad, and the nova_sst_engine_* entry points). */
+ * counted in n_bad, and the nova_sst_engine_* entry points; 4: the engine
+ * yields to other launches, takes failed requests back, and the counters,
+ * timeout, yield, reset and wait-delay entry points). */
 int nova_crc32c_abi_version(void);
 
 /* ---- diagnostics: libnova_crc32c_diag.so ONLY ---------------------------
- * The product library does not export anything below.  The diagnostics build
- * (same sources, -DNOVA_DIAG) adds timing ablations, alternative schedules and
- * read-ceiling probes for tools/ and the tuning tests.  All knobs are per
- * calling thread.
+ * The product library does not export anything below.  The diagnostics
+ * library is the product's objects linked with one more translation unit
+ * (crc32c_diag.hip: its own kernels and diagnostics instantiations of the
+ * product templates, reached through a hook table; no preprocessor switch) and
+ * adds timing ablations, alternative schedules and read-ceiling probes for
+ * tools/ and the tuning tests.  All knobs are per calling thread.
  * variant: 0 production, 1 ablation (no table lookups -- WRONG CRCs, timing
  * only), 2 default-policy (cached) data loads instead of nt. */
 void nova_diag_set_variant(int variant);
@@ -369,6 +403,14 @@ void nova_diag_set_chunk_blocks(int blocks);
  * ceiling for the roofline discussion. */
 int nova_diag_read_stream(const void* base, size_t bytes, uint32_t* out_dev, int wgs,
                           void* stream);
+/* Occupy every CU (one workgroup with all 160 KiB of LDS each) for `us`
+ * microseconds (<= 5 s): a foreign kernel holding the resident engine off the
+ * device, for the engine's take-back tests. */
+int nova_diag_hold_cus(uint32_t us, void* stream);
+/* The engine's ticket-group arithmetic on the host (CPU test): out[0..8)
+ * workgroups per group for a grid of `wgs`, out[8..16) a request's tickets
+ * [cstart, cend) per group, out[16] the groups that complete it. */
+int nova_diag_engine_groups(uint32_t wgs, uint64_t cstart, uint64_t cend, uint64_t* out);
 
 #ifdef __cplusplus
 }  /* extern "C" */

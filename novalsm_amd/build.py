@@ -26,6 +26,10 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libnova_crc32c.so")
 DIAG_LIB = os.path.join(LIB_DIR, "libnova_crc32c_diag.so")
+# native caller threads for the per-SSTable paths (bench.py, tools, tests);
+# links the product library
+CALLERS_LIB = os.path.join(LIB_DIR, "libnova_sst_callers.so")
+CALLERS_SOURCE = "sst_callers.cpp"
 ARCH = os.environ.get("NOVA_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["crc32c_device.hip", "crc32c_stream.cpp", "crc32c_host.cpp", "crc32c_queue.hip",
@@ -66,6 +70,9 @@ def build(force: bool = False, verbose: bool = False, extra: list[str] | None = 
     """Build the product library (and, with diag=True, the diagnostics one)."""
     want = [LIB] + ([DIAG_LIB] if diag else [])
     if not force and not any(_stale(x) for x in want):
+        if not os.path.exists(CALLERS_LIB) or \
+                os.path.getmtime(os.path.join(CSRC, CALLERS_SOURCE)) > os.path.getmtime(CALLERS_LIB):
+            build_callers()
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     cc = hipcc()
@@ -96,7 +103,19 @@ def build(force: bool = False, verbose: bool = False, extra: list[str] | None = 
         os.replace(tmp, lib)
     for o in jobs:
         os.remove(o)
+    build_callers(cc)
     return LIB
+
+
+def build_callers(cc: str | None = None) -> str:
+    """libnova_sst_callers.so (sst_callers.cpp) against the product library."""
+    cc = cc or hipcc()
+    tmp = CALLERS_LIB + ".tmp"
+    subprocess.run([cc, "-x", "hip", f"--offload-arch={ARCH}", "-O2", "-fPIC", "-std=c++17", "-Wall", "-shared",
+                    "-I", os.path.join(ROOT, "include"), os.path.join(CSRC, CALLERS_SOURCE), "-o", tmp,
+                    "-L", LIB_DIR, "-lnova_crc32c", "-Wl,-rpath,$ORIGIN", "-lpthread"], check=True)
+    os.replace(tmp, CALLERS_LIB)
+    return CALLERS_LIB
 
 
 if __name__ == "__main__":

@@ -70,6 +70,11 @@ _SIG = {
     "nova_sst_engine_set_trace": (_i32, [ctypes.c_int]),
     "nova_sst_engine_trace_stats": (_i32, [_vp, _vp]),
     "nova_sst_engine_trace_detail": (_i32, [_vp, _vp]),
+    "nova_sst_engine_counters": (_i32, [_vp, _sz]),
+    "nova_sst_engine_set_timeout_ms": (_i32, [_u32]),
+    "nova_sst_engine_yield": (_i32, [_vp]),
+    "nova_sst_engine_reset": (_i32, []),
+    "nova_sst_engine_set_wait_delay_us": (None, [_u32]),
     "nova_crc32c_stream_host": (_i32, [_vp, _u64, _u32, _sz, _vp, _u32, _sz, _i32]),
     "nova_crc32c_batch_host": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _sz, _i32]),
     "nova_sstable_write_trailers_host": (_i32, [_vp, _vp, _vp, _sz, _u32, _sz, _i32]),
@@ -108,8 +113,10 @@ _DIAG_SIG = {
     "nova_diag_read_stream": (_i32, [_vp, _sz, _vp, _i32, _vp]),
     "nova_diag_log_field_scatter": (_i32, [_vp, _vp, _u64, _vp]),
     "nova_diag_read_ceiling": (_i32, [_vp, _sz, _vp, _i32, _i32, _vp]),
+    "nova_diag_hold_cus": (_i32, [_u32, _vp]),
+    "nova_diag_engine_groups": (_i32, [_u32, _u64, _u64, _vp]),
 }
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # log verify status codes (include/nova_crc32c.h, db/log_reader.cc:228-262)
 LOG_CHECKSUM_MISMATCH = 0
@@ -443,6 +450,39 @@ def engine_stats() -> dict:
            "nova_sst_engine_stats")
     return {"requests": v[0].value, "launches": v[1].value, "fallbacks": v[2].value,
             "running": bool(run.value)}
+
+
+ENGINE_COUNTERS = ("requests", "launches", "fallbacks", "running", "exits_idle", "exits_yield",
+                   "exits_stop", "exits_lost", "timeouts", "errors", "taken_back", "unsafe",
+                   "yield_waits", "yield_bumps", "broken", "backing_off")
+
+
+def engine_counters() -> dict:
+    """nova_sst_engine_counters: the engine's lifetime counters (include/nova_crc32c.h)."""
+    v = (ctypes.c_uint64 * len(ENGINE_COUNTERS))()
+    _check(_L().nova_sst_engine_counters(v, len(ENGINE_COUNTERS)), "nova_sst_engine_counters")
+    return dict(zip(ENGINE_COUNTERS, [int(x) for x in v]))
+
+
+def engine_set_timeout_ms(ms: int) -> None:
+    """Host timeout of one engine request (0: NOVA_SST_ENGINE_TIMEOUT_MS)."""
+    _check(_L().nova_sst_engine_set_timeout_ms(int(ms)), "nova_sst_engine_set_timeout_ms")
+
+
+def engine_yield(stream=None) -> None:
+    """Make the resident engine yield to work enqueued on `stream` (kernels of
+    other libraries)."""
+    _check(_L().nova_sst_engine_yield(_stream_ptr(stream)), "nova_sst_engine_yield")
+
+
+def engine_reset() -> None:
+    """End an engine backoff now."""
+    _check(_L().nova_sst_engine_reset(), "nova_sst_engine_reset")
+
+
+def engine_set_wait_delay_us(us: int) -> None:
+    """Test hook (calling thread): start waiting for a submitted request `us` late."""
+    _L().nova_sst_engine_set_wait_delay_us(int(us))
 
 
 def engine_set_enabled(on: int) -> None:

@@ -21,110 +21,8 @@
 
 namespace {
 
-// XOR parity block over k data fragments (ltc/stoc_file_client_impl.cpp:334-349):
-// parity[i] = XOR_f mem[frag_off[f] + i] for i < parity_len.  Like the
-// reference, every fragment contributes parity_len bytes from its start (the
-// reference loop reads past a shorter fragment's end).  Each thread makes kU
-// 16-byte output chunks (grid-strided), so every fragment step issues kU
-// independent loads.  A fragment's misalignment s is wave-uniform: unaligned
-// fragments cost one more aligned load per chunk + v_alignbyte funnel shifts.
-// Loads are clamped to the aligned 16 B holding the fragment's last byte, so
-// nothing past the parity region's last 16-B line is touched; lanes past the
-// end re-read the last chunk and discard it.
-//
-// FU fragments are loaded together (U * FU loads in flight per thread) when
-// they are all 16-B aligned; a group with an unaligned fragment takes them one
-// at a time through the funnel-shift path.
-template <int U, int FU>
-__global__ void __launch_bounds__(256) xor_parity_kernel(const uint8_t* base, const uint64_t* frag_off,
-                                                         uint32_t n_frags, uint64_t parity_len,
-                                                         uint8_t* out) {
-  const uint64_t nchunks = (parity_len + 15) / 16;
-  const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c0 < nchunks;
-       c0 += U * nth) {
-    uint32_t x[U][4] = {};
-    uint64_t cc[U];
-#pragma unroll
-    for (int k = 0; k < U; k++) {
-      const uint64_t c = c0 + k * nth;
-      cc[k] = c < nchunks ? c : nchunks - 1;
-    }
-    uint32_t f = 0;
-    for (; f + FU <= n_frags; f += FU) {
-      uint64_t fa[FU];
-      uint32_t any_s = 0;
-#pragma unroll
-      for (int i = 0; i < FU; i++) {
-        fa[i] = (uint64_t)base + frag_off[f + i];
-        any_s |= (uint32_t)(fa[i] & 15);
-      }
-      if (any_s != 0) break;  // unaligned: the per-fragment path below
-      uint4 v[FU][U];
-#pragma unroll
-      for (int i = 0; i < FU; i++)
-#pragma unroll
-        for (int k = 0; k < U; k++) v[i][k] = gload16(fa[i] + 16 * cc[k]);
-#pragma unroll
-      for (int i = 0; i < FU; i++)
-#pragma unroll
-        for (int k = 0; k < U; k++) {
-          x[k][0] ^= v[i][k].x; x[k][1] ^= v[i][k].y; x[k][2] ^= v[i][k].z; x[k][3] ^= v[i][k].w;
-        }
-    }
-    for (; f < n_frags; f++) {
-      const uint64_t fa = (uint64_t)base + frag_off[f];
-      const uint32_t s = (uint32_t)(fa & 15);
-      const uint64_t fb = fa - s;                              // aligned line of byte 0
-      const uint64_t lastline = (fa + parity_len - 1) & ~15ull;  // line of the last byte
-      if (s == 0) {
-        uint4 v[U];
-#pragma unroll
-        for (int k = 0; k < U; k++) v[k] = gload16(fb + 16 * cc[k]);
-#pragma unroll
-        for (int k = 0; k < U; k++) {
-          x[k][0] ^= v[k].x; x[k][1] ^= v[k].y; x[k][2] ^= v[k].z; x[k][3] ^= v[k].w;
-        }
-      } else {
-        uint4 lo[U], hi[U];
-#pragma unroll
-        for (int k = 0; k < U; k++) {
-          const uint64_t l = fb + 16 * cc[k];
-          lo[k] = gload16(l);
-          hi[k] = gload16(l + 16 <= lastline ? l + 16 : lastline);
-        }
-        const uint32_t ws = s >> 2, bs = s & 3;
-#pragma unroll
-        for (int k = 0; k < U; k++) {
-          const uint32_t w[8] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w,
-                                 hi[k].x, hi[k].y, hi[k].z, hi[k].w};
-#pragma unroll
-          for (int e = 0; e < 4; e++) {
-            // W[e+ws], W[e+ws+1] without dynamic register indexing
-            uint32_t a = w[e], b = w[e + 1];
-            if (ws == 1) { a = w[e + 1]; b = w[e + 2]; }
-            else if (ws == 2) { a = w[e + 2]; b = w[e + 3]; }
-            else if (ws == 3) { a = w[e + 3]; b = w[e + 4]; }
-            x[k][e] ^= __builtin_amdgcn_alignbyte(b, a, bs);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < U; k++) {
-      const uint64_t c = c0 + k * nth;
-      if (c >= nchunks) break;
-      const uint64_t o = 16 * c;
-      if (o + 16 <= parity_len) {
-        u32x4 val = {x[k][0], x[k][1], x[k][2], x[k][3]};
-        __builtin_nontemporal_store(val, (__attribute__((address_space(1))) u32x4*)(uint64_t)(out + o));
-      } else {
-        for (uint64_t i = o; i < parity_len; i++)
-          out[i] = (uint8_t)(x[k][(i - o) >> 2] >> (8 * ((i - o) & 3)));
-      }
-    }
-  }
-}
+// (xor_parity_kernel: crc32c_kernels.hpp, shared with the diagnostics TU's A/B forms)
+
 
 
 // ---- few large blocks: split and combine --------------------
@@ -977,6 +875,8 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   DevTables* t = tables(&err);
   if (!t) return err;
   if (p.n_blocks == 0) return 0;
+  // the resident engine, if any, leaves the CUs to this call (crc32c_engine.hip)
+  EngineYield yield_engine(stream);
   if (split_wanted(mode, p, uniform, bytes_per_block)) {
     // no scratch for the pieces (nothing launched yet): the one-pass kernels
     // below; any failure after the first launch is returned as is
@@ -1101,7 +1001,7 @@ uint32_t cus_hint() {
 
 extern "C" {
 
-int nova_crc32c_abi_version(void) { return 3; }
+int nova_crc32c_abi_version(void) { return 4; }
 
 int nova_device_init(void) {
   int err = 0;
@@ -1112,7 +1012,9 @@ int nova_stream_release(void* stream) {
   int err = 0;
   DevTables* t = tables(&err);
   if (!t) return err;
-  return sched_release_stream(t, (hipStream_t)stream);
+  const int rc = sched_release_stream(t, (hipStream_t)stream);
+  engine_forget_stream((hipStream_t)stream);
+  return rc;
 }
 
 size_t nova_stream_slots(void) {
@@ -1233,6 +1135,7 @@ int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_fra
   const uint64_t cap = per_cu == 0xff ? (1ull << 31) - 1 : (uint64_t)t->cus * per_cu;
   if (wgs > cap) wgs = cap;
   hipStream_t st = (hipStream_t)stream;
+  EngineYield yield_engine(st);
   const uint8_t* b = (const uint8_t*)base;
   const uint32_t nf = (uint32_t)n_frags;
   const uint64_t pl = (uint64_t)parity_len;
@@ -1243,8 +1146,10 @@ int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_fra
     return (int)hipGetLastError();                                                            \
   }
   NOVA_XP(1, 1) NOVA_XP(2, 1) NOVA_XP(4, 1) NOVA_XP(4, 2) NOVA_XP(4, 4) NOVA_XP(2, 4) NOVA_XP(2, 2)
-  NOVA_XP(8, 1) NOVA_XP(8, 2) NOVA_XP(1, 8) NOVA_XP(2, 8) NOVA_XP(1, 4) NOVA_XP(1, 2) NOVA_XP(16, 1)
+  NOVA_XP(8, 1) NOVA_XP(8, 2) NOVA_XP(1, 8) NOVA_XP(2, 8) NOVA_XP(1, 4) NOVA_XP(1, 2)
 #undef NOVA_XP
+  int rc = NOVA_E_INVAL;  // other forms: the diagnostics library's (g_diag->parity)
+  if (g_diag && g_diag->parity && g_diag->parity(u, fu, b, frag_offsets, nf, pl, o, wgs, st, &rc)) return rc;
   return NOVA_E_INVAL;
 }
 
@@ -1255,6 +1160,7 @@ int nova_fill_splitmix64(void* dev, size_t nbytes, uint64_t seed, uint64_t first
   uint64_t blocks = (nbytes / 8 + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   if (blocks == 0) blocks = 1;
+  EngineYield yield_engine((hipStream_t)stream);
   hipLaunchKernelGGL(fill_splitmix64_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                      (uint8_t*)dev, (uint64_t)nbytes, seed, first_word);
   return (int)hipGetLastError();

@@ -1345,6 +1345,15 @@ int store_forms(int mode, CrcParams& p, const Plan& pl, DevTables* t, hipStream_
   return kNotTaken;
 }
 
+// One workgroup per CU (all of its LDS) for `ticks` of the 100 MHz real-time
+// counter (nova_diag_hold_cus).
+__global__ void __launch_bounds__(64) hold_cus_kernel(uint64_t ticks) {
+  extern __shared__ uint8_t hold_lds[];
+  if (threadIdx.x == 0) hold_lds[0] = 1;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 // ---- hooks (DiagHooks, crc32c_internal.hpp) -----------------------------------
 void push_op(const nova::gf2::Lin& m, std::vector<uint32_t>& v) {
   uint32_t tb[4][256];
@@ -1580,8 +1589,21 @@ int hook_describe_flat(int G, int mode, char* buf, size_t buflen) {
                   flat_chunk(G, mode), (int)flat_waves());
 }
 
+// XOR parity forms the product does not instantiate (A/B only): 16 chunks per
+// lane x 1 fragment spills 272 B of scratch (tools/kernel_meta.py) and measured
+// below the product's 8 x 1.
+bool hook_parity(int u, int fu, const uint8_t* b, const uint64_t* fo, uint32_t nf, uint64_t pl, uint8_t* o,
+                 uint64_t wgs, hipStream_t st, int* rc) {
+  if (u == 16 && fu == 1) {
+    hipLaunchKernelGGL((xor_parity_kernel<16, 1>), dim3(wgs), dim3(256), 0, st, b, fo, nf, pl, o);
+    *rc = (int)hipGetLastError();
+    return true;
+  }
+  return false;
+}
+
 DiagHooks g_hooks = {hook_init_device, hook_run_early, hook_run_planned, hook_rounds,
-                     hook_units, hook_stream, hook_burst, hook_describe_flat};
+                     hook_units, hook_stream, hook_burst, hook_describe_flat, hook_parity};
 // Installed when the library loads, before any call can initialise a device.
 struct Install {
   Install() { g_diag = &g_hooks; }
@@ -1612,6 +1634,38 @@ void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
 void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
 
 void nova_diag_set_log_window(int records) { g_tune_logwin.store(records); }
+
+// Holds every CU for `us` microseconds: one workgroup per CU with the whole
+// 160 KiB of LDS, spinning on the real-time counter -- a kernel of another
+// library or process that keeps the resident engine (crc32c_engine.hip) off
+// the device, for its take-back tests.  Launched from this library, it does
+// not register as a yield with the product library's engine.
+int nova_diag_hold_cus(uint32_t us, void* stream) {
+  int err = 0;
+  DevTables* t = tables(&err);
+  if (!t) return err;
+  if (us > 5000000) return NOVA_E_INVAL;  // bounded: at most 5 s
+  const int lds = 160 * 1024;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&hold_cus_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(hold_cus_kernel, dim3((uint32_t)t->cus), dim3(64), lds, (hipStream_t)stream,
+                     (uint64_t)us * 100);
+  return (int)hipGetLastError();
+}
+
+// The engine's ticket-group arithmetic (crc32c_internal.hpp), host side, for
+// the CPU test: for a grid of `wgs` workgroups and a request's tickets
+// [cstart, cend): out[0..8) = workgroups per group, out[8..16) = the
+// request's tickets per group, out[16] = groups whose lines complete it.
+int nova_diag_engine_groups(uint32_t wgs, uint64_t cstart, uint64_t cend, uint64_t* out) {
+  if (!out || cend < cstart) return NOVA_E_INVAL;
+  for (uint32_t g = 0; g < 2 * kEngGroups + 1; g++) out[g] = 0;
+  for (uint32_t w = 0; w < wgs; w++) out[engine_group_of_wg(w)]++;
+  for (uint32_t g = 0; g < kEngGroups; g++) out[kEngGroups + g] = engine_group_share(cstart, cend, g);
+  out[2 * kEngGroups] = engine_groups_used(cstart, cend);
+  return 0;
+}
 
 // Copy ceilings (copy_ceiling_kernel): variant = U | NTL << 4 | NTS << 5 |
 // KIND << 8; wgs 0 = one chunk per lane per step over the whole range.

@@ -20,25 +20,53 @@
 //     requests into device-memory slots, maps their ticket pages to them and
 //     publishes their chunk tickets by advancing one end word;
 //   * one poller wave per CU reads the end word and shares it through LDS;
-//     every other wave takes tickets from its XCD's head (eight heads,
-//     MI355X_MICROARCH.md "dequeue"), finds the ticket's request (its cursor
-//     slot and the ticket's page, one round trip), runs the chunk
-//     (engine_chunk: rounds of 4 blocks, all of a block's loads at once),
-//     counts it on its XCD's counter line and only then claims its next
-//     ticket (the claim's add is contended; before the chunk, every load of
-//     the chunk would wait for it);
-//   * the last chunk of an XCD bumps the request's top counter; the last of
+//     every other wave takes tickets from its group's head (eight heads, one
+//     per XCD: group = workgroup index % 8, which is the XCD a workgroup runs
+//     on under the round-robin dispatch; MI355X_MICROARCH.md "dequeue"),
+//     finds the ticket's request (its cursor slot and the ticket's page, one
+//     round trip), runs the chunk (engine_chunk: rounds of 4 blocks, all of a
+//     block's loads at once), counts it on its group's counter line and only
+//     then claims its next ticket (the claim's add is contended; before the
+//     chunk, every load of the chunk would wait for it);
+//   * the last chunk of a group bumps the request's top counter; the last of
 //     those writes the request's completion word in pinned host memory, on
 //     which its submitter spins (a test for >=: the word only grows).
-// Once no request arrives for the idle time (default 1 ms) and every taken
-// request is done, the dispatcher stops the workers and the kernel exits,
-// recording the first request it did not take; a submitter that finds its
-// request untaken relaunches the engine, which starts there.  Every spin is
-// bounded: workers give up (error word) after 20 s without new tickets and no
-// stop, the dispatcher after 20 s with a request unfinished and none new,
-// submitters after NOVA_SST_ENGINE_TIMEOUT_MS; a failed or
-// timed-out request is recomputed by the plain call (crc32c_queue.hip), so
-// results never depend on the engine.
+//
+// Sharing the GPU (round 5).  A resident instance holds ~153 KiB of every
+// CU's LDS, so no other LDS-using kernel can start while it runs.  Every other
+// launch of this library (engine_yield_begin / engine_yield_end around it)
+// bumps a yield word in pinned memory and records an event on its stream.  The
+// dispatcher, once it sees the word differ from its launch value, takes no
+// new request, finishes the ones it took and exits; the next instance is
+// launched behind every registered launch that has not finished
+// (hipStreamWaitEvent), so it cannot take the CUs back from them.  An instance
+// always takes the requests present when it starts (one batch) before it
+// honours a yield: under steady plain traffic every instance still makes
+// progress.
+//
+// Lifetime.  Once no request arrives for the idle time (default 1 ms) and
+// every taken request is done, the dispatcher stops the workers and the kernel
+// exits, recording the first request it did not take; a submitter that finds
+// its request untaken relaunches the engine, which starts there.  Every spin
+// is bounded: workers give up (error word) after 20 s without new tickets and
+// no stop, the dispatcher after 20 s with a request unfinished and none new,
+// submitters after NOVA_SST_ENGINE_TIMEOUT_MS.
+//
+// Taking a request back (round 5).  A submitter whose request
+// fails (timeout, engine error, launch failure) runs the plain call only once
+// the engine can no longer touch the request: it sets the request's cancel
+// word, then
+//   * the instance has not started (its `alive` word is not its generation):
+//     it will read the cancel word when it reaches the request (the instance
+//     stores `alive` and fences before its first ring read, the submitter
+//     stores `cancel` and fences before it reads `alive`), and skips it;
+//   * the instance exited without taking it: later instances skip it;
+//   * otherwise the instance is stopped and the submitter waits for the
+//     request's completion word or the kernel's end.
+// If none of these comes within the hard limit the call returns an error
+// WITHOUT the plain call (the engine may still write the outputs), and the
+// engine is not used again by this process.  Otherwise the engine backs off
+// (100 ms, doubling to 12.8 s, reset by the next success) and is retried.
 //
 // Memory visibility (cdna_hip_programming.md Guideline 16):
 //   * host -> engine: requests and the tail word are read with system-scope
@@ -59,11 +87,14 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstddef>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 
 #include "crc32c_kernels.hpp"
 
@@ -77,7 +108,7 @@ constexpr int kEngG = 16;         // lanes per block (units kernel: G = 16)
 // spilled and measured 5-20 % slower (profiles/r04_engine_conc_v4.log).
 constexpr int kEngMaxWaves = 8;
 constexpr int kEngWaves = 8;
-constexpr uint32_t kCntGroups = 8;
+constexpr uint32_t kCntGroups = kEngGroups;
 constexpr uint32_t kTrWords = 16;
 // Ticket pages: page[p] = the request holding ticket kPage * p (a hint: checked
 // against the slot's ticket range), so a wave finds its ticket's request in
@@ -85,11 +116,32 @@ constexpr uint32_t kTrWords = 16;
 // round trip (an idle wave's cursor lags by every request it sat out).
 constexpr uint32_t kPageShift = 4;
 constexpr uint32_t kPages = 1u << 14;  // 256K tickets covered (wraps: hints only)
+constexpr uint32_t kMaxIdleUs = 1000000;  // below the workers' 20 s give-up
+
+// Exit reasons (EngCtl::why)
+constexpr uint32_t kWhyIdle = 1, kWhyStop = 2, kWhyYield = 3, kWhyLost = 4;
 
 struct EngHostReq {  // a host ring entry (64 B), written by its submitter
   uint64_t base, offs, sizes, out, bad, n;
   uint32_t mode, flags;
-  uint32_t cb, pad;
+  uint32_t cb;
+  uint32_t cancel;  // the submitter took the request back: never run it
+};
+struct EngCtl {  // pinned host memory (fine-grained)
+  uint64_t htail;   // host: requests [first_seq, htail) are in the ring
+  uint32_t hstop;   // host: take no more requests, exit once the taken ones are done
+  uint32_t pad0;
+  uint64_t hyield;  // host: bumped by every non-engine launch of the library (yield)
+  uint64_t pad1[13];
+  uint64_t consumed;  // engine: the first seq it did not take (valid once exited)
+  uint32_t exited;    // engine: this instance takes no more requests
+  uint32_t error;     // engine: give-up code (1: a worker saw no new ticket for the give-up
+                      // time, 2: a published ticket without a slot, 3: a request unfinished
+                      // for the give-up time after the last arrival)
+  uint64_t alive;     // engine: the instance's generation, stored before its first ring read
+  uint32_t why;       // engine: exit reason (kWhy*)
+  uint32_t pad2;
+  uint64_t pad3[12];
 };
 struct EngSlot {  // a device slot (128 B), written by the dispatcher
   uint64_t seq1;          // request seq + 1 (0: never written)
@@ -98,31 +150,22 @@ struct EngSlot {  // a device slot (128 B), written by the dispatcher
   uint32_t mode, flags, cb, pad;
   uint64_t pad2[3];
 };
-struct EngCtl {  // pinned host memory (fine-grained)
-  uint64_t htail;  // host: requests [first_seq, htail) are in the ring
-  uint32_t hstop;  // host: exit once idle
-  uint32_t pad0;
-  uint64_t pad1[14];
-  uint64_t consumed;  // engine: the first seq it did not take (valid once exited)
-  uint32_t exited;    // engine: this instance takes no more requests
-  uint32_t error;     // engine: give-up code (1: a worker saw no new ticket for the give-up
-                      // time, 2: a published ticket without a slot, 3: a request unfinished
-                      // for the give-up time after the last arrival)
-  uint64_t pad2[14];
-};
-struct EngDev {  // device memory, zeroed before every launch
+struct EngDev {  // device memory: all zeroed once; the header before every launch
   uint64_t dend;  // chunk tickets published
   uint64_t p0[15];
   uint32_t dstop;
   uint32_t p1[31];
   uint64_t reqs_done;
   uint64_t p2[15];
+  uint32_t head[kCntGroups][32];  // per-group ticket heads, one 128-B line each
+  // ---- end of the per-launch header.  Below: a slot's counters are zeroed by
+  // the dispatcher when it writes the slot; slots and pages from an earlier
+  // instance hold seqs below the new first_seq, which the lookup never takes.
   // Chunks finished, per slot: one counter per ticket group t % 8 (1/8 of the
   // request's adds per address), then a top counter of the groups whose
-  // chunks are all done.  Same-address atomics
-  // serialize in memory; one counter for all of a 1024-chunk request put
-  // ~1024 of them on the request's critical path.
-  uint32_t head[kCntGroups][32];  // per-XCD ticket heads, one 128-B line each
+  // chunks are all done.  Same-address atomics serialize in memory; one
+  // counter for all of a 1024-chunk request put ~1024 of them on the
+  // request's critical path.
   uint32_t cgrp[kRing][kCntGroups][32];  // 128-B line each
   uint32_t ctop[kRing][32];
   EngSlot slot[kRing];
@@ -132,12 +175,15 @@ struct EngDev {  // device memory, zeroed before every launch
   uint64_t tr[kRing][kTrWords];
   uint64_t page[kPages];     // ticket page -> request seq + 1 (hint)
 };
+constexpr size_t kDevHeader = offsetof(EngDev, cgrp);
 struct EngParams {
   const EngHostReq* hring;
   uint64_t* hdone;  // hdone[seq % kRing] = seq + 1 once the request's results are in memory
   EngCtl* ctl;
   EngDev* dev;
   uint64_t first_seq;
+  uint64_t gen;            // this instance's generation (stored to ctl->alive)
+  uint64_t yield_gen;      // ctl->hyield at launch: any other value is a yield
   uint64_t idle_ticks;     // s_memrealtime ticks (100 MHz) without a request before exiting
   uint64_t give_up_ticks;  // no new ticket (worker) / an unfinished request (dispatcher) this long: exit
   uint64_t* htrace;        // trace (or null): per request, the tr words copied to pinned memory
@@ -196,13 +242,31 @@ constexpr uint32_t poll_off() { return byte_tab_off<G>() + 1024u; }
 __device__ void engine_dispatch(const EngParams& e) {
   const int lane = threadIdx.x & 63;
   EngDev* d = e.dev;
+  // `alive` reaches host memory before any ring entry is read: a submitter
+  // that cancelled a request and then read `alive` as not yet stored knows
+  // this instance will read the cancel word (see the header comment)
+  if (lane == 0) st_sys(&e.ctl->alive, e.gen);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
   uint64_t seen = e.first_seq, cend = 0;
   uint64_t last = now_ticks();
+  bool took = false;
   for (;;) {
-    uint64_t ht = 0;
-    if (lane == 0) ht = ld_sys(&e.ctl->htail);
+    uint64_t ht = 0, yv = 0;
+    uint32_t stop = 0;
+    if (lane == 0) {
+      ht = ld_sys(&e.ctl->htail);
+      stop = ld_sys(&e.ctl->hstop);
+      yv = ld_sys(&e.ctl->hyield);
+    }
     ht = uni64(ht);
-    if (ht > seen) {
+    stop = uni32(stop);
+    yv = uni64(yv);
+    // a yield stops the takes once this instance took its first batch (or
+    // found none): some request moves per instance however often plain
+    // launches arrive
+    const bool yielded = yv != e.yield_gen;
+    const bool drain = stop != 0 || (yielded && (took || ht <= seen));
+    if (!drain && ht > seen) {
       const uint32_t m = (uint32_t)(ht - seen < 64 ? ht - seen : 64);
       EngHostReq r{};
       uint64_t nch = 0;
@@ -217,6 +281,8 @@ __device__ void engine_dispatch(const EngParams& e) {
         r.mode = ld_sys(&h->mode);
         r.flags = ld_sys(&h->flags);
         r.cb = ld_sys(&h->cb);
+        r.cancel = ld_sys(&h->cancel);
+        if (r.cancel) r.n = 0;  // taken back by its submitter: no tickets, done at once
         if (r.cb == 0 || r.cb > 16) r.cb = 16;
         nch = (r.n + r.cb - 1) / r.cb;
       }
@@ -267,15 +333,18 @@ __device__ void engine_dispatch(const EngParams& e) {
       drain_vm();  // every lane's slot and page stores are written through before the end moves
       cend += total;
       if (lane == 0) st_agent(&d->dend, cend);
+      // requests without tickets (taken back, or empty) are done now
+      if ((uint32_t)lane < m && nch == 0) {
+        st_sys(&e.hdone[(seen + lane) % kRing], seen + lane + 1);
+        __hip_atomic_fetch_add((g64*)&d->reqs_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       seen += m;
+      took = true;
       last = now_ticks();
       continue;
     }
-    uint32_t stop = 0;
-    if (lane == 0) stop = ld_sys(&e.ctl->hstop);
-    stop = uni32(stop);
     const uint64_t quiet = now_ticks() - last;
-    if (stop || quiet > e.idle_ticks) {
+    if (drain || quiet > e.idle_ticks) {
       uint64_t done = 0;
       if (lane == 0) done = ld_agent(&d->reqs_done);
       const bool all_done = uni64(done) == seen - e.first_seq;  // every request taken is finished
@@ -284,6 +353,7 @@ __device__ void engine_dispatch(const EngParams& e) {
       if (all_done || lost) {
         if (lane == 0) {
           if (lost) st_sys(&e.ctl->error, 3u);
+          st_sys(&e.ctl->why, lost ? kWhyLost : stop ? kWhyStop : yielded ? kWhyYield : kWhyIdle);
           st_agent(&d->dstop, 1u);
           st_sys(&e.ctl->consumed, seen);
           __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)&e.ctl->exited, 1u,
@@ -377,31 +447,31 @@ __device__ __forceinline__ void engine_chunk(const uint8_t* lds, const CrcParams
     Y.t = gload16((valid && (kTail2 || (u1 & 15) != 0)) ? E : zl);
     if constexpr (kTail2) Y.t2 = gload16(valid && u1 + 4 > E + 16 ? E + 16 : zl);
     uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    // 32-bit positions relative to the lane's first piece: the block's first
-    // byte (head masking) and its first line (pieces before it read zeros)
-    const int64_t ur = (int64_t)(u0 - first), ar = (int64_t)(A0 - first);
-    int32_t urel = ur < -(1 << 20) ? -(1 << 20) : (ur > (1 << 30) ? (1 << 30) : (int32_t)ur);
-    int32_t arel = ar < -(1 << 20) ? -(1 << 20) : (ar > (1 << 30) ? (1 << 30) : (int32_t)ar);
+    // positions relative to the lane's first piece: the block's first byte
+    // (head masking) and its first line (pieces before it read zeros); 64-bit,
+    // since a round may pair a block over 1 GiB with short ones whose start
+    // then lies more than 2^30 bytes after the round's first piece
+    int64_t urel = (int64_t)(u0 - first), arel = (int64_t)(A0 - first);
     for (uint32_t k0 = 0; k0 < Kw; k0 += kEK) {
       uint4 d[kEK];
 #pragma unroll
       for (int i = 0; i < kEK; i++) {
-        const bool in = valid && k0 + i < Kw && (int32_t)(kS * i) >= arel;
+        const bool in = valid && k0 + i < Kw && (int64_t)(kS * i) >= arel;
         d[i] = gload16(in ? first + (uint64_t)i * kS : zl);
       }
       if (k0 == 0 && b0 + kGroups < b_hi) desc(b0 + kGroups, o_nxt, l_nxt);  // under the data loads
 #pragma unroll
       for (int i = 0; i < kEK; i++) {
         if (k0 + i < Kw) {  // wave-uniform
-          const int32_t hr = urel - (int32_t)(kS * i);
-          const int32_t h = hr < -4 ? -4 : (hr > 32 ? 32 : hr);
+          const int64_t hr = urel - (int64_t)(kS * i);
+          const int32_t h = hr < -4 ? -4 : (hr > 32 ? 32 : (int32_t)hr);
           const uint4 w = is_head(h) ? head_piece(d[i], h, Y.ninit) : d[i];
           swath4<0>(lds, c0, c1, c2, c3, w, lo0, lo1, lo2, lo3);
         }
       }
       first += (uint64_t)kEK * kS;  // the next pass
-      urel -= (int32_t)(kEK * kS);
-      arel -= (int32_t)(kEK * kS);
+      urel -= (int64_t)(kEK * kS);
+      arel -= (int64_t)(kEK * kS);
     }
     // fold the group's stream words: in-lane M4/M8, then M16 .. M128 across the group
     uint32_t v = lapply(tree + kTreeBytes, lapply(tree, c0) ^ c1) ^ (lapply(tree, c2) ^ c3);
@@ -446,11 +516,16 @@ template <int G>
 __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   EngDev* d = e.dev;
-  // Tickets t with t % 8 == x go to XCD x's waves, each taking the next from
-  // its XCD's head (dynamic: a request's chunks go to whichever waves are
-  // free; one queue per CU instead made every request wait for the slowest
-  // of 256 queues -- 35 % less at 16 callers).
-  const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & (kCntGroups - 1);
+  // Tickets t with t % 8 == x go to the waves of group x, each taking the
+  // next from its group's head (dynamic: a request's chunks go to whichever
+  // waves are free; one queue per CU instead made every request wait for the
+  // slowest of 256 queues -- 35 % less at 16 callers).  The group is the
+  // workgroup index mod 8: every group has workgroups whatever the device's
+  // XCD count or partition mode (the hardware XCC id may miss values, which
+  // left tickets unclaimed: ADVICE r04), and under the round-robin dispatch
+  // of a full MI355X it is the workgroup's XCD, so each head's line stays in
+  // one XCD's L2.
+  const uint32_t xcc = engine_group_of_wg(blockIdx.x);
   auto claim = [&]() -> uint64_t {
     uint32_t k = 0;
     if (lane == 0)
@@ -521,10 +596,15 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
     // All of a slot's fields are read at once (one round trip), together with
     // t's ticket page; when the cursor's slot does not hold t the page's
     // request is tried next, then slots are walked forward one at a time.
+    // A page is a hint: after a wrap it may name a later request, or one the
+    // dispatcher is still writing (its page store and slot store come from
+    // different lanes, unordered: ADVICE r04) -- any inconsistency met after
+    // following it restarts the walk from the cursor, which is never past t's
+    // request and whose slots were all written before t was published.
     uint64_t cstart = 0, cend = 0, base = 0, offs = 0, sizes = 0, out = 0, bad = 0, n = 0;
     uint32_t mode = 0, flags = 0, cb = 0;
-    bool hinted = false;
-    const uint64_t r0 = r;  // the cursor is never past t's request; a hint may be (it wraps)
+    bool hinted = false, via_hint = false;
+    const uint64_t r0 = r;
     for (;;) {
       const EngSlot* S = &d->slot[r % kRing];
       uint64_t s1 = 0, hint = 0;
@@ -552,6 +632,7 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
         hint = uni64(hint);
         if (!(s1 == r + 1 && t >= uni64(cstart) && t < ce) && hint > r + 1) {
           r = hint - 1;
+          via_hint = true;
           continue;
         }
       }
@@ -565,9 +646,15 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
       }
       if (s1 == r + 1 && t < uni64(cstart)) {  // a stale (wrapped) hint overshot: walk from the cursor
         r = r0;
+        via_hint = false;
         continue;
       }
       if (s1 == r + 1) break;
+      if (via_hint) {  // the hinted slot is not written (yet): walk from the cursor
+        r = r0;
+        via_hint = false;
+        continue;
+      }
       if (lane == 0) st_sys(&e.ctl->error, 2u);  // published tickets with no slot: cannot happen
       return;
     }
@@ -599,12 +686,11 @@ __device__ void engine_work(const EngParams& e, const uint8_t* lds) {
     drain_vm();
     const uint64_t ts_drain = e.htrace ? now_ticks() : 0;
     if (lane == 0) {
-      // the request's tickets are counted per XCD (t % 8), one line each;
-      // this XCD's share: t' in [cstart, cend), t' % 8 == grp
+      // the request's tickets are counted per group (t % 8), one line each;
+      // this group's share: t' in [cstart, cend), t' % 8 == grp
       const uint32_t grp = xcc;
-      auto below = [&](uint64_t n) -> uint64_t { return n > grp ? (n - grp + kCntGroups - 1) / kCntGroups : 0; };
-      const uint64_t mine = below(cend) - below(cstart);
-      const uint64_t groups = cend - cstart < kCntGroups ? cend - cstart : kCntGroups;
+      const uint64_t mine = engine_group_share(cstart, cend, grp);
+      const uint64_t groups = engine_groups_used(cstart, cend);
       const uint32_t prev = __hip_atomic_fetch_add((g32*)&d->cgrp[r % kRing][grp][0], 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t ts_count = e.htrace ? now_ticks() : 0;
@@ -677,6 +763,22 @@ uint64_t env_u64(const char* name, uint64_t def) {
   return end && *end == 0 ? (uint64_t)x : def;
 }
 
+using Clock = std::chrono::steady_clock;
+
+// engine_submit's result when the request could not be taken back: the
+// caller must NOT run the plain call (the engine may still write the outputs)
+constexpr int kEngineUnsafe = -1000;
+// ring-full wait before the request goes to the plain call (nothing published yet)
+constexpr uint64_t kRingWaitMs = 1000;
+
+thread_local uint32_t tl_wait_delay_us = 0;  // test hook: nova_sst_engine_set_wait_delay_us
+
+uint64_t stream_key(hipStream_t s) {
+  if (s == hipStreamPerThread)  // one alias per thread: key by the thread
+    return (std::hash<std::thread::id>{}(std::this_thread::get_id()) << 1) | 1u;
+  return (uint64_t)(uintptr_t)s;
+}
+
 struct Engine {
   std::mutex mu;
   bool ready = false, broken = false, running = false;
@@ -689,11 +791,25 @@ struct Engine {
   EngDev* ddev = nullptr;
   uint64_t next_seq = 0;     // the next request's seq
   uint64_t inst_first = 0;   // the running instance's first seq
-  uint64_t gen = 0;          // instances launched
+  uint64_t gen = 0;          // instances launched (the running one's generation)
   std::atomic<uint64_t> inflight{0};         // requests submitted and not yet returned
   std::atomic<uint64_t> inflight_blocks{0};  // their blocks
   uint64_t requests = 0, relaunches = 0, fallbacks = 0;
+  uint64_t exits[5] = {};  // instance exits by reason (kWhy*), counted at relaunch / stop
+  uint64_t timeouts = 0, errors = 0, taken_back = 0, unsafe = 0, yield_waits = 0;
   uint32_t idle_us = 0, waves = 0;
+  std::atomic<uint32_t> timeout_ms{0};        // 0: NOVA_SST_ENGINE_TIMEOUT_MS (default 10000)
+  std::atomic<uint32_t> failures{0};          // consecutive failed requests (backoff)
+  std::atomic<int64_t> avoid_until_ns{0};     // steady clock: requests go plain until then
+  // Yield registry: the launches this engine must not take the CUs from.
+  // `live` once the pinned control block exists; then every non-engine launch
+  // of the library bumps ygen (stored to ctl->hyield) and records an event on
+  // its stream (the stream's last one is kept).  ymu orders bumps, records and
+  // the relaunch's snapshot (mu, when both are held, is taken first).
+  std::atomic<bool> live{false};
+  std::mutex ymu;
+  uint64_t ygen = 0;
+  std::unordered_map<uint64_t, hipEvent_t> yev;
   // trace (nova_sst_engine_set_trace): per-request spans, summed under tmu
   uint64_t* htrace = nullptr;  // pinned, kRing x kTrWords
   bool trace = false;
@@ -728,6 +844,7 @@ struct Engine {
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&htrace, sizeof(uint64_t) * kTrWords * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess) e = hipMalloc((void**)&ddev, sizeof(EngDev));
+    if (e == hipSuccess) e = hipMemset(ddev, 0, sizeof(EngDev));  // slots: seq1 = 0 (never written)
     if (e == hipSuccess)
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG, kEngMaxWaves>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)engine_lds<kEngG>(kEngMaxWaves));
@@ -740,20 +857,50 @@ struct Engine {
     memset(ring, 0, sizeof(EngHostReq) * kRing);
     memset(hdone, 0, sizeof(uint64_t) * kRing);
     memset(ctl, 0, sizeof(EngCtl));
-    if (!idle_us) idle_us = (uint32_t)env_u64("NOVA_SST_ENGINE_IDLE_US", 1000);
+    if (!idle_us) idle_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_IDLE_US", 1000));
     waves = (uint32_t)env_u64("NOVA_SST_ENGINE_WAVES", kEngWaves);
     if (waves < 2 || waves > (uint32_t)kEngMaxWaves) waves = kEngWaves;
+    // From here on every non-engine launch registers itself.  A launch made
+    // before it saw `live` was enqueued before this store; the device-wide
+    // sync below waits for it, so the first instance cannot take the CUs from it.
+    live.store(true);
+    if ((e = hipDeviceSynchronize()) != hipSuccess) {
+      (void)hipGetLastError();
+      broken = true;
+      return (int)e;
+    }
     ready = true;
     return 0;
+  }
+
+  // Registered launches not yet finished: the engine's stream waits for them
+  // (under ymu), and the instance's yield value is read in the same section,
+  // so a launch registered later changes ctl->hyield for it.
+  uint64_t wait_for_yielded_locked() {
+    std::lock_guard<std::mutex> lk(ymu);
+    for (auto it = yev.begin(); it != yev.end();) {
+      const hipError_t q = hipEventQuery(it->second);
+      if (q == hipErrorNotReady) {
+        if (hipStreamWaitEvent(stream, it->second, 0) == hipSuccess) yield_waits++;
+        ++it;
+      } else if (yev.size() > 256) {  // finished: drop it (bounded map)
+        (void)hipEventDestroy(it->second);
+        it = yev.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    (void)hipGetLastError();
+    return ygen;
   }
 
   // A fresh instance over requests [first, ...): the previous one has exited.
   int launch_locked(uint64_t first) {
     hipError_t e = hipStreamSynchronize(stream);
-    if (e == hipSuccess) e = hipMemsetAsync(ddev, 0, sizeof(EngDev), stream);
+    if (e == hipSuccess) e = hipMemsetAsync(ddev, 0, kDevHeader, stream);
     if (e != hipSuccess) {
       (void)hipGetLastError();
-      broken = true;
+      running = false;
       return (int)e;
     }
     std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -762,16 +909,22 @@ struct Engine {
     c->consumed = 0;
     c->hstop = 0;
     c->error = 0;
+    c->why = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     int err = 0;
     DevTables* t = tables(&err);
-    if (!t) return err;
+    if (!t) {
+      running = false;
+      return err;
+    }
     EngParams p{};
     p.hring = ring;
     p.hdone = hdone;
     p.ctl = ctl;
     p.dev = ddev;
     p.first_seq = first;
+    p.gen = gen + 1;
+    p.yield_gen = wait_for_yielded_locked();
     p.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
     p.give_up_ticks = 20ull * 100000000ull;  // 20 s (every spin of the engine is bounded)
     p.htrace = trace ? htrace : nullptr;
@@ -785,7 +938,7 @@ struct Engine {
                        engine_lds<kEngG>((int)waves), stream, p);
     e = hipGetLastError();
     if (e != hipSuccess) {
-      broken = true;
+      running = false;
       return (int)e;
     }
     inst_first = first;
@@ -794,12 +947,17 @@ struct Engine {
     return 0;
   }
 
-  // The running instance took no more requests (idle exit, or a stop): a
+  // The running instance took no more requests (idle exit, yield or stop): a
   // fresh one starts at the first request it did not take.
   int relaunch_if_exited_locked() {
     volatile EngCtl* c = ctl;
     if (running && !c->exited) return 0;
-    const uint64_t first = running ? c->consumed : inst_first;
+    uint64_t first = inst_first;
+    if (running) {
+      first = c->consumed;
+      const uint32_t why = c->why;
+      exits[why < 5 ? why : 0]++;
+    }
     running = false;
     relaunches++;
     return launch_locked(first);
@@ -809,6 +967,59 @@ struct Engine {
     if (seq < kRing) return true;
     const volatile uint64_t* h = hdone;
     return h[seq % kRing] >= seq - kRing + 1;  // monotone per slot
+  }
+
+  uint32_t timeout() const {
+    static const uint32_t env = (uint32_t)env_u64("NOVA_SST_ENGINE_TIMEOUT_MS", 10000);
+    const uint32_t t = timeout_ms.load();
+    return t ? t : env;
+  }
+
+  // Take request seq back (its submitter failed to get a result): returns 0
+  // once the engine can no longer touch it (the plain call may run), or
+  // kEngineUnsafe.  Under mu: no instance is launched meanwhile.
+  int take_back_locked(uint64_t seq) {
+    volatile EngHostReq* h = ring + seq % kRing;
+    volatile EngCtl* c = ctl;
+    const volatile uint64_t* hd = hdone + seq % kRing;
+    taken_back++;
+    h->cancel = 1;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (*hd >= seq + 1) return 0;           // done or skipped: never touched again
+    if (!running) return 0;                 // no instance: the next one skips it
+    if (c->alive != gen) return 0;          // not started: it will read the cancel word
+    if (c->exited && c->consumed <= seq) return 0;  // exited without taking it
+    // The running instance took it or may: stop it, then wait for the request
+    // (run or skipped) or for the kernel's end.
+    c->hstop = 1;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    const auto t0 = Clock::now();
+    const auto limit = std::chrono::milliseconds(std::max<uint32_t>(timeout(), 30000));
+    for (;;) {
+      if (*hd >= seq + 1) return 0;
+      const hipError_t q = hipStreamQuery(stream);
+      if (q == hipSuccess) return 0;  // the instance (the stream's last work) has ended
+      (void)hipGetLastError();
+      if (Clock::now() - t0 > limit) {
+        unsafe++;
+        broken = true;  // an engine that neither finishes nor ends: not used again
+        return kEngineUnsafe;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+
+  // After a failed request: back off (100 ms, doubling to 12.8 s; reset by a success).
+  void back_off() {
+    const uint32_t f = failures.fetch_add(1) + 1;
+    const int64_t ms = 100ll << std::min<uint32_t>(f - 1, 7);
+    const int64_t until = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              (Clock::now() + std::chrono::milliseconds(ms)).time_since_epoch()).count();
+    avoid_until_ns.store(until);
+  }
+  bool backing_off() const {
+    const int64_t u = avoid_until_ns.load(std::memory_order_relaxed);
+    return u && std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count() < u;
   }
 };
 
@@ -835,16 +1046,15 @@ int engine_stop(Engine& g) {
   if (!g.ready || !g.running) return 0;
   volatile EngCtl* c = g.ctl;
   c->hstop = 1;
-  const auto t0 = std::chrono::steady_clock::now();
+  const auto t0 = Clock::now();
   while (!c->exited) {
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
-      g.broken = true;
-      return NOVA_E_NODEV;
-    }
+    if (Clock::now() - t0 > std::chrono::seconds(10)) return NOVA_E_NODEV;  // still running; retried later
     std::this_thread::yield();
   }
   const hipError_t e = hipStreamSynchronize(g.stream);
   g.inst_first = c->consumed;
+  const uint32_t why = c->why;
+  g.exits[why < 5 ? why : 0]++;
   g.running = false;
   c->hstop = 0;
   return e == hipSuccess ? 0 : (int)e;
@@ -855,22 +1065,81 @@ void stop_all_at_exit() {
     if (g.ready && g.running) (void)engine_stop(g);
 }
 
+Engine* engine_if_live() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  Engine* g = &g_eng[dev];
+  return g->live.load() ? g : nullptr;
+}
+
+void bump_yield_locked(Engine& g) {
+  g.ygen++;
+  reinterpret_cast<volatile uint64_t*>(&g.ctl->hyield)[0] = g.ygen;
+}
+
 }  // namespace
 
 namespace nova_dev {
 
-// Runs one request on the engine and waits for it.  Returns 0, or nonzero when
-// the engine cannot run it (the caller then makes the plain call).
+void engine_yield_begin() {
+  Engine* g = engine_if_live();
+  if (!g) return;
+  std::lock_guard<std::mutex> lk(g->ymu);
+  bump_yield_locked(*g);
+}
+
+void engine_yield_end(hipStream_t s) {
+  Engine* g = engine_if_live();
+  if (!g) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();  // being captured into a graph: nothing to record now
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g->ymu);
+  hipEvent_t& ev = g->yev[stream_key(s)];
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    ev = nullptr;
+    g->yev.erase(stream_key(s));
+    bump_yield_locked(*g);
+    return;
+  }
+  if (hipEventRecord(ev, s) != hipSuccess) (void)hipGetLastError();
+  bump_yield_locked(*g);
+}
+
+void engine_forget_stream(hipStream_t s) {
+  Engine* g = engine_if_live();
+  if (!g) return;
+  std::lock_guard<std::mutex> lk(g->ymu);
+  auto it = g->yev.find(stream_key(s));
+  if (it == g->yev.end()) return;
+  // (the caller synchronised the stream; a stream wait that captured the
+  // event keeps its own reference)
+  (void)hipEventDestroy(it->second);
+  (void)hipGetLastError();
+  g->yev.erase(it);
+}
+
+// Runs one request on the engine and waits for it.  Returns 0; nonzero when
+// the engine did not run it and cannot touch it any more (the caller then
+// makes the plain call); kEngineUnsafe when it could not be taken back (no
+// plain call: an error for the caller).
 int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uint32_t* sizes, uint64_t n,
                   uint32_t flags, void* out, uint32_t* bad) {
   int err = 0;
   Engine* gp = engine_for_device(&err);
   if (!gp) return err;
   Engine& g = *gp;
-  static const uint64_t timeout_ms = env_u64("NOVA_SST_ENGINE_TIMEOUT_MS", 10000);
   // blocks per chunk fixed at 1..16 (0: adaptive, below)
   static const uint32_t cb_fixed = (uint32_t)std::min<uint64_t>(16, env_u64("NOVA_SST_ENGINE_CB", 0));
+  if (g.backing_off()) return NOVA_E_NODEV;
   uint64_t seq = 0;
+  bool failed = false;
   {
     std::unique_lock<std::mutex> lk(g.mu);
     if (g.broken) return NOVA_E_NODEV;
@@ -878,7 +1147,11 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
     (void)hipGetDevice(&dev);
     if ((err = g.init_locked(dev))) return err;
     seq = g.next_seq;
+    const auto tw = Clock::now();
     while (!g.ring_slot_free(seq)) {  // kRing requests in flight: wait for the oldest
+      // (a taken-back request's slot frees once an instance skips it)
+      if ((err = g.relaunch_if_exited_locked()) || Clock::now() - tw > std::chrono::milliseconds(kRingWaitMs))
+        return err ? err : NOVA_E_NODEV;  // nothing published: the plain call is safe
       lk.unlock();
       std::this_thread::yield();
       lk.lock();
@@ -912,60 +1185,72 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
     h->mode = r.mode;
     h->flags = r.flags;
     h->cb = r.cb;
+    h->cancel = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     reinterpret_cast<volatile uint64_t*>(&g.ctl->htail)[0] = seq + 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     g.requests++;
-    if ((err = g.relaunch_if_exited_locked())) {
-      g.inflight.fetch_sub(1);
-      g.inflight_blocks.fetch_sub(n);
-      return err;
+    if (g.relaunch_if_exited_locked()) {
+      g.errors++;
+      failed = true;
     }
   }
+  if (tl_wait_delay_us)  // test hook: this waiter starts late (past a ring turn)
+    std::this_thread::sleep_for(std::chrono::microseconds(tl_wait_delay_us));
   // wait for the completion word; relaunch if the instance exited without
   // taking this request
-  const auto t_submit = std::chrono::steady_clock::now();
+  const auto t_submit = Clock::now();
   const volatile uint64_t* hd = g.hdone + seq % kRing;
   const volatile EngCtl* c = g.ctl;
-  const auto t0 = std::chrono::steady_clock::now();
+  const auto t0 = Clock::now();
+  const uint32_t timeout_ms = g.timeout();
   // The word only grows (seq + 1, then seq + 1 + kRing once this request is
   // done and its ring slot reused), so a waiter descheduled past a full ring
   // turn still sees its request done.
-  for (uint64_t spin = 0;; spin++) {
+  for (uint64_t spin = 0; !failed; spin++) {
     if (*hd >= seq + 1) break;
     if ((spin & 255) == 255) {
       if (c->error) {
         std::lock_guard<std::mutex> lk(g.mu);
-        g.broken = true;
-        g.inflight.fetch_sub(1);
-        g.inflight_blocks.fetch_sub(n);
-        return NOVA_E_NODEV;
+        g.errors++;
+        failed = true;
+        break;
       }
       if (c->exited) {
         std::lock_guard<std::mutex> lk(g.mu);
-        if (*hd < seq + 1 && (err = g.relaunch_if_exited_locked())) {
-          g.inflight.fetch_sub(1);
-          g.inflight_blocks.fetch_sub(n);
-          return err;
+        if (*hd < seq + 1 && g.relaunch_if_exited_locked()) {
+          g.errors++;
+          failed = true;
+          break;
         }
       }
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+      if (Clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
         std::lock_guard<std::mutex> lk(g.mu);
-        g.broken = true;  // later requests take the plain path
-        g.inflight.fetch_sub(1);
-        g.inflight_blocks.fetch_sub(n);
-        return NOVA_E_NODEV;
+        g.timeouts++;
+        failed = true;
+        break;
       }
       if (spin > (1u << 16)) std::this_thread::yield();
     }
     __builtin_ia32_pause();
   }
+  if (failed) {
+    int rc = 0;
+    {
+      std::lock_guard<std::mutex> lk(g.mu);
+      rc = g.take_back_locked(seq);
+    }
+    g.back_off();
+    g.inflight.fetch_sub(1);
+    g.inflight_blocks.fetch_sub(n);
+    return rc ? rc : NOVA_E_NODEV;
+  }
   std::atomic_thread_fence(std::memory_order_acquire);
   g.inflight.fetch_sub(1);
   g.inflight_blocks.fetch_sub(n);
+  if (g.failures.load(std::memory_order_relaxed)) g.failures.store(0);
   if (g.trace) {  // this request's spans (the stamps were stored before its completion word)
-    const double host_us =
-        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_submit).count();
+    const double host_us = std::chrono::duration<double, std::micro>(Clock::now() - t_submit).count();
     const volatile uint64_t* tr = g.htrace + (seq % kRing) * kTrWords;
     const uint64_t t0 = tr[0], t1 = tr[1], t2 = tr[2];
     uint64_t w[12];
@@ -990,6 +1275,8 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   }
   return 0;
 }
+
+bool engine_unsafe(int rc) { return rc == kEngineUnsafe; }
 
 std::atomic<int> g_engine_override{-1};  // nova_sst_engine_set_enabled (-1: NOVA_SST_ENGINE)
 
@@ -1039,6 +1326,22 @@ int nova_sst_engine_stats(uint64_t* requests, uint64_t* launches, uint64_t* fall
   if (launches) *launches = gp->gen;
   if (fallbacks) *fallbacks = gp->fallbacks;
   if (running) *running = gp->running && gp->ctl && !((volatile EngCtl*)gp->ctl)->exited ? 1 : 0;
+  return 0;
+}
+
+int nova_sst_engine_counters(uint64_t* out, size_t n) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  if (!out) return NOVA_E_INVAL;
+  std::lock_guard<std::mutex> lk(gp->mu);
+  const uint64_t v[NOVA_ENGINE_COUNTERS] = {
+      gp->requests, gp->gen, gp->fallbacks,
+      (uint64_t)(gp->running && gp->ctl && !((volatile EngCtl*)gp->ctl)->exited ? 1 : 0),
+      gp->exits[kWhyIdle], gp->exits[kWhyYield], gp->exits[kWhyStop], gp->exits[kWhyLost],
+      gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
+      (uint64_t)gp->broken, (uint64_t)gp->backing_off()};
+  for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
   return 0;
 }
 
@@ -1096,7 +1399,34 @@ int nova_sst_engine_set_idle_us(uint32_t us) {
   Engine* gp = engine_for_device(&err);
   if (!gp) return err;
   std::lock_guard<std::mutex> lk(gp->mu);
-  gp->idle_us = us ? us : 1000;  // the next instance
+  // the next instance; at most 1 s, below the workers' 20 s give-up
+  gp->idle_us = us ? std::min<uint32_t>(us, kMaxIdleUs) : 1000;
+  return 0;
+}
+
+int nova_sst_engine_set_timeout_ms(uint32_t ms) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  gp->timeout_ms.store(ms);
+  return 0;
+}
+
+void nova_sst_engine_set_wait_delay_us(uint32_t us) { tl_wait_delay_us = us; }
+
+int nova_sst_engine_yield(void* stream) {
+  nova_dev::engine_yield_begin();
+  nova_dev::engine_yield_end((hipStream_t)stream);
+  return 0;
+}
+
+int nova_sst_engine_reset(void) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<std::mutex> lk(gp->mu);
+  gp->failures.store(0);
+  gp->avoid_until_ns.store(0);
   return 0;
 }
 

@@ -241,6 +241,42 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
                   uint32_t flags, void* out, uint32_t* bad);
 bool engine_enabled();
 void engine_count_fallback();
+// Engine ticket groups (crc32c_engine.hip): ticket t goes to group t % 8,
+// taken by the waves of the workgroups w with w % 8 == group (every group has
+// workgroups whenever the grid has at least 8); a request's chunk tickets
+// [cstart, cend) hold group_share(cstart, cend, g) tickets of group g, counted
+// on g's completion line, and the request is done when groups_used(...) lines
+// are full.  Host-callable for the CPU test (nova_diag_engine_groups).
+constexpr uint32_t kEngGroups = 8;
+__host__ __device__ inline uint32_t engine_group_of_wg(uint32_t wg) { return wg & (kEngGroups - 1); }
+__host__ __device__ inline uint64_t engine_group_below(uint64_t n, uint32_t g) {
+  return n > g ? (n - g + kEngGroups - 1) / kEngGroups : 0;  // tickets t < n with t % 8 == g
+}
+__host__ __device__ inline uint64_t engine_group_share(uint64_t cstart, uint64_t cend, uint32_t g) {
+  return engine_group_below(cend, g) - engine_group_below(cstart, g);
+}
+__host__ __device__ inline uint64_t engine_groups_used(uint64_t cstart, uint64_t cend) {
+  return cend - cstart < kEngGroups ? cend - cstart : kEngGroups;
+}
+// engine_submit's code for a request the engine could not be made to let go
+// of: the caller returns an error and must not run the plain call.
+bool engine_unsafe(int rc);
+// Sharing the GPU with the engine: every launch of the library that is not the
+// engine's is bracketed by engine_yield_begin (the resident engine starts to
+// drain and exit) and engine_yield_end(stream) once it is enqueued (the next
+// engine instance waits for it).  Both do nothing until the engine of the
+// current device has been started once.  engine_forget_stream drops a
+// released stream's event.
+void engine_yield_begin();
+void engine_yield_end(hipStream_t s);
+void engine_forget_stream(hipStream_t s);
+struct EngineYield {
+  hipStream_t s;
+  explicit EngineYield(hipStream_t st) : s(st) { engine_yield_begin(); }
+  ~EngineYield() { engine_yield_end(s); }
+  EngineYield(const EngineYield&) = delete;
+  EngineYield& operator=(const EngineYield&) = delete;
+};
 int trailer_layout(const CrcParams& p, DevTables* t, hipStream_t stream, uint32_t* elig, uint32_t* flag);
 
 // ---- diagnostics hooks (crc32c_diag.hip fills g_diag; null in the product) --
@@ -259,6 +295,10 @@ struct DiagHooks {
   bool (*burst)(int V, int mode, CrcParams& p, DevTables* t, hipStream_t s, int* rc);
   // nova_crc32c_describe of a flat-kernel plan
   int (*describe_flat)(int G, int mode, char* buf, size_t buflen);
+  // nova_xor_parity: a variant (u chunks per lane, fu fragments per load) the
+  // product does not instantiate (rejected A/B forms, e.g. 16 x 1, which spills)
+  bool (*parity)(int u, int fu, const uint8_t* base, const uint64_t* frag_offsets, uint32_t n_frags,
+                 uint64_t parity_len, uint8_t* out, uint64_t wgs, hipStream_t s, int* rc);
 };
 extern DiagHooks* g_diag;
 

@@ -292,12 +292,14 @@ int enqueue(Req& r, hipStream_t stream) {
   r.stream = stream;
   bool plain = r.n > kMaxBlocks;  // larger than one batch: the plain call (one launch is efficient)
   if (!plain && engine_enabled()) {
-    // the persistent engine (crc32c_engine.hip); if it cannot run the
-    // request, the plain call computes it (after zeroing a verify counter
-    // the engine may have added to)
-    if (engine_submit(r.mode, r.buf, r.offs, r.sizes, r.n, r.flags,
-                      r.mode == kVerify ? (void*)r.ok : nullptr, r.bad) == 0)
-      return 0;
+    // the persistent engine (crc32c_engine.hip); if it did not run the
+    // request and has let go of it, the plain call computes it (after zeroing
+    // a verify counter the engine may have added to)
+    const int erc = engine_submit(r.mode, r.buf, r.offs, r.sizes, r.n, r.flags,
+                                  r.mode == kVerify ? (void*)r.ok : nullptr, r.bad);
+    if (erc == 0) return 0;
+    // the engine may still write this request's outputs: no plain call
+    if (engine_unsafe(erc)) return NOVA_E_NODEV;
     engine_count_fallback();
     if (r.mode == kVerify && r.bad && (e = hipMemsetAsync(r.bad, 0, sizeof(uint32_t), stream)) != hipSuccess)
       return (int)e;

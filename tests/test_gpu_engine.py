@@ -1,0 +1,316 @@
+"""The persistent per-SSTable engine sharing the GPU (round 5):
+yields to other launches of the library, takes failed requests back before any
+plain call, keeps its results exact under mixed callers, and survives a waiter
+that starts late by more than a whole ring turn.
+
+Run on a real MI355X:  python -m pytest tests -m gpu
+"""
+import json
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from novalsm_amd import crc32c as C
+
+pytestmark = pytest.mark.gpu
+
+RING = 1024  # crc32c_engine.hip kRing
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    C.load(build_if_missing=True)
+    assert C.load().nova_device_init() == 0
+    return torch
+
+
+@pytest.fixture
+def engine_on():
+    C.engine_set_enabled(1)
+    C.engine_reset()
+    yield
+    C.engine_set_timeout_ms(0)
+    C.engine_set_idle_us(0)
+    C.engine_reset()
+    C.engine_set_enabled(-1)
+
+
+def _sst_table(torch, oracle, n, seed, victims=()):
+    """An SSTable image (4096+U[0,255] B blocks, StoC trailers) with some blocks
+    corrupted; the oracle's expected flags."""
+    from bench import sst4k_layout
+    offs_np, lens_np, total = sst4k_layout(n, seed)
+    img = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    C.fill_splitmix64(img, 1000 + seed)
+    offs = torch.from_numpy(offs_np.view(np.int64)).cuda()
+    lens = torch.from_numpy(lens_np.view(np.int32)).cuda()
+    C.write_trailers(img, offs, lens)
+    torch.cuda.synchronize()
+    host = img.cpu().numpy()
+    want = np.array([oracle.verify(host[int(o):int(o) + int(ln) + 5].tobytes())
+                     for o, ln in zip(offs_np, lens_np)], np.uint8)
+    assert want.all()
+    for v in victims:
+        img[int(offs_np[v]) + 11] ^= 0x08
+        want[v] = 0
+    torch.cuda.synchronize()
+    return dict(n=n, img=img, offs=offs, lens=lens, offs_np=offs_np, lens_np=lens_np, want=want)
+
+
+def _plain_inputs(torch, oracle):
+    """The plain thread's three calls, with expected results from the oracle:
+    an SSTable verify (2 corrupted blocks), a log verify (3 corrupted records)
+    and a CRC batch of mixed block sizes."""
+    from novalsm_amd.callers import Plain
+    from novalsm_amd.synth import log_image
+    keep = []
+    v = _sst_table(torch, oracle, 2048, 71, victims=(5, 1500))
+    rng = np.random.default_rng(5)
+    plen = rng.integers(0, 700, 20000)
+    host, loffs, _, _ = log_image(13, plen)
+    oracle.log_write(host, loffs)
+    vic = rng.choice(len(loffs), 3, replace=False)
+    for r in vic:
+        host[int(loffs[r]) + 6] ^= 0x02
+    lbuf = torch.from_numpy(host.copy()).cuda()
+    ldoffs = torch.from_numpy(np.asarray(loffs, np.int64)).cuda()
+    lwant = oracle.log_check(host, loffs).astype(np.uint8)
+    lbad = int((lwant == C.LOG_CHECKSUM_MISMATCH).sum())
+    assert lbad == 3
+    bl = rng.choice([4096, 16384, 65536], 600).astype(np.uint32) + rng.integers(1, 64, 600).astype(np.uint32)
+    bo = np.zeros(600, np.uint64)
+    bo[1:] = np.cumsum(bl[:-1].astype(np.uint64))
+    bhost = np.frombuffer(np.random.default_rng(9).bytes(int(bo[-1] + bl[-1]) + 64), np.uint8).copy()
+    bwant = oracle.batch(bhost, bo, bl, None).astype(np.uint32)
+    bbuf = torch.from_numpy(bhost).cuda()
+    bdo = torch.from_numpy(bo.view(np.int64)).cuda()
+    bdl = torch.from_numpy(bl.view(np.int32)).cuda()
+    vwant = np.ascontiguousarray(v["want"])
+    keep += [v, lbuf, ldoffs, lwant, bbuf, bdo, bdl, bwant, vwant]
+    p = Plain(v_img=v["img"].data_ptr(), v_offs=v["offs"].data_ptr(), v_lens=v["lens"].data_ptr(), v_n=v["n"],
+              v_expect_ok=vwant.ctypes.data, v_expect_bad=2,
+              l_img=lbuf.data_ptr(), l_len=len(host), l_offs=ldoffs.data_ptr(), l_n=len(loffs),
+              l_expect=lwant.ctypes.data, l_expect_bad=lbad,
+              b_img=bbuf.data_ptr(), b_offs=bdo.data_ptr(), b_lens=bdl.data_ptr(), b_n=600,
+              b_expect=bwant.ctypes.data, gap_us=0.0)
+    torch.cuda.synchronize()
+    return p, keep
+
+
+@pytest.mark.parametrize("op", ["verify", "trailers"])
+def test_engine_mixed_callers(torch_gpu, oracle, engine_on, op):
+    """8 native threads hammer nova_sst_queue_* on their
+    own 4096-block tables for 1 s while a 9th thread issues plain
+    nova_sstable_verify_blocks, nova_log_verify_records and nova_crc32c_batch
+    calls back to back on its own stream.  Every engine call's result and every
+    plain call's result is exact (sst_callers.cpp checks them natively against
+    expectations taken from the oracle), nothing falls back or times out, the
+    engine yields to the plain calls (its instances exit for them), and the
+    plain calls' largest latency is bounded: 2 ms, the yield's whole budget
+    (the requests the engine had taken, its exit, and the plain call itself)."""
+    from novalsm_amd import callers
+    plain, keep = _plain_inputs(torch_gpu, oracle)
+    r = callers.run(op, 8, 4096, 1.0, "engine", warm_s=0.3, seed=3, plain=plain)
+    print(json.dumps(r))
+    assert r["verified"] and r["wrong_results"] == 0 and r["rc"] == 0, r
+    e, pl = r["engine"], r["plain"]
+    assert e["fallbacks"] == 0 and e["timeouts"] == 0 and e["errors"] == 0 and e["unsafe"] == 0, e
+    assert e["exits_yield"] >= 1, e
+    for name, s in pl.items():
+        assert s["wrong"] == 0, (name, s)
+        assert s["calls"] >= 10, (name, s)
+        assert s["max_us"] <= 2000.0, (name, s)
+    assert r["calls_in_window"] >= 1000, r  # the engine callers kept going
+    del keep
+
+
+def test_engine_yields_to_a_plain_call(torch_gpu, oracle, engine_on):
+    """A resident engine with a long idle time (500 ms) holds every CU's LDS;
+    a plain verify on another stream must not wait for its idle exit: the
+    plain call makes it yield (exits_yield counts it), finishes in well under
+    the idle time, and the next queue call relaunches the engine."""
+    torch = torch_gpu
+    C.engine_stop()
+    C.engine_set_idle_us(500000)
+    tb = _sst_table(torch, oracle, 1024, 33, victims=(7,))
+    ok = torch.empty(tb["n"], dtype=torch.uint8, device="cuda")
+    nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+    C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, nb)
+    assert np.array_equal(ok.cpu().numpy(), tb["want"]) and int(nb.item()) == 1
+    assert C.engine_counters()["running"] == 1
+    c0 = C.engine_counters()
+    s = torch.cuda.Stream()
+    ok2 = torch.empty(tb["n"], dtype=torch.uint8, device="cuda")
+    nb2 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    C.verify_blocks(tb["img"], tb["offs"], tb["lens"], stream=s, ok=ok2, bad=nb2)
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    assert np.array_equal(ok2.cpu().numpy(), tb["want"]) and int(nb2.item()) == 1
+    c1 = C.engine_counters()
+    assert dt < 0.1, dt  # not the 500 ms idle exit
+    time.sleep(0.01)
+    nb.zero_()
+    C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, nb)
+    assert np.array_equal(ok.cpu().numpy(), tb["want"]) and int(nb.item()) == 1
+    c2 = C.engine_counters()
+    assert c2["exits_yield"] - c0["exits_yield"] >= 1, (c0, c1, c2)
+    assert c2["launches"] - c0["launches"] >= 1 and c2["fallbacks"] == c0["fallbacks"], (c0, c2)
+    C.engine_stop()
+
+
+def test_engine_waiter_past_ring_turn(torch_gpu, oracle, engine_on):
+    """VERDICT r04 item 5, the round-4 hang: one caller's waiter starts 400 ms
+    late (nova_sst_engine_set_wait_delay_us), while four other threads complete
+    more than a whole ring turn (1024) of requests, so the caller's ring slot
+    and completion word are reused before it looks.  It must still see its
+    request done (the word only grows: a >= test), with the right flags, no
+    timeout, no fallback and no relaunch storm."""
+    torch = torch_gpu
+    late = _sst_table(torch, oracle, 4096, 21, victims=(100, 4000))
+    small = [_sst_table(torch, oracle, 1, 50 + k) for k in range(4)]
+    c0 = C.engine_counters()
+    res, errors, ends = {}, [], []
+    started = threading.Event()
+
+    def late_caller():
+        try:
+            C.engine_set_wait_delay_us(400000)
+            ok = torch.empty(late["n"], dtype=torch.uint8, device="cuda")
+            nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            started.set()
+            t0 = time.perf_counter()
+            C.queue_verify_blocks(late["img"], late["offs"], late["lens"], ok, nb)
+            res["span"] = (t0, time.perf_counter())
+            res["ok"], res["bad"] = ok.cpu().numpy(), int(nb.item())
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+        finally:
+            C.engine_set_wait_delay_us(0)
+
+    def filler(tb):
+        try:
+            ok = torch.empty(1, dtype=torch.uint8, device="cuda")
+            s = torch.cuda.Stream()
+            started.wait()
+            deadline = time.perf_counter() + 0.38
+            while time.perf_counter() < deadline:
+                C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, stream=s)
+                ends.append(time.perf_counter())
+            if int(ok.cpu()[0]) != 1:
+                errors.append("filler flags")
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=late_caller)] + [threading.Thread(target=filler, args=(tb,)) for tb in small]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    t0, t1 = res["span"]
+    inside = sum(1 for t in ends if t0 < t < t1)
+    assert inside > RING, (inside, len(ends))  # more than a ring turn completed while it slept
+    assert np.array_equal(res["ok"], late["want"]) and res["bad"] == 2
+    c1 = C.engine_counters()
+    assert c1["fallbacks"] == c0["fallbacks"] and c1["timeouts"] == c0["timeouts"], (c0, c1)
+    assert c1["errors"] == c0["errors"] and c1["taken_back"] == c0["taken_back"], (c0, c1)
+    assert c1["launches"] - c0["launches"] <= 3, (c0, c1)
+
+
+def test_engine_take_back_when_held_off(torch_gpu, oracle, engine_on):
+    """a request whose engine cannot run -- here a foreign
+    kernel (nova_diag_hold_cus, another library's, so no yield) holds every
+    CU's LDS for 400 ms -- times out (30 ms) and is taken back before the plain
+    call computes it: results exact, one timeout, one take-back, one fallback.
+    When the held engine instance finally starts it must skip the request:
+    sentinels written into the outputs after the call returned stay untouched.
+    After the backoff the engine serves requests again."""
+    torch = torch_gpu
+    D = C.load_diag()
+    C.engine_stop()
+    tb = _sst_table(torch, oracle, 4096, 44, victims=(9, 3000))
+    ok = torch.empty(tb["n"], dtype=torch.uint8, device="cuda")
+    nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+    C.engine_set_timeout_ms(30)
+    hold = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    assert D.nova_diag_hold_cus(400000, hold.cuda_stream) == 0
+    time.sleep(0.02)  # the hold occupies every CU
+    c0 = C.engine_counters()
+    t0 = time.perf_counter()
+    C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, nb)
+    dt = time.perf_counter() - t0
+    c1 = C.engine_counters()
+    assert np.array_equal(ok.cpu().numpy(), tb["want"]) and int(nb.item()) == 2
+    assert c1["timeouts"] - c0["timeouts"] == 1 and c1["taken_back"] - c0["taken_back"] == 1, (c0, c1)
+    assert c1["fallbacks"] - c0["fallbacks"] == 1 and c1["unsafe"] == c0["unsafe"], (c0, c1)
+    assert c1["backing_off"] == 1 and not c1["broken"], c1
+    assert dt > 0.2, dt  # the plain call itself waited for the hold
+    ok.fill_(0xEE)
+    nb.fill_(12345)
+    torch.cuda.synchronize()
+    hold.synchronize()
+    time.sleep(0.3)  # the held instance has started and skipped the request
+    torch.cuda.synchronize()
+    assert (ok.cpu().numpy() == 0xEE).all() and int(nb.item()) == 12345
+    C.engine_set_timeout_ms(0)
+    C.engine_reset()
+    nb.zero_()
+    C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, nb)
+    assert np.array_equal(ok.cpu().numpy(), tb["want"]) and int(nb.item()) == 2
+    c2 = C.engine_counters()
+    assert c2["fallbacks"] == c1["fallbacks"] and c2["requests"] - c1["requests"] == 1, (c1, c2)
+    C.engine_stop()
+
+
+def test_engine_stop_under_traffic(torch_gpu, oracle, engine_on):
+    """nova_sst_engine_stop while four threads keep calling: the stop takes
+    effect (the dispatcher stops taking requests even though new ones keep
+    arriving), returns, and the callers' next requests relaunch the engine;
+    every result exact, nothing falls back."""
+    torch = torch_gpu
+    tabs = [_sst_table(torch, oracle, 512, 60 + k, victims=(k,)) for k in range(4)]
+    stop = threading.Event()
+    errors, counts = [], [0] * 4
+    c0 = C.engine_counters()
+
+    def caller(k):
+        try:
+            tb = tabs[k]
+            s = torch.cuda.Stream()
+            ok = torch.empty(tb["n"], dtype=torch.uint8, device="cuda")
+            nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+            while not stop.is_set():
+                with torch.cuda.stream(s):
+                    nb.zero_()
+                    C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, nb, stream=s)
+                    if not np.array_equal(ok.cpu().numpy(), tb["want"]) or int(nb.item()) != 1:
+                        errors.append(k)
+                        return
+                counts[k] += 1
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=caller, args=(k,)) for k in range(4)]
+    for x in th:
+        x.start()
+    for _ in range(5):
+        time.sleep(0.05)
+        C.engine_stop()
+    time.sleep(0.05)
+    stop.set()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    c1 = C.engine_counters()
+    assert c1["exits_stop"] - c0["exits_stop"] >= 3, (c0, c1)
+    assert c1["fallbacks"] == c0["fallbacks"] and c1["timeouts"] == c0["timeouts"], (c0, c1)
+    assert min(counts) > 0, counts

@@ -61,9 +61,9 @@ def test_product_kernels_use_no_scratch(lib):
     the gfx950 code objects in the built .so, tools/kernel_meta.py).  Round 3:
     a whole-uint4 select in the rounds kernel's head masking went through a
     private array and every launch ran 2.4x slower; the units kernel spilled
-    5-7 VGPRs at a 16-wave launch bound it never launched with.  The one
-    exception is xor_parity_kernel<16,1>, a measured-and-rejected variant
-    reachable only through the diagnostics knob."""
+    5-7 VGPRs at a 16-wave launch bound it never launched with.  No
+    exceptions: the one rejected form that spills, xor_parity_kernel<16,1>,
+    lives in the diagnostics library since round 5."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import kernel_meta
@@ -72,13 +72,13 @@ def test_product_kernels_use_no_scratch(lib):
     ks = kernel_meta.kernels(os.path.join(ROOT, "novalsm_amd", "lib", "libnova_crc32c.so"))
     assert len(ks) >= 40
     assert any("crc32c_rounds_kernel" in k for k in ks) and any("crc32c_stream_kernel" in k for k in ks)
-    bad = {k: v for k, v in ks.items()
-           if (v["private"] or v["vgpr_spill"]) and "xor_parity_kernelILi16ELi1E" not in k}
+    bad = {k: v for k, v in ks.items() if v["private"] or v["vgpr_spill"]}
     assert not bad, bad
+    assert not any("xor_parity_kernelILi16ELi1E" in k for k in ks)
 
 
 def test_abi_version(lib):
-    assert lib.nova_crc32c_abi_version() == C.ABI_VERSION == 3
+    assert lib.nova_crc32c_abi_version() == C.ABI_VERSION == 4
 
 
 def test_standard_results():
