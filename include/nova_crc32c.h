@@ -162,6 +162,11 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
  * requests already taken.  Kernels of OTHER libraries are
  * not seen: call nova_sst_engine_yield(stream) after enqueuing them on
  * `stream` (or keep the engine off with nova_sst_engine_set_enabled(0)).
+ * Other streams' work is never queued behind the resident kernel: it is
+ * launched cooperatively, which HIP runs on a hardware queue of its own
+ * (NOVA_SST_ENGINE_QUEUE).  A device-wide sync
+ * (hipDeviceSynchronize) waits for the running instance, which exits after
+ * at most one time slice (nova_sst_engine_set_slice_us, default 2 ms).
  * Work queued on `stream` before the call (the image, its descriptors)
  * completes first: the call synchronises `stream` when it is busy.  A table
  * of more than 2^20 blocks runs as the plain call on `stream`, and so does a
@@ -201,9 +206,16 @@ int nova_sst_engine_set_idle_us(uint32_t us);
  * exits after the idle time, for a yield, for a stop, giving up on a request;
  * requests timed out, engine errors, requests taken back, requests that could
  * not be taken back; relaunches that waited for a yielded launch, yield bumps;
- * disabled for good, backing off now. */
-#define NOVA_ENGINE_COUNTERS 16
+ * disabled for good, backing off now; instance exits at the end of a time
+ * slice (NOVA_SST_ENGINE_SLICE_US). */
+#define NOVA_ENGINE_COUNTERS 17
 int nova_sst_engine_counters(uint64_t* out, size_t n);
+/* Time slice of an engine instance in us, from the next instance (0: back to
+ * NOVA_SST_ENGINE_SLICE_US, default 2000; 0xFFFFFFFF: none).  An instance
+ * takes no request after running this long, finishes the ones it took and
+ * exits; the next one follows at once.  Bounds what a device-wide sync and
+ * another library's kernels wait under steady traffic. */
+int nova_sst_engine_set_slice_us(uint32_t us);
 /* Host timeout for one engine request (0: NOVA_SST_ENGINE_TIMEOUT_MS). */
 int nova_sst_engine_set_timeout_ms(uint32_t ms);
 /* Make the resident engine yield to work the caller enqueued on `stream`

@@ -72,6 +72,7 @@ _SIG = {
     "nova_sst_engine_trace_detail": (_i32, [_vp, _vp]),
     "nova_sst_engine_counters": (_i32, [_vp, _sz]),
     "nova_sst_engine_set_timeout_ms": (_i32, [_u32]),
+    "nova_sst_engine_set_slice_us": (_i32, [_u32]),
     "nova_sst_engine_yield": (_i32, [_vp]),
     "nova_sst_engine_reset": (_i32, []),
     "nova_sst_engine_set_wait_delay_us": (None, [_u32]),
@@ -454,7 +455,7 @@ def engine_stats() -> dict:
 
 ENGINE_COUNTERS = ("requests", "launches", "fallbacks", "running", "exits_idle", "exits_yield",
                    "exits_stop", "exits_lost", "timeouts", "errors", "taken_back", "unsafe",
-                   "yield_waits", "yield_bumps", "broken", "backing_off")
+                   "yield_waits", "yield_bumps", "broken", "backing_off", "exits_slice")
 
 
 def engine_counters() -> dict:
@@ -462,6 +463,13 @@ def engine_counters() -> dict:
     v = (ctypes.c_uint64 * len(ENGINE_COUNTERS))()
     _check(_L().nova_sst_engine_counters(v, len(ENGINE_COUNTERS)), "nova_sst_engine_counters")
     return dict(zip(ENGINE_COUNTERS, [int(x) for x in v]))
+
+
+def engine_set_slice_us(us: int) -> None:
+    """Engine instance time slice in us from the next instance (0: the
+    NOVA_SST_ENGINE_SLICE_US default; None: no slice)."""
+    v = 0xFFFFFFFF if us is None else int(us)
+    _check(_L().nova_sst_engine_set_slice_us(v), "nova_sst_engine_set_slice_us")
 
 
 def engine_set_timeout_ms(ms: int) -> None:

@@ -95,6 +95,7 @@
 #include <mutex>
 #include <thread>
 #include <unordered_map>
+#include <vector>
 
 #include "crc32c_kernels.hpp"
 
@@ -119,7 +120,8 @@ constexpr uint32_t kPages = 1u << 14;  // 256K tickets covered (wraps: hints onl
 constexpr uint32_t kMaxIdleUs = 1000000;  // below the workers' 20 s give-up
 
 // Exit reasons (EngCtl::why)
-constexpr uint32_t kWhyIdle = 1, kWhyStop = 2, kWhyYield = 3, kWhyLost = 4;
+constexpr uint32_t kWhyIdle = 1, kWhyStop = 2, kWhyYield = 3, kWhyLost = 4, kWhySlice = 5;
+constexpr uint32_t kWhyN = 6;
 
 struct EngHostReq {  // a host ring entry (64 B), written by its submitter
   uint64_t base, offs, sizes, out, bad, n;
@@ -141,7 +143,8 @@ struct EngCtl {  // pinned host memory (fine-grained)
   uint64_t alive;     // engine: the instance's generation, stored before its first ring read
   uint32_t why;       // engine: exit reason (kWhy*)
   uint32_t pad2;
-  uint64_t pad3[12];
+  uint64_t dbg[4];    // engine: at exit, the yield word seen, the launch's, the quiet ticks, the idle ticks
+  uint64_t pad3[8];
 };
 struct EngSlot {  // a device slot (128 B), written by the dispatcher
   uint64_t seq1;          // request seq + 1 (0: never written)
@@ -186,6 +189,7 @@ struct EngParams {
   uint64_t yield_gen;      // ctl->hyield at launch: any other value is a yield
   uint64_t idle_ticks;     // s_memrealtime ticks (100 MHz) without a request before exiting
   uint64_t give_up_ticks;  // no new ticket (worker) / an unfinished request (dispatcher) this long: exit
+  uint64_t slice_ticks;    // 0, or: take no request after running this long (then exit; the next instance follows)
   uint64_t* htrace;        // trace (or null): per request, the tr words copied to pinned memory
   CrcParams tab;           // tables and zero line for every chunk
 };
@@ -249,6 +253,7 @@ __device__ void engine_dispatch(const EngParams& e) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
   uint64_t seen = e.first_seq, cend = 0;
   uint64_t last = now_ticks();
+  const uint64_t born = last;
   bool took = false;
   for (;;) {
     uint64_t ht = 0, yv = 0;
@@ -265,7 +270,8 @@ __device__ void engine_dispatch(const EngParams& e) {
     // found none): some request moves per instance however often plain
     // launches arrive
     const bool yielded = yv != e.yield_gen;
-    const bool drain = stop != 0 || (yielded && (took || ht <= seen));
+    const bool sliced = e.slice_ticks && took && now_ticks() - born > e.slice_ticks;
+    const bool drain = stop != 0 || sliced || (yielded && (took || ht <= seen));
     if (!drain && ht > seen) {
       const uint32_t m = (uint32_t)(ht - seen < 64 ? ht - seen : 64);
       EngHostReq r{};
@@ -353,7 +359,11 @@ __device__ void engine_dispatch(const EngParams& e) {
       if (all_done || lost) {
         if (lane == 0) {
           if (lost) st_sys(&e.ctl->error, 3u);
-          st_sys(&e.ctl->why, lost ? kWhyLost : stop ? kWhyStop : yielded ? kWhyYield : kWhyIdle);
+          st_sys(&e.ctl->why, lost ? kWhyLost : stop ? kWhyStop : yielded ? kWhyYield : sliced ? kWhySlice : kWhyIdle);
+          st_sys(&e.ctl->dbg[0], yv);
+          st_sys(&e.ctl->dbg[1], e.yield_gen);
+          st_sys(&e.ctl->dbg[2], quiet);
+          st_sys(&e.ctl->dbg[3], e.idle_ticks);
           st_agent(&d->dstop, 1u);
           st_sys(&e.ctl->consumed, seen);
           __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)&e.ctl->exited, 1u,
@@ -795,7 +805,10 @@ struct Engine {
   std::atomic<uint64_t> inflight{0};         // requests submitted and not yet returned
   std::atomic<uint64_t> inflight_blocks{0};  // their blocks
   uint64_t requests = 0, relaunches = 0, fallbacks = 0;
-  uint64_t exits[5] = {};  // instance exits by reason (kWhy*), counted at relaunch / stop
+  uint64_t exits[kWhyN] = {};  // instance exits by reason (kWhy*), counted at relaunch / stop
+  int queue_mode = 0;          // NOVA_SST_ENGINE_QUEUE (see init_locked)
+  uint32_t slice_us = 0;       // NOVA_SST_ENGINE_SLICE_US / nova_sst_engine_set_slice_us
+  bool slice_set = false;      // set through the API
   uint64_t timeouts = 0, errors = 0, taken_back = 0, unsafe = 0, yield_waits = 0;
   uint32_t idle_us = 0, waves = 0;
   std::atomic<uint32_t> timeout_ms{0};        // 0: NOVA_SST_ENGINE_TIMEOUT_MS (default 10000)
@@ -834,7 +847,40 @@ struct Engine {
       const uint64_t want = env_u64("NOVA_SST_ENGINE_CUS", 0);
       if (want >= 8 && want < (uint64_t)cus) cus = (int)(want & ~7ull);
     }
-    hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+    // NOVA_SST_ENGINE_QUEUE: how the instance reaches the device.  HIP maps
+    // streams onto GPU_MAX_HW_QUEUES shared hardware queues (4 by default),
+    // whose packets run in order: work of any stream that shares the
+    // engine's queue waits behind the resident kernel -- for as long as
+    // requests keep arriving (tools/queue_probe.py: a torch op on such a
+    // stream waited 1.6 s).  1 (default): the instance is launched as a
+    // cooperative kernel, which the runtime sends to a queue of its own,
+    // and the stream stays non-blocking (the probe: 16 streams and the null
+    // stream unaffected); 0: a plain launch on a non-blocking stream (shared
+    // queue: a stream behind the instance waits up to one time slice, below);
+    // 2: a stream with a CU mask of every CU (a queue of its own, but a
+    // blocking stream: the null stream waits for the engine -- measured, not
+    // used).  A cooperative launch that fails falls back to 0.
+    queue_mode = (int)env_u64("NOVA_SST_ENGINE_QUEUE", 1);
+    // NOVA_SST_ENGINE_SLICE_US (default 2000): an instance takes no request
+    // after running this long; it finishes the ones it took and exits, and the
+    // next request's waiter launches the next instance.  A device-wide sync
+    // (hipDeviceSynchronize, torch.cuda.synchronize) waits for the work each
+    // stream had when it was called -- the running instance, not its
+    // successors -- and a kernel of another library waiting for CUs gets them
+    // at the instance boundary: both wait about one slice at most under
+    // steady traffic, instead of until the traffic stops.  0: no slice.
+    if (!slice_set)
+      slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 2000));
+    hipError_t e = hipSuccess;
+    if (queue_mode == 2) {
+      int phys = 0;
+      (void)hipDeviceGetAttribute(&phys, hipDeviceAttributeMultiprocessorCount, d);
+      std::vector<uint32_t> mask((uint32_t)std::max(phys, 1) / 32 + 1, 0u);
+      for (int c = 0; c < phys; c++) mask[c / 32] |= 1u << (c % 32);
+      e = hipExtStreamCreateWithCUMask(&stream, (uint32_t)mask.size(), mask.data());
+    } else {
+      e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+    }
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&ring, sizeof(EngHostReq) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
@@ -927,6 +973,7 @@ struct Engine {
     p.yield_gen = wait_for_yielded_locked();
     p.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
     p.give_up_ticks = 20ull * 100000000ull;  // 20 s (every spin of the engine is bounded)
+    p.slice_ticks = (uint64_t)slice_us * 100;
     p.htrace = trace ? htrace : nullptr;
     p.tab.tab_main = t->main[gindex(kEngG)];
     p.tab.tab_tree = t->tree;
@@ -934,9 +981,21 @@ struct Engine {
     p.tab.tab_sh16 = t->sh16;
     p.tab.tab_byte = t->byte8;  // M_1 byte table (tail bytes)
     p.tab.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
-    hipLaunchKernelGGL((crc32c_engine_kernel<kEngG, kEngMaxWaves>), dim3((uint32_t)cus), dim3(64 * waves),
-                       engine_lds<kEngG>((int)waves), stream, p);
-    e = hipGetLastError();
+    if (queue_mode == 1) {
+      void* args[] = {&p};
+      e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG, kEngMaxWaves>),
+                                     dim3((uint32_t)cus), dim3(64 * waves), args,
+                                     (unsigned)engine_lds<kEngG>((int)waves), stream);
+      if (e != hipSuccess) {  // not available: plain launches (time-sliced like the others)
+        (void)hipGetLastError();
+        queue_mode = 0;
+      }
+    }
+    if (queue_mode != 1) {
+      hipLaunchKernelGGL((crc32c_engine_kernel<kEngG, kEngMaxWaves>), dim3((uint32_t)cus), dim3(64 * waves),
+                         engine_lds<kEngG>((int)waves), stream, p);
+      e = hipGetLastError();
+    }
     if (e != hipSuccess) {
       running = false;
       return (int)e;
@@ -956,7 +1015,7 @@ struct Engine {
     if (running) {
       first = c->consumed;
       const uint32_t why = c->why;
-      exits[why < 5 ? why : 0]++;
+      exits[why < kWhyN ? why : 0]++;
     }
     running = false;
     relaunches++;
@@ -1054,7 +1113,7 @@ int engine_stop(Engine& g) {
   const hipError_t e = hipStreamSynchronize(g.stream);
   g.inst_first = c->consumed;
   const uint32_t why = c->why;
-  g.exits[why < 5 ? why : 0]++;
+  g.exits[why < kWhyN ? why : 0]++;
   g.running = false;
   c->hstop = 0;
   return e == hipSuccess ? 0 : (int)e;
@@ -1340,8 +1399,18 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
       (uint64_t)(gp->running && gp->ctl && !((volatile EngCtl*)gp->ctl)->exited ? 1 : 0),
       gp->exits[kWhyIdle], gp->exits[kWhyYield], gp->exits[kWhyStop], gp->exits[kWhyLost],
       gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
-      (uint64_t)gp->broken, (uint64_t)gp->backing_off()};
+      (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice]};
   for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
+  return 0;
+}
+
+int nova_sst_engine_debug(uint64_t* out) {  // temporary: the last exit's words
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp || !gp->ctl) return NOVA_E_NODEV;
+  volatile EngCtl* c = gp->ctl;
+  out[0] = c->why; out[1] = c->exited; out[2] = c->dbg[0]; out[3] = c->dbg[1]; out[4] = c->dbg[2];
+  out[5] = c->dbg[3]; out[6] = gp->ygen; out[7] = c->hyield; out[8] = c->consumed;
   return 0;
 }
 
@@ -1401,6 +1470,22 @@ int nova_sst_engine_set_idle_us(uint32_t us) {
   std::lock_guard<std::mutex> lk(gp->mu);
   // the next instance; at most 1 s, below the workers' 20 s give-up
   gp->idle_us = us ? std::min<uint32_t>(us, kMaxIdleUs) : 1000;
+  return 0;
+}
+
+int nova_sst_engine_set_slice_us(uint32_t us) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<std::mutex> lk(gp->mu);
+  // from the next instance; ~0u: no slice; 0: back to NOVA_SST_ENGINE_SLICE_US
+  if (us == 0) {
+    gp->slice_set = false;
+    gp->slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 2000));
+  } else {
+    gp->slice_set = true;
+    gp->slice_us = us == ~0u ? 0u : std::min<uint32_t>(us, kMaxIdleUs);
+  }
   return 0;
 }
 

@@ -425,7 +425,7 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
   const char* cn[NOVA_ENGINE_COUNTERS] = {"requests", "launches", "fallbacks", "running", "exits_idle",
                                           "exits_yield", "exits_stop", "exits_lost", "timeouts", "errors",
                                           "taken_back", "unsafe", "yield_waits", "yield_bumps", "broken",
-                                          "backing_off"};
+                                          "backing_off", "exits_slice"};
   for (int i = 0; i < NOVA_ENGINE_COUNTERS; i++) {
     if (i == 3 || i == 14 || i == 15) continue;  // states, not counts
     char b[64];
