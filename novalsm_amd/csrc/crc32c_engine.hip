@@ -14,11 +14,12 @@
 //   * one workgroup per CU (8 waves) stays resident with the M_256 tables in
 //     LDS (G = 16 lanes per block);
 //   * a submitting thread writes its request (image, descriptor arrays,
-//     outputs, op, blocks per chunk) into a ring in pinned host memory and
-//     bumps a tail word;
-//   * wave 0 of workgroup 0 -- the dispatcher -- polls the tail, copies new
-//     requests into device-memory slots, maps their ticket pages to them and
-//     publishes their chunk tickets by advancing one end word;
+//     outputs, op, blocks per chunk) into a ring in pinned host memory, as
+//     tagged 8-byte words, and bumps a tail word;
+//   * wave 0 of workgroup 0 -- the dispatcher -- polls the next entry's words
+//     and the tail in one round trip, copies new requests into device-memory
+//     slots, maps their ticket pages to them and publishes their chunk
+//     tickets by advancing one end word;
 //   * one poller wave per CU reads the end word and shares it through LDS;
 //     every other wave takes tickets from its group's head (eight heads, one
 //     per XCD: group = workgroup index % 8, which is the XCD a workgroup runs
@@ -123,11 +124,23 @@ constexpr uint32_t kMaxIdleUs = 1000000;  // below the workers' 20 s give-up (AD
 constexpr uint32_t kWhyIdle = 1, kWhyStop = 2, kWhyYield = 3, kWhyLost = 4, kWhySlice = 5;
 constexpr uint32_t kWhyN = 6;
 
-struct EngHostReq {  // a host ring entry (64 B), written by its submitter
+// A host ring entry (128 B), written by its submitter: 12 words, each
+// (tag << 32) | a 32-bit half of a field, tag = low 32 bits of seq + 1.  The
+// dispatcher polls the next entry's 12 words with one 8-B load per lane, in
+// the same round trip as the tail, stop, yield and cancel words: an entry
+// whose 12 tags are all its seq + 1 is complete (each word is one 8-B store
+// and one 8-B load, so a half-written entry shows stale tags), and is taken
+// without a second round trip over PCIe.
+enum EngWord : uint32_t {
+  kWBaseLo, kWBaseHi, kWOffsLo, kWOffsHi, kWSizesLo, kWSizesHi, kWOutLo, kWOutHi, kWBadLo, kWBadHi,
+  kWN, kWPacked, kWords  // kWPacked: flags (bits 0-15) | mode << 16 | blocks per chunk << 20
+};
+struct EngHostReq {
+  uint64_t w[16];
+};
+struct EngReq {  // an entry, decoded
   uint64_t base, offs, sizes, out, bad, n;
-  uint32_t mode, flags;
-  uint32_t cb;
-  uint32_t cancel;  // the submitter took the request back: never run it
+  uint32_t mode, flags, cb;
 };
 struct EngCtl {  // pinned host memory (fine-grained)
   uint64_t htail;   // host: requests [first_seq, htail) are in the ring
@@ -143,8 +156,7 @@ struct EngCtl {  // pinned host memory (fine-grained)
   uint64_t alive;     // engine: the instance's generation, stored before its first ring read
   uint32_t why;       // engine: exit reason (kWhy*)
   uint32_t pad2;
-  uint64_t dbg[4];    // engine: at exit, the yield word seen, the launch's, the quiet ticks, the idle ticks
-  uint64_t pad3[8];
+  uint64_t pad3[12];
 };
 struct EngSlot {  // a device slot (128 B), written by the dispatcher
   uint64_t seq1;          // request seq + 1 (0: never written)
@@ -181,6 +193,7 @@ struct EngDev {  // device memory: all zeroed once; the header before every laun
 constexpr size_t kDevHeader = offsetof(EngDev, cgrp);
 struct EngParams {
   const EngHostReq* hring;
+  const uint64_t* hcancel;  // hcancel[seq % kRing] == seq + 1: its submitter took the request back
   uint64_t* hdone;  // hdone[seq % kRing] = seq + 1 once the request's results are in memory
   EngCtl* ctl;
   EngDev* dev;
@@ -243,7 +256,7 @@ template <int G>
 constexpr uint32_t poll_off() { return byte_tab_off<G>() + 1024u; }
 
 // Wave 0 of workgroup 0: host ring -> device slots, tickets published.
-__device__ void engine_dispatch(const EngParams& e) {
+__device__ __forceinline__ void engine_dispatch(const EngParams& e) {
   const int lane = threadIdx.x & 63;
   EngDev* d = e.dev;
   // `alive` reaches host memory before any ring entry is read: a submitter
@@ -256,39 +269,94 @@ __device__ void engine_dispatch(const EngParams& e) {
   const uint64_t born = last;
   bool took = false;
   for (;;) {
-    uint64_t ht = 0, yv = 0;
-    uint32_t stop = 0;
-    if (lane == 0) {
-      ht = ld_sys(&e.ctl->htail);
-      stop = ld_sys(&e.ctl->hstop);
-      yv = ld_sys(&e.ctl->hyield);
+    // one round trip: lanes 0-11 the words of entry `seen`, lane 12 its cancel
+    // word, 13 the tail, 14 the stop word, 15 the yield word
+    uint64_t x = 0;
+    {
+      const uint64_t* a = nullptr;
+      if (lane < (int)kWords) a = &e.hring[seen % kRing].w[lane];
+      else if (lane == 12) a = &e.hcancel[seen % kRing];
+      else if (lane == 13) a = &e.ctl->htail;
+      else if (lane == 14) a = reinterpret_cast<const uint64_t*>(&e.ctl->hstop);  // hstop | pad0 << 32
+      else if (lane == 15) a = &e.ctl->hyield;
+      if (lane < 16) x = ld_sys(a);
     }
-    ht = uni64(ht);
-    stop = uni32(stop);
-    yv = uni64(yv);
+    const uint32_t tag0 = (uint32_t)(seen + 1);
+    const bool first_ready =
+        (__builtin_amdgcn_ballot_w64(lane < (int)kWords && (uint32_t)(x >> 32) == tag0) & 0xfffull) == 0xfffull;
+    auto lane64 = [&](int l) -> uint64_t {
+      return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+    };
+    const uint64_t ht = lane64(13);
+    const uint32_t stop = (uint32_t)lane64(14);
+    const uint64_t yv = lane64(15);
+    const bool avail = first_ready || ht > seen;
     // a yield stops the takes once this instance took its first batch (or
     // found none): some request moves per instance however often plain
     // launches arrive
     const bool yielded = yv != e.yield_gen;
     const bool sliced = e.slice_ticks && took && now_ticks() - born > e.slice_ticks;
-    const bool drain = stop != 0 || sliced || (yielded && (took || ht <= seen));
-    if (!drain && ht > seen) {
-      const uint32_t m = (uint32_t)(ht - seen < 64 ? ht - seen : 64);
-      EngHostReq r{};
-      uint64_t nch = 0;
-      if ((uint32_t)lane < m) {
-        const EngHostReq* h = e.hring + (seen + lane) % kRing;
-        r.base = ld_sys(&h->base);
-        r.offs = ld_sys(&h->offs);
-        r.sizes = ld_sys(&h->sizes);
-        r.out = ld_sys(&h->out);
-        r.bad = ld_sys(&h->bad);
-        r.n = ld_sys(&h->n);
-        r.mode = ld_sys(&h->mode);
-        r.flags = ld_sys(&h->flags);
-        r.cb = ld_sys(&h->cb);
-        r.cancel = ld_sys(&h->cancel);
-        if (r.cancel) r.n = 0;  // taken back by its submitter: no tickets, done at once
+    const bool drain = stop != 0 || sliced || (yielded && (took || !avail));
+    if (!drain && avail) {
+      // one request (the common case): decoded from the poll; more: every
+      // lane reads its own entry (a second round trip), taken up to the
+      // first that is not complete yet
+      uint32_t m = 1;
+      EngReq r{};
+      uint64_t cancel = 0, nch = 0;
+      bool mine = lane == 0;
+      if (first_ready && ht <= seen + 1) {
+        auto half = [&](uint32_t k) -> uint64_t { return (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)k); };
+        if (lane == 0) {
+          r.base = half(kWBaseLo) | half(kWBaseHi) << 32;
+          r.offs = half(kWOffsLo) | half(kWOffsHi) << 32;
+          r.sizes = half(kWSizesLo) | half(kWSizesHi) << 32;
+          r.out = half(kWOutLo) | half(kWOutHi) << 32;
+          r.bad = half(kWBadLo) | half(kWBadHi) << 32;
+          r.n = half(kWN);
+          const uint32_t pk = (uint32_t)half(kWPacked);
+          r.flags = pk & 0xffffu;
+          r.mode = (pk >> 16) & 0xfu;
+          r.cb = pk >> 20;
+          cancel = lane64(12);
+        }
+      } else {
+        const uint32_t want = (uint32_t)(ht - seen < 64 ? ht - seen : 64);
+        bool ok = false;
+        if ((uint32_t)lane < want) {
+          const uint64_t seq = seen + lane;
+          const EngHostReq* h = e.hring + seq % kRing;
+          uint64_t w[kWords];
+#pragma unroll
+          for (uint32_t k = 0; k < kWords; k++) w[k] = ld_sys(&h->w[k]);
+          cancel = ld_sys(&e.hcancel[seq % kRing]);
+          ok = true;
+#pragma unroll
+          for (uint32_t k = 0; k < kWords; k++) ok = ok && (uint32_t)(w[k] >> 32) == (uint32_t)(seq + 1);
+          r.base = (uint32_t)w[kWBaseLo] | (uint64_t)(uint32_t)w[kWBaseHi] << 32;
+          r.offs = (uint32_t)w[kWOffsLo] | (uint64_t)(uint32_t)w[kWOffsHi] << 32;
+          r.sizes = (uint32_t)w[kWSizesLo] | (uint64_t)(uint32_t)w[kWSizesHi] << 32;
+          r.out = (uint32_t)w[kWOutLo] | (uint64_t)(uint32_t)w[kWOutHi] << 32;
+          r.bad = (uint32_t)w[kWBadLo] | (uint64_t)(uint32_t)w[kWBadHi] << 32;
+          r.n = (uint32_t)w[kWN];
+          const uint32_t pk = (uint32_t)w[kWPacked];
+          r.flags = pk & 0xffffu;
+          r.mode = (pk >> 16) & 0xfu;
+          r.cb = pk >> 20;
+        }
+        // the complete entries from `seen` on (lane 0's is, by the tail)
+        const uint64_t notok = ~__builtin_amdgcn_ballot_w64(ok);
+        m = notok ? (uint32_t)__builtin_ctzll(notok) : 64u;
+        if (m > want) m = want;
+        if (m == 0) {  // (the tail ran ahead of a word's visibility: poll again)
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        mine = (uint32_t)lane < m;
+      }
+      if (mine) {
+        if (cancel == seen + lane + 1) r.n = 0;  // taken back by its submitter: no tickets, done at once
         if (r.cb == 0 || r.cb > 16) r.cb = 16;
         nch = (r.n + r.cb - 1) / r.cb;
       }
@@ -360,10 +428,6 @@ __device__ void engine_dispatch(const EngParams& e) {
         if (lane == 0) {
           if (lost) st_sys(&e.ctl->error, 3u);
           st_sys(&e.ctl->why, lost ? kWhyLost : stop ? kWhyStop : yielded ? kWhyYield : sliced ? kWhySlice : kWhyIdle);
-          st_sys(&e.ctl->dbg[0], yv);
-          st_sys(&e.ctl->dbg[1], e.yield_gen);
-          st_sys(&e.ctl->dbg[2], quiet);
-          st_sys(&e.ctl->dbg[3], e.idle_ticks);
           st_agent(&d->dstop, 1u);
           st_sys(&e.ctl->consumed, seen);
           __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)&e.ctl->exited, 1u,
@@ -523,7 +587,7 @@ __device__ __forceinline__ void engine_chunk(const uint8_t* lds, const CrcParams
 
 // Every other wave: tickets -> chunks (engine_chunk).
 template <int G>
-__device__ void engine_work(const EngParams& e, const uint8_t* lds) {
+__device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   EngDev* d = e.dev;
   // Tickets t with t % 8 == x go to the waves of group x, each taking the
@@ -796,6 +860,7 @@ struct Engine {
   int cus = 0;
   hipStream_t stream = nullptr;
   EngHostReq* ring = nullptr;  // pinned
+  uint64_t* hcancel = nullptr; // pinned: seq + 1 of a request taken back
   uint64_t* hdone = nullptr;   // pinned
   EngCtl* ctl = nullptr;       // pinned
   EngDev* ddev = nullptr;
@@ -886,6 +951,8 @@ struct Engine {
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&hdone, sizeof(uint64_t) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
+      e = hipHostMalloc((void**)&hcancel, sizeof(uint64_t) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess)
       e = hipHostMalloc((void**)&ctl, sizeof(EngCtl), hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&htrace, sizeof(uint64_t) * kTrWords * kRing, hipHostMallocCoherent | hipHostMallocMapped);
@@ -902,6 +969,7 @@ struct Engine {
     }
     memset(ring, 0, sizeof(EngHostReq) * kRing);
     memset(hdone, 0, sizeof(uint64_t) * kRing);
+    memset(hcancel, 0, sizeof(uint64_t) * kRing);
     memset(ctl, 0, sizeof(EngCtl));
     if (!idle_us) idle_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_IDLE_US", 1000));
     waves = (uint32_t)env_u64("NOVA_SST_ENGINE_WAVES", kEngWaves);
@@ -965,6 +1033,7 @@ struct Engine {
     }
     EngParams p{};
     p.hring = ring;
+    p.hcancel = hcancel;
     p.hdone = hdone;
     p.ctl = ctl;
     p.dev = ddev;
@@ -1038,11 +1107,10 @@ struct Engine {
   // once the engine can no longer touch it (the plain call may run), or
   // kEngineUnsafe.  Under mu: no instance is launched meanwhile.
   int take_back_locked(uint64_t seq) {
-    volatile EngHostReq* h = ring + seq % kRing;
     volatile EngCtl* c = ctl;
     const volatile uint64_t* hd = hdone + seq % kRing;
     taken_back++;
-    h->cancel = 1;
+    reinterpret_cast<volatile uint64_t*>(hcancel)[seq % kRing] = seq + 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     if (*hd >= seq + 1) return 0;           // done or skipped: never touched again
     if (!running) return 0;                 // no instance: the next one skips it
@@ -1217,34 +1285,20 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
       seq = g.next_seq;
     }
     g.next_seq = seq + 1;
-    // blocks per chunk: one round per wave when the request is alone (latency),
-    // four rounds when others are in flight (fewer tickets, longer streams)
     g.inflight.fetch_add(1);
     const uint64_t blocks = g.inflight_blocks.fetch_add(n) + n;
-    EngHostReq r{};
-    r.base = (uint64_t)base;
-    r.offs = (uint64_t)offs;
-    r.sizes = (uint64_t)sizes;
-    r.out = (uint64_t)out;
-    r.bad = (uint64_t)bad;
-    r.n = n;
-    r.mode = (uint32_t)mode;
-    r.flags = flags;
     // blocks per chunk: 4 (one round of the chunk body) per 16K blocks in
     // flight -- short chunks (latency) when the engine is quiet, longer ones
     // (fewer tickets per block) when it is busy (tools/concurrent_sst.py sweep)
-    r.cb = cb_fixed ? cb_fixed : (uint32_t)std::min<uint64_t>(16, 4 * ((blocks + 16383) / 16384));
-    volatile EngHostReq* h = g.ring + seq % kRing;
-    h->base = r.base;
-    h->offs = r.offs;
-    h->sizes = r.sizes;
-    h->out = r.out;
-    h->bad = r.bad;
-    h->n = r.n;
-    h->mode = r.mode;
-    h->flags = r.flags;
-    h->cb = r.cb;
-    h->cancel = 0;
+    const uint32_t cb = cb_fixed ? cb_fixed : (uint32_t)std::min<uint64_t>(16, 4 * ((blocks + 16383) / 16384));
+    const uint32_t half[kWords] = {
+        (uint32_t)(uint64_t)base, (uint32_t)((uint64_t)base >> 32), (uint32_t)(uint64_t)offs,
+        (uint32_t)((uint64_t)offs >> 32), (uint32_t)(uint64_t)sizes, (uint32_t)((uint64_t)sizes >> 32),
+        (uint32_t)(uint64_t)out, (uint32_t)((uint64_t)out >> 32), (uint32_t)(uint64_t)bad,
+        (uint32_t)((uint64_t)bad >> 32), (uint32_t)n, (flags & 0xffffu) | ((uint32_t)mode << 16) | (cb << 20)};
+    const uint64_t tag = (uint64_t)(uint32_t)(seq + 1) << 32;
+    volatile uint64_t* w = g.ring[seq % kRing].w;
+    for (uint32_t k = 0; k < kWords; k++) w[k] = tag | half[k];  // one 8-B store each
     std::atomic_thread_fence(std::memory_order_seq_cst);
     reinterpret_cast<volatile uint64_t*>(&g.ctl->htail)[0] = seq + 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -1401,16 +1455,6 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
       gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
       (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice]};
   for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
-  return 0;
-}
-
-int nova_sst_engine_debug(uint64_t* out) {  // temporary: the last exit's words
-  int err = 0;
-  Engine* gp = engine_for_device(&err);
-  if (!gp || !gp->ctl) return NOVA_E_NODEV;
-  volatile EngCtl* c = gp->ctl;
-  out[0] = c->why; out[1] = c->exited; out[2] = c->dbg[0]; out[3] = c->dbg[1]; out[4] = c->dbg[2];
-  out[5] = c->dbg[3]; out[6] = gp->ygen; out[7] = c->hyield; out[8] = c->consumed;
   return 0;
 }
 
