@@ -1472,7 +1472,11 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
   // the load side (empty steps) until it is: no stage ever runs out of order.
   constexpr uint32_t kNone = 0xffffffffu;  // no chunk (chunk ids fit 32 bits: n < 2^38)
   uint32_t t_rec = 0, t_olo = 0, t_ohi = 0, t_len = 0, t_aux = 0;
-  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0, h4 = 0, h5 = 0, h6 = 0;
+  // log records: the header's bytes 3-6 (length LE16 at bits 8-23, type at
+  // 24-31) and, for verify, bytes 0-3 (the stored masked CRC), as two
+  // unaligned dword loads (gfx950 takes them whole: two registers and two
+  // loads per record instead of seven byte loads)
+  uint32_t hw0 = 0, hw1 = 0;
   uint64_t n_u0 = 0, c_u0 = 0;
   uint32_t n_n = 0, n_rec = 0, n_aux = 0, c_n = 0, c_rec = 0, c_aux = 0;
   uint32_t t_ok = 0, n_ok = 0, c_ok = 0;  // slot holds a block of the batch
@@ -1588,15 +1592,9 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
         // a header past its log block / the image is not read (bounds, status)
         const uint64_t o = ((uint64_t)t_ohi << 32) | t_olo;
         const uint8_t* h = log_header_fits(o, p.buf_len) ? (const uint8_t*)a : p.zline;
-        h4 = h[4];
-        h5 = h[5];
-        if constexpr (MODE == kLogVerify) {
-          h0 = h[0];
-          h1 = h[1];
-          h2 = h[2];
-          h3 = h[3];
-          h6 = h[6];
-        }
+        typedef __attribute__((address_space(1))) const uint32_t __attribute__((aligned(1))) gu32u;
+        hw1 = *(gu32u*)(h + 3);
+        if constexpr (MODE == kLogVerify) hw0 = *(gu32u*)h;
         stage = 4;
       } else {
         n_u0 = a;
@@ -1626,15 +1624,15 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
     } else if (st == 4) {
       const uint64_t o = ((uint64_t)t_ohi << 32) | t_olo;
       n_u0 = base + o + 6;  // CRC input: type byte + payload
-      const uint32_t length = h4 | (h5 << 8);  // db/log_format.h:27-30
+      const uint32_t length = (hw1 >> 8) & 0xffffu;  // db/log_format.h:27-30
       const uint32_t ls = log_header_fits(o, p.buf_len)
-                              ? log_status(o, length, MODE == kLogVerify ? h6 : 1u, p.buf_len)
+                              ? log_status(o, length, MODE == kLogVerify ? hw1 >> 24 : 1u, p.buf_len)
                               : log_nohdr_status(o, p.buf_len);
       n_n = ls == NOVA_LOG_OK ? 1u + length : 0u;  // 0: not read, n_aux = status
       // kVarOutPos: results go to the record's position in p.perm's order
       // (dense per chunk); log_unperm_kernel moves them to the records
       n_rec = (VAR & kVarOutPos) ? t_chunk * C + my : t_rec;
-      n_aux = ls == NOVA_LOG_OK ? (MODE == kLogWrite ? t_aux : (h0 | (h1 << 8) | (h2 << 16) | (h3 << 24)))
+      n_aux = ls == NOVA_LOG_OK ? (MODE == kLogWrite ? t_aux : hw0)
                                 : ls;
       n_chunk = t_chunk;
       if constexpr (kBatch) {
@@ -1812,7 +1810,7 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatT
     } else {
       asm volatile("" ::"v"(t_rec));
       if constexpr (kLog)
-        asm volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(h4), "v"(h5), "v"(h6));
+        asm volatile("" ::"v"(hw0), "v"(hw1));
       if constexpr (kBatch && !kLog) {  // stage 3's tail loads, for stage 4
         asm volatile("" ::"v"(t_tl.x), "v"(t_tl.y), "v"(t_tl.z), "v"(t_tl.w));
         if constexpr (kTail2) asm volatile("" ::"v"(t_t2));
