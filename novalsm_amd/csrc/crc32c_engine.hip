@@ -29,9 +29,10 @@
 //     block's loads at once), counts it on its group's counter line and only
 //     then claims its next ticket (the claim's add is contended; before the
 //     chunk, every load of the chunk would wait for it);
-//   * the last chunk of a group bumps the request's top counter; the last of
-//     those writes the request's completion word in pinned host memory, on
-//     which its submitter spins (a test for >=: the word only grows).
+//   * the last chunk of a group writes that group's completion word of the
+//     request in pinned host memory (the dispatcher writes those of groups
+//     without tickets); the submitter spins until all 8 are set (a test for
+//     >=: the words only grow).
 //
 // Sharing the GPU (round 5).  A resident instance holds ~153 KiB of every
 // CU's LDS, so no other LDS-using kernel can start while it runs.  Every other
@@ -177,12 +178,13 @@ struct EngDev {  // device memory: all zeroed once; the header before every laun
   // the dispatcher when it writes the slot; slots and pages from an earlier
   // instance hold seqs below the new first_seq, which the lookup never takes.
   // Chunks finished, per slot: one counter per ticket group t % 8 (1/8 of the
-  // request's adds per address), then a top counter of the groups whose
-  // chunks are all done.  Same-address atomics serialize in memory; one
-  // counter for all of a 1024-chunk request put ~1024 of them on the
-  // request's critical path.
+  // request's adds per address).  Same-address atomics serialize in memory;
+  // one counter for all of a 1024-chunk request put ~1024 of them on the
+  // request's critical path.  The group whose count completes stores its own
+  // completion word in host memory (hdone, 8 per request): a second-level
+  // counter of the groups -- one more dependent device atomic on every
+  // request's critical path -- is not needed.
   uint32_t cgrp[kRing][kCntGroups][32];  // 128-B line each
-  uint32_t ctop[kRing][32];
   EngSlot slot[kRing];
   // trace (s_memrealtime): 0 dispatched, 2 last chunk done; chunk 0's wave:
   // 3 ticket seen, 1 slot found, 4 body done, 5 drained, 6 counted; the last
@@ -194,7 +196,10 @@ constexpr size_t kDevHeader = offsetof(EngDev, cgrp);
 struct EngParams {
   const EngHostReq* hring;
   const uint64_t* hcancel;  // hcancel[seq % kRing] == seq + 1: its submitter took the request back
-  uint64_t* hdone;  // hdone[seq % kRing] = seq + 1 once the request's results are in memory
+  // hdone[(seq % kRing) * 8 + g] = seq + 1 once group g's results of the request
+  // are in memory (groups without tickets: at publication); the request is
+  // done when all 8 are
+  uint64_t* hdone;
   EngCtl* ctl;
   EngDev* dev;
   uint64_t first_seq;
@@ -268,6 +273,7 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
   uint64_t last = now_ticks();
   const uint64_t born = last;
   bool took = false;
+  uint64_t auto_done = 0;  // group completions of groups without tickets (reqs_done counts the rest)
   for (;;) {
     // one round trip: lanes 0-11 the words of entry `seen`, lane 12 its cancel
     // word, 13 the tail, 14 the stop word, 15 the yield word
@@ -373,7 +379,6 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
         EngSlot* S = &d->slot[seq % kRing];
         // the slot's previous request (seq - kRing) is done: its counters are free
         for (uint32_t x = 0; x < kCntGroups; x++) st_agent(&d->cgrp[seq % kRing][x][0], 0u);
-        st_agent(&d->ctop[seq % kRing][0], 0u);
         st_agent(&S->cstart, cend + inc - nch);
         st_agent(&S->cend, cend + inc);
         st_agent(&S->base, r.base);
@@ -407,11 +412,20 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
       drain_vm();  // every lane's slot and page stores are written through before the end moves
       cend += total;
       if (lane == 0) st_agent(&d->dend, cend);
-      // requests without tickets (taken back, or empty) are done now
-      if ((uint32_t)lane < m && nch == 0) {
-        st_sys(&e.hdone[(seen + lane) % kRing], seen + lane + 1);
-        __hip_atomic_fetch_add((g64*)&d->reqs_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // groups without tickets in a request (all 8 for one taken back) are
+      // done now; they count toward the dispatcher's expected completions
+      uint32_t idle_groups = 0;
+      if ((uint32_t)lane < m) {
+        const uint64_t seq = seen + lane;
+        const uint64_t cs = cend - total + inc - nch, ce = cend - total + inc;
+        for (uint32_t g = 0; g < kCntGroups; g++)
+          if (engine_group_share(cs, ce, g) == 0) {
+            st_sys(&e.hdone[(seq % kRing) * kCntGroups + g], seq + 1);
+            idle_groups++;
+          }
       }
+      for (int s = 32; s >= 1; s >>= 1) idle_groups += (uint32_t)__shfl_xor((int)idle_groups, s);
+      auto_done += uni32(idle_groups);
       seen += m;
       took = true;
       last = now_ticks();
@@ -421,7 +435,8 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
     if (drain || quiet > e.idle_ticks) {
       uint64_t done = 0;
       if (lane == 0) done = ld_agent(&d->reqs_done);
-      const bool all_done = uni64(done) == seen - e.first_seq;  // every request taken is finished
+      // every request taken is finished: all 8 groups of each
+      const bool all_done = uni64(done) + auto_done == kCntGroups * (seen - e.first_seq);
       // a request unfinished long after the last arrival cannot finish: give up
       const bool lost = !all_done && quiet > e.give_up_ticks;
       if (all_done || lost) {
@@ -764,7 +779,6 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
       // this group's share: t' in [cstart, cend), t' % 8 == grp
       const uint32_t grp = xcc;
       const uint64_t mine = engine_group_share(cstart, cend, grp);
-      const uint64_t groups = engine_groups_used(cstart, cend);
       const uint32_t prev = __hip_atomic_fetch_add((g32*)&d->cgrp[r % kRing][grp][0], 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t ts_count = e.htrace ? now_ticks() : 0;
@@ -776,12 +790,11 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
         st_agent(&w[5], ts_drain);
         st_agent(&w[6], ts_count);
       }
-      if ((uint64_t)prev + 1 == mine &&
-          (uint64_t)__hip_atomic_fetch_add((g32*)&d->ctop[r % kRing][0], 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT) + 1 == groups) {
-        // the request's last chunk: every other chunk's wave drained its
-        // results before its add, this one before its own
-        if (e.htrace) {
+      if ((uint64_t)prev + 1 == mine) {
+        // the group's last chunk of the request: every other chunk of the
+        // group drained its results before its add, this one before its own
+        if (e.htrace && grp == (uint32_t)((cend - 1) % kCntGroups)) {
+          // (trace: the group of the request's last ticket stands for "last")
           uint64_t* w = d->tr[r % kRing];
           st_agent(&w[2], now_ticks());
           st_agent(&w[7], ts_seen);
@@ -793,7 +806,7 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
           for (uint32_t k = 0; k < 12; k++) st_sys(&e.htrace[(r % kRing) * kTrWords + k], ld_agent(&w[k]));
           drain_vm();
         }
-        st_sys(&e.hdone[r % kRing], r + 1);
+        st_sys(&e.hdone[(r % kRing) * kCntGroups + grp], r + 1);
         __hip_atomic_fetch_add((g64*)&d->reqs_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -949,7 +962,7 @@ struct Engine {
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&ring, sizeof(EngHostReq) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
-      e = hipHostMalloc((void**)&hdone, sizeof(uint64_t) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
+      e = hipHostMalloc((void**)&hdone, sizeof(uint64_t) * kRing * kCntGroups, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&hcancel, sizeof(uint64_t) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
@@ -968,7 +981,7 @@ struct Engine {
       return (int)e;
     }
     memset(ring, 0, sizeof(EngHostReq) * kRing);
-    memset(hdone, 0, sizeof(uint64_t) * kRing);
+    memset(hdone, 0, sizeof(uint64_t) * kRing * kCntGroups);
     memset(hcancel, 0, sizeof(uint64_t) * kRing);
     memset(ctl, 0, sizeof(EngCtl));
     if (!idle_us) idle_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_IDLE_US", 1000));
@@ -1091,11 +1104,15 @@ struct Engine {
     return launch_locked(first);
   }
 
-  bool ring_slot_free(uint64_t seq) const {
-    if (seq < kRing) return true;
-    const volatile uint64_t* h = hdone;
-    return h[seq % kRing] >= seq - kRing + 1;  // monotone per slot
+  // Request seq's 8 group completion words all hold seq + 1 or more (each
+  // only grows: seq + 1, then a later occupant's seq + 1 + k * kRing).
+  bool done(uint64_t seq) const {
+    const volatile uint64_t* h = hdone + (seq % kRing) * kCntGroups;
+    bool all = true;
+    for (uint32_t g = 0; g < kCntGroups; g++) all = all && h[g] >= seq + 1;
+    return all;
   }
+  bool ring_slot_free(uint64_t seq) const { return seq < kRing || done(seq - kRing); }
 
   uint32_t timeout() const {
     static const uint32_t env = (uint32_t)env_u64("NOVA_SST_ENGINE_TIMEOUT_MS", 10000);
@@ -1108,11 +1125,10 @@ struct Engine {
   // kEngineUnsafe.  Under mu: no instance is launched meanwhile.
   int take_back_locked(uint64_t seq) {
     volatile EngCtl* c = ctl;
-    const volatile uint64_t* hd = hdone + seq % kRing;
     taken_back++;
     reinterpret_cast<volatile uint64_t*>(hcancel)[seq % kRing] = seq + 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    if (*hd >= seq + 1) return 0;           // done or skipped: never touched again
+    if (done(seq)) return 0;                // done or skipped: never touched again
     if (!running) return 0;                 // no instance: the next one skips it
     if (c->alive != gen) return 0;          // not started: it will read the cancel word
     if (c->exited && c->consumed <= seq) return 0;  // exited without taking it
@@ -1123,7 +1139,7 @@ struct Engine {
     const auto t0 = Clock::now();
     const auto limit = std::chrono::milliseconds(std::max<uint32_t>(timeout(), 30000));
     for (;;) {
-      if (*hd >= seq + 1) return 0;
+      if (done(seq)) return 0;
       const hipError_t q = hipStreamQuery(stream);
       if (q == hipSuccess) return 0;  // the instance (the stream's last work) has ended
       (void)hipGetLastError();
@@ -1313,15 +1329,14 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   // wait for the completion word; relaunch if the instance exited without
   // taking this request
   const auto t_submit = Clock::now();
-  const volatile uint64_t* hd = g.hdone + seq % kRing;
   const volatile EngCtl* c = g.ctl;
   const auto t0 = Clock::now();
   const uint32_t timeout_ms = g.timeout();
-  // The word only grows (seq + 1, then seq + 1 + kRing once this request is
+  // The words only grow (seq + 1, then seq + 1 + kRing once this request is
   // done and its ring slot reused), so a waiter descheduled past a full ring
   // turn still sees its request done.
   for (uint64_t spin = 0; !failed; spin++) {
-    if (*hd >= seq + 1) break;
+    if (g.done(seq)) break;
     if ((spin & 255) == 255) {
       if (c->error) {
         std::lock_guard<std::mutex> lk(g.mu);
@@ -1331,7 +1346,7 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
       }
       if (c->exited) {
         std::lock_guard<std::mutex> lk(g.mu);
-        if (*hd < seq + 1 && g.relaunch_if_exited_locked()) {
+        if (!g.done(seq) && g.relaunch_if_exited_locked()) {
           g.errors++;
           failed = true;
           break;
