@@ -508,6 +508,59 @@ int device_extend(uint32_t crc, const char* buf, size_t size, uint32_t* out) {
   return 0;
 }
 
+// nova_crc32c_stream_host's pipelined form (NOVA_STREAM_HOST_PIPE).
+int stream_host_pipe(const void* host_base, uint64_t stride, uint32_t len, size_t n_blocks, uint32_t* host_out,
+                     uint32_t flags, size_t chunk_blocks, int nb, size_t span, size_t chunk_span, HostReg& hr) {
+  (void)span;
+  (void)hr;  // (registered by the caller for the whole call)
+  Streams st;
+  int rc = st.get(2);
+  if (rc) return rc;
+  hipStream_t sc = st.s[0], sk = st.s[1];  // copy, compute
+  std::vector<DevBuf> dbuf(nb), dout(nb);
+  std::vector<hipEvent_t> landed(nb, nullptr), freed(nb, nullptr);
+  PinBuf pout;
+  rc = pout.ensure(n_blocks * 4);
+  for (int b = 0; b < nb && !rc; b++) {
+    rc = dbuf[b].ensure(chunk_span);
+    if (!rc) rc = dout[b].ensure(chunk_blocks * 4);
+    if (!rc && (hipEventCreateWithFlags(&landed[b], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&freed[b], hipEventDisableTiming) != hipSuccess))
+      rc = NOVA_E_NOMEM;
+  }
+  const uint8_t* hb = static_cast<const uint8_t*>(host_base);
+  size_t k = 0;
+  for (size_t b0 = 0; b0 < n_blocks && !rc; b0 += chunk_blocks, k++) {
+    const size_t m = (n_blocks - b0 < chunk_blocks) ? n_blocks - b0 : chunk_blocks;
+    const int b = (int)(k % (size_t)nb);
+    const size_t bytes = (m - 1) * stride + len;
+    hipError_t e = hipSuccess;
+    if (k >= (size_t)nb) e = hipStreamWaitEvent(sc, freed[b], 0);  // its previous chunk was read
+    if (e == hipSuccess) e = hipMemcpyAsync(dbuf[b].p, hb + b0 * stride, bytes, hipMemcpyHostToDevice, sc);
+    if (e == hipSuccess) e = hipEventRecord(landed[b], sc);
+    if (e == hipSuccess) e = hipStreamWaitEvent(sk, landed[b], 0);
+    if (e != hipSuccess) {
+      rc = (int)e;
+      break;
+    }
+    rc = nova_crc32c_batch_strided(dbuf[b].p, stride, len, m, nullptr, static_cast<uint32_t*>(dout[b].p), flags,
+                                   sk);
+    if (rc) break;
+    e = hipMemcpyAsync(static_cast<uint32_t*>(pout.p) + b0, dout[b].p, m * 4, hipMemcpyDeviceToHost, sk);
+    if (e == hipSuccess) e = hipEventRecord(freed[b], sk);
+    if (e != hipSuccess) rc = (int)e;
+  }
+  const int rs = st.sync();
+  if (!rc) rc = rs;
+  for (int b = 0; b < nb; b++) {
+    if (landed[b]) (void)hipEventDestroy(landed[b]);
+    if (freed[b]) (void)hipEventDestroy(freed[b]);
+  }
+  if (rc) (void)hipGetLastError();
+  if (!rc) std::memcpy(host_out, pout.p, n_blocks * 4);
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -526,6 +579,16 @@ int nova_crc32c_stream_host(const void* host_base, uint64_t stride, uint32_t len
   HostReg hr;
   if ((err = hr.reg(host_base, span))) return err;
   const size_t chunk_span = (chunk_blocks - 1) * stride + len;
+  // NOVA_STREAM_HOST_PIPE (default 1): every H2D copy on ONE copy stream,
+  // back to back, so the link is fed as by a single large copy; a compute
+  // stream runs each chunk's kernel once its copy has landed (an event) and
+  // copies its CRCs back; n_streams device buffers rotate, a copy into one
+  // waiting for the kernel that read it before (an event).  0: the round-1
+  // form, each of n_streams streams copying, checksumming and returning its
+  // own chunks (copies from several streams compete for the link).
+  static const bool pipe = env_size("NOVA_STREAM_HOST_PIPE", 1) != 0;
+  if (pipe) return stream_host_pipe(host_base, stride, len, n_blocks, host_out, flags, chunk_blocks,
+                                    std::max(2, n_streams), span, chunk_span, hr);
   Streams st;
   if ((err = st.get(n_streams))) return err;
   std::vector<DevBuf> dbuf(n_streams), dout(n_streams);
