@@ -10,3 +10,9 @@ python3 -c "
 import json; d=json.loads(open('gpurun_out/logbench.log').read().strip().splitlines()[-1])
 print('primary', d['config']['workload'][:30], d['roofline']['frac'])
 for s in d['secondary']: print(s['config'], s.get('frac'), s.get('kernel'))"
+for pipe in 1 0 1; do
+  NOVA_STREAM_HOST_PIPE=$pipe timeout -k 10 300 python -u bench.py --config 5 --steps 5 --warmup 1 > gpurun_out/cfg5_pipe$pipe.log 2>&1 || { tail -5 gpurun_out/cfg5_pipe$pipe.log; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/cfg5_pipe$pipe.log').read().strip().splitlines()[-1]); r=d['roofline']
+print('cfg5 pipe=$pipe', d['value'], 'GiB/s frac', r['frac'], 'ceiling', r['ceiling']['forms'], d['verified_sample'])"
+done
