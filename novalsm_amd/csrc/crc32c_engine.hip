@@ -113,10 +113,14 @@ constexpr int kEngMaxWaves = 8;
 constexpr int kEngWaves = 8;
 constexpr uint32_t kCntGroups = kEngGroups;
 constexpr uint32_t kTrWords = 16;
-// Ticket pages: page[p] = the request holding ticket kPage * p (a hint: checked
-// against the slot's ticket range), so a wave finds its ticket's request in
-// one or two round trips instead of walking its cursor forward one slot per
-// round trip (an idle wave's cursor lags by every request it sat out).
+// Ticket pages: page[p] holds a copy of the request holding ticket kPage * p
+// (its descriptor, tickets and seq, as 16 tagged 8-B words), so a wave finds
+// its ticket's request in ONE round trip: its 16 lanes read the page, and a
+// consistent copy (every tag the same seq) of a request of this instance
+// whose tickets hold t is used as is.  Otherwise (a page whose first ticket
+// belongs to an earlier request, one overwritten after a wrap, or one being
+// rewritten) the copy's seq is a hint for the walk from the wave's cursor
+// (an idle wave's cursor lags by every request it sat out).
 constexpr uint32_t kPageShift = 4;
 constexpr uint32_t kPages = 1u << 14;  // 256K tickets covered (wraps: hints only)
 constexpr uint32_t kMaxIdleUs = 1000000;  // below the workers' 20 s give-up
@@ -166,6 +170,14 @@ struct EngSlot {  // a device slot (128 B), written by the dispatcher
   uint32_t mode, flags, cb, pad;
   uint64_t pad2[3];
 };
+// A ticket page: (tag << 32) | payload, tag = low 32 bits of the request's seq + 1.
+enum EngPageWord : uint32_t {
+  kPSeqHi, kPCsLo, kPCsHi, kPNch, kPBaseLo, kPBaseHi, kPOffsLo, kPOffsHi, kPSizesLo, kPSizesHi,
+  kPOutLo, kPOutHi, kPBadLo, kPBadHi, kPN, kPPacked, kPWords  // kPPacked as kWPacked
+};
+struct EngPage {
+  uint64_t w[kPWords];
+};
 struct EngDev {  // device memory: all zeroed once; the header before every launch
   uint64_t dend;  // chunk tickets published
   uint64_t p0[15];
@@ -190,7 +202,7 @@ struct EngDev {  // device memory: all zeroed once; the header before every laun
   // 3 ticket seen, 1 slot found, 4 body done, 5 drained, 6 counted; the last
   // chunk's wave: 7 ticket seen, 8 slot found, 9 body done, 10 drained, 11 counted
   uint64_t tr[kRing][kTrWords];
-  uint64_t page[kPages];     // ticket page -> request seq + 1 (hint)
+  EngPage page[kPages];      // ticket page -> a copy of the request holding its first ticket
 };
 constexpr size_t kDevHeader = offsetof(EngDev, cgrp);
 struct EngParams {
@@ -398,16 +410,31 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
       }
       const uint64_t total = uni64(((uint64_t)(uint32_t)__shfl((int)(uint32_t)(inc >> 32), 63) << 32) |
                                    (uint32_t)__shfl((int)(uint32_t)inc, 63));
-      // ticket pages: every page whose first ticket a request holds names it
-      // (the wave's 64 lanes write one request's pages at a time)
+      // ticket pages: every page whose first ticket a request holds gets a
+      // copy of it (the wave's 64 lanes write one request's pages at a time)
       for (uint32_t k = 0; k < m; k++) {
-        const uint64_t cs = cend + uni64(((uint64_t)(uint32_t)__shfl((int)(uint32_t)((inc - nch) >> 32), (int)k) << 32) |
-                                         (uint32_t)__shfl((int)(uint32_t)(inc - nch), (int)k));
-        const uint64_t ce = cend + uni64(((uint64_t)(uint32_t)__shfl((int)(uint32_t)(inc >> 32), (int)k) << 32) |
-                                         (uint32_t)__shfl((int)(uint32_t)inc, (int)k));
+        auto rl = [&](uint64_t v) -> uint64_t {  // lane k's 64-bit value
+          return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
+        };
+        const uint64_t cs = cend + rl(inc - nch), ce = cend + rl(inc);
         const uint64_t p0 = (cs + (1u << kPageShift) - 1) >> kPageShift, p1 = (ce + (1u << kPageShift) - 1) >> kPageShift;
         const uint64_t np = p1 - p0 < kPages ? p1 - p0 : kPages;
-        for (uint64_t j = lane; j < np; j += 64) st_agent(&d->page[(p0 + j) & (kPages - 1)], seen + k + 1);
+        if (np == 0) continue;  // (scalar)
+        const uint64_t seq1 = seen + k + 1;
+        const uint64_t tag = (uint64_t)(uint32_t)seq1 << 32;
+        const uint64_t rb = rl(r.base), ro = rl(r.offs), rs = rl(r.sizes), rq = rl(r.out), rd = rl(r.bad);
+        const uint32_t rn = (uint32_t)rl(r.n);
+        const uint32_t rp = (uint32_t)__builtin_amdgcn_readlane((int)((r.flags & 0xffffu) | (r.mode << 16) | (r.cb << 20)), (int)k);
+        const uint32_t pv[kPWords] = {(uint32_t)(seq1 >> 32), (uint32_t)cs, (uint32_t)(cs >> 32), (uint32_t)(ce - cs),
+                                      (uint32_t)rb, (uint32_t)(rb >> 32), (uint32_t)ro, (uint32_t)(ro >> 32),
+                                      (uint32_t)rs, (uint32_t)(rs >> 32), (uint32_t)rq, (uint32_t)(rq >> 32),
+                                      (uint32_t)rd, (uint32_t)(rd >> 32), rn, rp};
+        for (uint64_t j = lane; j < np; j += 64) {
+          EngPage* pg = &d->page[(p0 + j) & (kPages - 1)];
+#pragma unroll
+          for (uint32_t w = 0; w < kPWords; w++) st_agent(&pg->w[w], tag | pv[w]);
+        }
       }
       drain_vm();  // every lane's slot and page stores are written through before the end moves
       cend += total;
@@ -682,23 +709,48 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
     // r + kRing only after request r is done, and a live request's seq is
     // above (newest written seq) - kRing, so a slot found holding a newer
     // seq s1 - 1 moves the cursor to s1 - kRing (still at or below it).
-    // All of a slot's fields are read at once (one round trip), together with
-    // t's ticket page; when the cursor's slot does not hold t the page's
-    // request is tried next, then slots are walked forward one at a time.
-    // A page is a hint: after a wrap it may name a later request, or one the
-    // dispatcher is still writing (its page store and slot store come from
-    // different lanes, unordered: ADVICE r04) -- any inconsistency met after
-    // following it restarts the walk from the cursor, which is never past t's
-    // request and whose slots were all written before t was published.
+    // First t's ticket page (one round trip); a consistent copy of a request
+    // of this instance that holds t is t's request (tickets are unique within
+    // an instance).  Otherwise its seq is a hint for the walk: the cursor's
+    // slot is read whole (one round trip), the hinted request is tried next,
+    // then slots are walked forward one at a time.  After a wrap a hint may
+    // name a later request, or one the dispatcher is still writing (ADVICE
+    // r04) -- any inconsistency met after following it restarts the walk from
+    // the cursor, which is never past t's request and whose slots were all
+    // written before t was published.
     uint64_t cstart = 0, cend = 0, base = 0, offs = 0, sizes = 0, out = 0, bad = 0, n = 0;
     uint32_t mode = 0, flags = 0, cb = 0;
+    // t's page: lanes 0-15 read its 16 words (one round trip)
+    uint64_t pw = 0;
+    if (lane < (int)kPWords) pw = ld_agent(&d->page[(t >> kPageShift) & (kPages - 1)].w[lane]);
+    auto pl = [&](uint32_t k) -> uint64_t { return (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pw, (int)k); };
+    const uint32_t ptag = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pw >> 32), 0);
+    const bool pcons = ptag != 0 &&
+        (__builtin_amdgcn_ballot_w64(lane < (int)kPWords && (uint32_t)(pw >> 32) == ptag) & 0xffffull) == 0xffffull;
+    const uint64_t pseq1 = pcons ? (pl(kPSeqHi) << 32 | ptag) : 0;
+    const uint64_t pcs = pl(kPCsLo) | pl(kPCsHi) << 32;
+    bool found = pcons && pseq1 > e.first_seq && t >= pcs && t < pcs + pl(kPNch);
+    if (found) {  // the page's copy is t's request (seqs of earlier instances are below first_seq)
+      r = pseq1 - 1;
+      cstart = pcs;
+      cend = pcs + pl(kPNch);
+      base = pl(kPBaseLo) | pl(kPBaseHi) << 32;
+      offs = pl(kPOffsLo) | pl(kPOffsHi) << 32;
+      sizes = pl(kPSizesLo) | pl(kPSizesHi) << 32;
+      out = pl(kPOutLo) | pl(kPOutHi) << 32;
+      bad = pl(kPBadLo) | pl(kPBadHi) << 32;
+      n = pl(kPN);
+      const uint32_t pk = (uint32_t)pl(kPPacked);
+      flags = pk & 0xffffu;
+      mode = (pk >> 16) & 0xfu;
+      cb = pk >> 20;
+    }
     bool hinted = false, via_hint = false;
     const uint64_t r0 = r;
-    for (;;) {
+    while (!found) {
       const EngSlot* S = &d->slot[r % kRing];
-      uint64_t s1 = 0, hint = 0;
+      uint64_t s1 = 0;
       if (lane == 0) {
-        if (!hinted) hint = ld_agent(&d->page[(t >> kPageShift) & (kPages - 1)]);
         s1 = ld_agent(&S->seq1);
         cstart = ld_agent(&S->cstart);
         cend = ld_agent(&S->cend);
@@ -715,12 +767,11 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
       s1 = uni64(s1);
       const uint64_t ce = uni64(cend);
       if (!hinted) {
-        // the page of t names the request holding its first ticket: t's request
-        // or an earlier one (pages hold hints, checked below like the cursor)
+        // the page's seq is a hint: t's request or an earlier one (checked
+        // below like the cursor)
         hinted = true;
-        hint = uni64(hint);
-        if (!(s1 == r + 1 && t >= uni64(cstart) && t < ce) && hint > r + 1) {
-          r = hint - 1;
+        if (!(s1 == r + 1 && t >= uni64(cstart) && t < ce) && pseq1 > r + 1) {
+          r = pseq1 - 1;
           via_hint = true;
           continue;
         }
