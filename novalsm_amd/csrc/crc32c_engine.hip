@@ -939,6 +939,7 @@ struct Engine {
   uint32_t slice_us = 0;       // NOVA_SST_ENGINE_SLICE_US / nova_sst_engine_set_slice_us
   bool slice_set = false;      // set through the API
   uint64_t timeouts = 0, errors = 0, taken_back = 0, unsafe = 0, yield_waits = 0;
+  uint64_t launch_ns_max = 0, launch_slow = 0;  // host time in launch_locked: the largest, launches over 1 ms
   uint32_t idle_us = 0, waves = 0;
   std::atomic<uint32_t> timeout_ms{0};        // 0: NOVA_SST_ENGINE_TIMEOUT_MS (default 10000)
   std::atomic<uint32_t> failures{0};          // consecutive failed requests (backoff)
@@ -1074,6 +1075,14 @@ struct Engine {
 
   // A fresh instance over requests [first, ...): the previous one has exited.
   int launch_locked(uint64_t first) {
+    const auto tl0 = Clock::now();
+    const int rc = launch_locked_(first);
+    const uint64_t ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - tl0).count();
+    launch_ns_max = std::max(launch_ns_max, ns);
+    launch_slow += ns > 1000000 ? 1 : 0;
+    return rc;
+  }
+  int launch_locked_(uint64_t first) {
     hipError_t e = hipStreamSynchronize(stream);
     if (e == hipSuccess) e = hipMemsetAsync(ddev, 0, kDevHeader, stream);
     if (e != hipSuccess) {
@@ -1519,7 +1528,8 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
       (uint64_t)(gp->running && gp->ctl && !((volatile EngCtl*)gp->ctl)->exited ? 1 : 0),
       gp->exits[kWhyIdle], gp->exits[kWhyYield], gp->exits[kWhyStop], gp->exits[kWhyLost],
       gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
-      (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice]};
+      (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice], gp->launch_ns_max / 1000,
+      gp->launch_slow};
   for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
   return 0;
 }
