@@ -207,9 +207,10 @@ int nova_sst_engine_set_idle_us(uint32_t us);
  * requests timed out, engine errors, requests taken back, requests that could
  * not be taken back; relaunches that waited for a yielded launch, yield bumps;
  * disabled for good, backing off now; instance exits at the end of a time
- * slice (NOVA_SST_ENGINE_SLICE_US); the longest host time of a launch (us)
- * and the launches that took over 1 ms. */
-#define NOVA_ENGINE_COUNTERS 19
+ * slice (NOVA_SST_ENGINE_SLICE_US); the longest host time of a relaunch (us)
+ * and the relaunches that took over 1 ms; the longest gap between two polls
+ * of a dispatcher (us, a stalled or preempted instance). */
+#define NOVA_ENGINE_COUNTERS 20
 int nova_sst_engine_counters(uint64_t* out, size_t n);
 /* Time slice of an engine instance in us, from the next instance (0: back to
  * NOVA_SST_ENGINE_SLICE_US, default 2000; 0xFFFFFFFF: none).  An instance

@@ -161,7 +161,8 @@ struct EngCtl {  // pinned host memory (fine-grained)
   uint64_t alive;     // engine: the instance's generation, stored before its first ring read
   uint32_t why;       // engine: exit reason (kWhy*)
   uint32_t pad2;
-  uint64_t pad3[12];
+  uint64_t maxgap;    // engine: the dispatcher's longest gap between two polls (ticks), at exit
+  uint64_t pad3[11];
 };
 struct EngSlot {  // a device slot (128 B), written by the dispatcher
   uint64_t seq1;          // request seq + 1 (0: never written)
@@ -284,9 +285,15 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
   uint64_t seen = e.first_seq, cend = 0;
   uint64_t last = now_ticks();
   const uint64_t born = last;
+  uint64_t prev_poll = last, maxgap = 0;  // (a stalled or preempted dispatcher shows as a long gap)
   bool took = false;
   uint64_t auto_done = 0;  // group completions of groups without tickets (reqs_done counts the rest)
   for (;;) {
+    {
+      const uint64_t nowp = now_ticks();
+      maxgap = nowp - prev_poll > maxgap ? nowp - prev_poll : maxgap;
+      prev_poll = nowp;
+    }
     // one round trip: lanes 0-11 the words of entry `seen`, lane 12 its cancel
     // word, 13 the tail, 14 the stop word, 15 the yield word
     uint64_t x = 0;
@@ -470,6 +477,7 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
         if (lane == 0) {
           if (lost) st_sys(&e.ctl->error, 3u);
           st_sys(&e.ctl->why, lost ? kWhyLost : stop ? kWhyStop : yielded ? kWhyYield : sliced ? kWhySlice : kWhyIdle);
+          st_sys(&e.ctl->maxgap, maxgap);
           st_agent(&d->dstop, 1u);
           st_sys(&e.ctl->consumed, seen);
           __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)&e.ctl->exited, 1u,
@@ -939,7 +947,8 @@ struct Engine {
   uint32_t slice_us = 0;       // NOVA_SST_ENGINE_SLICE_US / nova_sst_engine_set_slice_us
   bool slice_set = false;      // set through the API
   uint64_t timeouts = 0, errors = 0, taken_back = 0, unsafe = 0, yield_waits = 0;
-  uint64_t launch_ns_max = 0, launch_slow = 0;  // host time in launch_locked: the largest, launches over 1 ms
+  uint64_t launch_ns_max = 0, launch_slow = 0;  // host time in launch_locked: the largest (not the first), launches over 1 ms
+  uint64_t gap_ticks_max = 0;                   // the dispatchers' longest gap between two polls
   uint32_t idle_us = 0, waves = 0;
   std::atomic<uint32_t> timeout_ms{0};        // 0: NOVA_SST_ENGINE_TIMEOUT_MS (default 10000)
   std::atomic<uint32_t> failures{0};          // consecutive failed requests (backoff)
@@ -1078,8 +1087,10 @@ struct Engine {
     const auto tl0 = Clock::now();
     const int rc = launch_locked_(first);
     const uint64_t ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - tl0).count();
-    launch_ns_max = std::max(launch_ns_max, ns);
-    launch_slow += ns > 1000000 ? 1 : 0;
+    if (gen > 1) {  // (the first launch loads the code object)
+      launch_ns_max = std::max(launch_ns_max, ns);
+      launch_slow += ns > 1000000 ? 1 : 0;
+    }
     return rc;
   }
   int launch_locked_(uint64_t first) {
@@ -1158,6 +1169,8 @@ struct Engine {
       first = c->consumed;
       const uint32_t why = c->why;
       exits[why < kWhyN ? why : 0]++;
+      const uint64_t mg = c->maxgap;
+      gap_ticks_max = mg > gap_ticks_max ? mg : gap_ticks_max;
     }
     running = false;
     relaunches++;
@@ -1529,7 +1542,7 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
       gp->exits[kWhyIdle], gp->exits[kWhyYield], gp->exits[kWhyStop], gp->exits[kWhyLost],
       gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
       (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice], gp->launch_ns_max / 1000,
-      gp->launch_slow};
+      gp->launch_slow, gp->gap_ticks_max / 100};
   for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
   return 0;
 }

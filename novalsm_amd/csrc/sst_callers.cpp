@@ -209,6 +209,9 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
   CKN(nova_device_init());
   const int prev_enabled = -1;
   if (cfg->path == 1) CKN(nova_sst_engine_set_enabled(1));
+  // NOVA_CALLERS_TRACE=1: the engine's per-request spans (nova_sst_engine_set_trace) in the JSON
+  const bool trace = getenv("NOVA_CALLERS_TRACE") && atoi(getenv("NOVA_CALLERS_TRACE")) != 0;
+  if (cfg->path == 1 && trace) CKN(nova_sst_engine_set_trace(1));
   if (cfg->path == 2) CKN(nova_sst_engine_set_enabled(0));
   std::vector<Table> tabs(T);
   int rc = 0;
@@ -425,16 +428,34 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
   const char* cn[NOVA_ENGINE_COUNTERS] = {"requests", "launches", "fallbacks", "running", "exits_idle",
                                           "exits_yield", "exits_stop", "exits_lost", "timeouts", "errors",
                                           "taken_back", "unsafe", "yield_waits", "yield_bumps", "broken",
-                                          "backing_off", "exits_slice", "launch_us_max", "launch_slow"};
+                                          "backing_off", "exits_slice", "launch_us_max", "launch_slow",
+                                          "poll_gap_us_max"};
   for (int i = 0; i < NOVA_ENGINE_COUNTERS; i++) {
     if (i == 3 || i == 14 || i == 15) continue;  // states, not counts
     char b[64];
     // launch_us_max: a maximum, not a count
     snprintf(b, sizeof b, "%s\"%s\": %llu", eng.size() > 1 ? ", " : "", cn[i],
-             (unsigned long long)(i == 17 ? c1[i] : c1[i] - c0[i]));
+             (unsigned long long)(i == 17 || i == 19 ? c1[i] : c1[i] - c0[i]));
     eng += b;
   }
   eng += "}";
+  std::string tr = "null";
+  if (trace) {
+    uint64_t tn = 0, dn = 0;
+    double ts[5] = {}, td[11] = {};
+    (void)nova_sst_engine_trace_stats(&tn, ts);
+    (void)nova_sst_engine_trace_detail(&dn, td);
+    char b[768];
+    snprintf(b, sizeof b,
+             "{\"requests\": %llu, \"host_submit_to_done_us\": %.2f, \"gpu_dispatch_to_first_chunk_us\": %.2f, "
+             "\"gpu_first_to_last_chunk_us\": %.2f, \"gpu_dispatch_to_last_us\": %.2f, \"chunk0_us\": {\"seen\": %.2f, "
+             "\"slot\": %.2f, \"body\": %.2f, \"drained\": %.2f, \"counted\": %.2f}, \"last_us\": {\"seen\": %.2f, "
+             "\"slot\": %.2f, \"body\": %.2f, \"drained\": %.2f, \"counted\": %.2f, \"done\": %.2f}}",
+             (unsigned long long)tn, ts[0], ts[1], ts[2], ts[3], td[2], td[0], td[3], td[4], td[5], td[6], td[7],
+             td[8], td[9], td[10], td[1]);
+    tr = b;
+    (void)nova_sst_engine_set_trace(0);
+  }
   const double p50 = pct(lat, 0.5);
   const int n = snprintf(
       json, cap,
@@ -442,13 +463,13 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
       "\"window_s\": %.3f, \"warm_s\": %.3f, \"calls\": %llu, \"calls_in_window\": %llu, "
       "\"aggregate_GBps\": %.1f, \"frac_of_8TBps\": %.4f, \"p50_us\": %.1f, \"p90_us\": %.1f, \"p99_us\": %.1f, "
       "\"p999_us\": %.1f, \"max_us\": %.1f, \"max_over_p50\": %.2f, \"slowest_us_at_s\": %s, "
-      "\"engine\": %s, \"cpu_throttled_periods\": %llu, \"cpu_throttled_us\": %llu, \"plain\": %s, "
+      "\"engine\": %s, \"trace\": %s, \"cpu_throttled_periods\": %llu, \"cpu_throttled_us\": %llu, \"plain\": %s, "
       "\"wrong_results\": %llu, \"verified\": %s, \"rc\": %d}",
       verify ? "verify" : "trailers", cfg->path == 0 ? "direct" : cfg->path == 1 ? "engine" : "queue", T,
       (unsigned long long)cfg->blocks, (unsigned long long)(T ? tabs[0].algo_bytes : 0), window, cfg->warm_s,
       (unsigned long long)total_calls, (unsigned long long)calls_in, bytes / window / 1e9,
       bytes / window / 8e12, p50, pct(lat, 0.9), pct(lat, 0.99), pct(lat, 0.999), lat.empty() ? 0.0 : lat.back(),
-      p50 > 0 ? (lat.empty() ? 0.0 : lat.back()) / p50 : 0.0, sl.c_str(), eng.c_str(),
+      p50 > 0 ? (lat.empty() ? 0.0 : lat.back()) / p50 : 0.0, sl.c_str(), eng.c_str(), tr.c_str(),
       (unsigned long long)(thr1 - thr0), (unsigned long long)(thr_us1 - thr_us0), plain.c_str(),
       (unsigned long long)wrong, verified ? "true" : "false", rc);
   for (auto& tb : tabs) free_table(tb);

@@ -1,4 +1,5 @@
 set -u
+timeout -k 10 60 python -u tools/stall_probe.py --seconds 3 > gpurun_out/stall_probe.log 2>&1; echo "== stall probe"; tail -1 gpurun_out/stall_probe.log
 mkdir -p gpurun_out
 for q in 1 0; do
   NOVA_SST_ENGINE_QUEUE=$q timeout -k 10 200 python -u -m pytest tests/test_gpu_engine.py -m gpu -v -s --timeout 120 --timeout-method thread -k "mixed" > gpurun_out/mixed_q$q.log 2>&1
