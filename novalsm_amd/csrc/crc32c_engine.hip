@@ -85,8 +85,12 @@
 //     ~15 us per request; the last chunk's wave then stores the completion
 //     word (system scope).
 #include <hip/hip_runtime.h>
+#include <sched.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
 #include <atomic>
 #include <chrono>
 #include <cstddef>
@@ -911,6 +915,28 @@ uint64_t env_u64(const char* name, uint64_t def) {
 
 using Clock = std::chrono::steady_clock;
 
+// CPUs this process may keep busy: its affinity mask, capped by a cgroup v2
+// CPU quota (cpu.max); spinning waiters get all but two of them
+// (NOVA_SST_ENGINE_SPINNERS overrides).
+int spinner_budget() {
+  const uint64_t env = env_u64("NOVA_SST_ENGINE_SPINNERS", 0);
+  if (env) return (int)std::min<uint64_t>(env, 1024);
+  int cpus = 0;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = CPU_COUNT(&set);
+  if (cpus <= 0) cpus = 1;
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    unsigned long long period = 0;
+    if (fscanf(f, "%31s %llu", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+      const double quota = strtod(q, nullptr) / (double)period;
+      if (quota > 0 && quota < cpus) cpus = (int)std::ceil(quota);
+    }
+    fclose(f);
+  }
+  return std::max(1, cpus - 2);
+}
+
 // engine_submit's result when the request could not be taken back: the
 // caller must NOT run the plain call (the engine may still write the outputs)
 constexpr int kEngineUnsafe = -1000;
@@ -951,6 +977,13 @@ struct Engine {
   uint64_t gap_ticks_max = 0;                   // the dispatchers' longest gap between two polls
   uint32_t idle_us = 0, waves = 0;
   std::atomic<uint32_t> timeout_ms{0};        // 0: NOVA_SST_ENGINE_TIMEOUT_MS (default 10000)
+  // Waiting (round 5): at most max_spinners waiters spin; the others poll in
+  // short sleeps.  16 waiters spinning on a 16-CPU cgroup quota exhausted it
+  // every 100-200 ms and every thread of the process was stopped for 2-7 ms
+  // (cpu.stat nr_throttled; the 2.1-2.4 ms tails at 16 threads).
+  int max_spinners = 1;
+  std::atomic<int> spinners{0};
+  uint64_t sleep_waits = 0;  // requests whose waiter slept (approximate: not under mu)
   std::atomic<uint32_t> failures{0};          // consecutive failed requests (backoff)
   std::atomic<int64_t> avoid_until_ns{0};     // steady clock: requests go plain until then
   // Yield registry: the launches this engine must not take the CUs from.
@@ -1000,7 +1033,7 @@ struct Engine {
     // blocking stream: the null stream waits for the engine -- measured, not
     // used).  A cooperative launch that fails falls back to 0.
     queue_mode = (int)env_u64("NOVA_SST_ENGINE_QUEUE", 1);
-    // NOVA_SST_ENGINE_SLICE_US (default 2000): an instance takes no request
+    // NOVA_SST_ENGINE_SLICE_US (default 5000): an instance takes no request
     // after running this long; it finishes the ones it took and exits, and the
     // next request's waiter launches the next instance.  A device-wide sync
     // (hipDeviceSynchronize, torch.cuda.synchronize) waits for the work each
@@ -1009,7 +1042,7 @@ struct Engine {
     // at the instance boundary: both wait about one slice at most under
     // steady traffic, instead of until the traffic stops.  0: no slice.
     if (!slice_set)
-      slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 2000));
+      slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 5000));
     hipError_t e = hipSuccess;
     if (queue_mode == 2) {
       int phys = 0;
@@ -1046,6 +1079,7 @@ struct Engine {
     memset(hcancel, 0, sizeof(uint64_t) * kRing);
     memset(ctl, 0, sizeof(EngCtl));
     if (!idle_us) idle_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_IDLE_US", 1000));
+    max_spinners = spinner_budget();
     waves = (uint32_t)env_u64("NOVA_SST_ENGINE_WAVES", kEngWaves);
     if (waves < 2 || waves > (uint32_t)kEngMaxWaves) waves = kEngWaves;
     // From here on every non-engine launch registers itself.  A launch made
@@ -1408,9 +1442,12 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   // The words only grow (seq + 1, then seq + 1 + kRing once this request is
   // done and its ring slot reused), so a waiter descheduled past a full ring
   // turn still sees its request done.
+  bool spinning = g.spinners.fetch_add(1) < g.max_spinners;
+  if (!spinning) g.spinners.fetch_sub(1);
+  int slack = -1;  // the thread's timer slack before its first sleep (restored after)
   for (uint64_t spin = 0; !failed; spin++) {
     if (g.done(seq)) break;
-    if ((spin & 255) == 255) {
+    if (!spinning || (spin & 255) == 255) {
       if (c->error) {
         std::lock_guard<std::mutex> lk(g.mu);
         g.errors++;
@@ -1431,10 +1468,26 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
         failed = true;
         break;
       }
-      if (spin > (1u << 16)) std::this_thread::yield();
+      if (spinning && spin > (1u << 16)) std::this_thread::yield();
     }
-    __builtin_ia32_pause();
+    if (spinning) {
+      __builtin_ia32_pause();
+      continue;
+    }
+    // more waiters than CPUs to spin on: poll every ~10 us, asleep
+    if (slack < 0) {
+      slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+      (void)prctl(PR_SET_TIMERSLACK, 1000ul, 0, 0, 0);  // 1 us: the sleeps end on time
+      g.sleep_waits++;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(8));
+    if (g.spinners.load(std::memory_order_relaxed) < g.max_spinners) {  // a spinner left: take its place
+      if (g.spinners.fetch_add(1) < g.max_spinners) spinning = true;
+      else g.spinners.fetch_sub(1);
+    }
   }
+  if (spinning) g.spinners.fetch_sub(1);
+  if (slack >= 0) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
   if (failed) {
     int rc = 0;
     {
@@ -1542,7 +1595,7 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
       gp->exits[kWhyIdle], gp->exits[kWhyYield], gp->exits[kWhyStop], gp->exits[kWhyLost],
       gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
       (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice], gp->launch_ns_max / 1000,
-      gp->launch_slow, gp->gap_ticks_max / 100};
+      gp->launch_slow, gp->gap_ticks_max / 100, gp->sleep_waits, (uint64_t)gp->max_spinners};
   for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
   return 0;
 }
@@ -1614,7 +1667,7 @@ int nova_sst_engine_set_slice_us(uint32_t us) {
   // from the next instance; ~0u: no slice; 0: back to NOVA_SST_ENGINE_SLICE_US
   if (us == 0) {
     gp->slice_set = false;
-    gp->slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 2000));
+    gp->slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 5000));
   } else {
     gp->slice_set = true;
     gp->slice_us = us == ~0u ? 0u : std::min<uint32_t>(us, kMaxIdleUs);
