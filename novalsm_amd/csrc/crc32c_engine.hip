@@ -437,15 +437,30 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
         const uint64_t rb = rl(r.base), ro = rl(r.offs), rs = rl(r.sizes), rq = rl(r.out), rd = rl(r.bad);
         const uint32_t rn = (uint32_t)rl(r.n);
         const uint32_t rp = (uint32_t)__builtin_amdgcn_readlane((int)((r.flags & 0xffffu) | (r.mode << 16) | (r.cb << 20)), (int)k);
-        const uint32_t pv[kPWords] = {(uint32_t)(seq1 >> 32), (uint32_t)cs, (uint32_t)(cs >> 32), (uint32_t)(ce - cs),
-                                      (uint32_t)rb, (uint32_t)(rb >> 32), (uint32_t)ro, (uint32_t)(ro >> 32),
-                                      (uint32_t)rs, (uint32_t)(rs >> 32), (uint32_t)rq, (uint32_t)(rq >> 32),
-                                      (uint32_t)rd, (uint32_t)(rd >> 32), rn, rp};
-        for (uint64_t j = lane; j < np; j += 64) {
-          EngPage* pg = &d->page[(p0 + j) & (kPages - 1)];
-#pragma unroll
-          for (uint32_t w = 0; w < kPWords; w++) st_agent(&pg->w[w], tag | pv[w]);
+        // 16 lanes per page, one word each: every store instruction writes 4
+        // whole 128-B pages (coalesced) instead of one word of 64 pages
+        const uint32_t wi = (uint32_t)lane & (kPWords - 1);
+        uint32_t pv = 0;
+        switch (wi) {
+          case kPSeqHi: pv = (uint32_t)(seq1 >> 32); break;
+          case kPCsLo: pv = (uint32_t)cs; break;
+          case kPCsHi: pv = (uint32_t)(cs >> 32); break;
+          case kPNch: pv = (uint32_t)(ce - cs); break;
+          case kPBaseLo: pv = (uint32_t)rb; break;
+          case kPBaseHi: pv = (uint32_t)(rb >> 32); break;
+          case kPOffsLo: pv = (uint32_t)ro; break;
+          case kPOffsHi: pv = (uint32_t)(ro >> 32); break;
+          case kPSizesLo: pv = (uint32_t)rs; break;
+          case kPSizesHi: pv = (uint32_t)(rs >> 32); break;
+          case kPOutLo: pv = (uint32_t)rq; break;
+          case kPOutHi: pv = (uint32_t)(rq >> 32); break;
+          case kPBadLo: pv = (uint32_t)rd; break;
+          case kPBadHi: pv = (uint32_t)(rd >> 32); break;
+          case kPN: pv = rn; break;
+          default: pv = rp; break;
         }
+        for (uint64_t j = (uint32_t)lane / kPWords; j < np; j += 64 / kPWords)
+          st_agent(&d->page[(p0 + j) & (kPages - 1)].w[wi], tag | pv);
       }
       drain_vm();  // every lane's slot and page stores are written through before the end moves
       cend += total;
