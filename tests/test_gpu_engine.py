@@ -36,6 +36,7 @@ def engine_on():
     yield
     C.engine_set_timeout_ms(0)
     C.engine_set_idle_us(0)
+    C.engine_set_slice_us(0)
     C.engine_reset()
     C.engine_set_enabled(-1)
 
@@ -175,6 +176,8 @@ def test_engine_waiter_past_ring_turn(torch_gpu, oracle, engine_on):
     request done (the word only grows: a >= test), with the right flags, no
     timeout, no fallback and no relaunch storm."""
     torch = torch_gpu
+    C.engine_set_slice_us(None)  # no time slice: every relaunch below would be a storm
+    C.engine_stop()
     late = _sst_table(torch, oracle, 4096, 21, victims=(100, 4000))
     small = [_sst_table(torch, oracle, 1, 50 + k) for k in range(4)]
     c0 = C.engine_counters()
@@ -254,7 +257,7 @@ def test_engine_take_back_when_held_off(torch_gpu, oracle, engine_on):
     assert np.array_equal(ok.cpu().numpy(), tb["want"]) and int(nb.item()) == 2
     assert c1["timeouts"] - c0["timeouts"] == 1 and c1["taken_back"] - c0["taken_back"] == 1, (c0, c1)
     assert c1["fallbacks"] - c0["fallbacks"] == 1 and c1["unsafe"] == c0["unsafe"], (c0, c1)
-    assert c1["backing_off"] == 1 and not c1["broken"], c1
+    assert not c1["broken"], c1  # (the 100 ms backoff ran out while the plain call waited for the hold)
     assert dt > 0.2, dt  # the plain call itself waited for the hold
     ok.fill_(0xEE)
     nb.fill_(12345)

@@ -1264,6 +1264,7 @@ def test_engine_idle_exit_and_buffer_rewrite(torch_gpu, oracle):
     C.engine_set_enabled(1)
     C.engine_stop()
     C.engine_set_idle_us(300)
+    fb0 = C.engine_stats()["fallbacks"]
     stop = threading.Event()
     errors = []
     noise = _sst_tables(torch, oracle, [3000, 700], 77)
@@ -1325,7 +1326,7 @@ def test_engine_idle_exit_and_buffer_rewrite(torch_gpu, oracle):
         C.engine_stop()
         C.engine_set_enabled(-1)
     assert not errors, errors[:4]
-    assert C.engine_stats()["fallbacks"] == 0
+    assert C.engine_stats()["fallbacks"] == fb0
 
 
 @pytest.mark.parametrize("size", ["one_pass", "two_pass"])

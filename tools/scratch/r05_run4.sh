@@ -8,7 +8,7 @@ for l in open(sys.argv[1]):
   d=json.loads(l[i:].split('\n')[0]); e=d['engine']
   print(d['op'], d['threads'], d['aggregate_GBps'], d['p50_us'], d['p99_us'], d['max_us'], d['slowest_us_at_s'][:2], 'L',e['launches'],'slice',e['exits_slice'],'yield',e['exits_yield'],'sleepw',e['sleep_waits'],'spin',e['max_spinners'],'thr',d['cpu_throttled_periods'], json.dumps({k:(v['max_us'],v['p50_us']) for k,v in (d['plain'] or {}).items()}), d['verified'])
 " "$1"; }
-timeout -k 10 400 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread -k "engine or sst_queue or adjacent" > gpurun_out/engine_tests.log 2>&1 || { tail -30 gpurun_out/engine_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_parity.py -m gpu -v --timeout 120 --timeout-method thread -k "engine or sst_queue or adjacent" > gpurun_out/engine_tests.log 2>&1 || { tail -30 gpurun_out/engine_tests.log; exit 1; }
 tail -1 gpurun_out/engine_tests.log
 timeout -k 10 300 python -u tools/concurrent_sst.py --threads 1,8,16 --blocks 4096 --paths engine > gpurun_out/conc_default.log 2>&1 || { tail -5 gpurun_out/conc_default.log; exit 1; }
 echo "== default"; summ gpurun_out/conc_default.log
