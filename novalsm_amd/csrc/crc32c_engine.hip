@@ -1143,8 +1143,12 @@ struct Engine {
     return rc;
   }
   int launch_locked_(uint64_t first) {
-    hipError_t e = hipStreamSynchronize(stream);
-    if (e == hipSuccess) e = hipMemsetAsync(ddev, 0, kDevHeader, stream);
+    // No host wait for the previous instance: its dispatcher has exited (it
+    // took no more requests and finished the ones it took), its workers only
+    // see the stop and end, and the header reset and the new instance follow
+    // it in stream order.  (A stream sync here cost every relaunch -- every
+    // time slice, every yield -- a host round trip.)
+    hipError_t e = hipMemsetAsync(ddev, 0, kDevHeader, stream);
     if (e != hipSuccess) {
       (void)hipGetLastError();
       running = false;
