@@ -166,7 +166,7 @@ int nova_sstable_verify_blocks_ex(const void* buf, const uint64_t* offsets, cons
  * launched cooperatively, which HIP runs on a hardware queue of its own
  * (NOVA_SST_ENGINE_QUEUE).  A device-wide sync
  * (hipDeviceSynchronize) waits for the running instance, which exits after
- * at most one time slice (nova_sst_engine_set_slice_us, default 5 ms).
+ * at most one time slice (nova_sst_engine_set_slice_us, default 20 ms).
  * Work queued on `stream` before the call (the image, its descriptors)
  * completes first: the call synchronises `stream` when it is busy.  A table
  * of more than 2^20 blocks runs as the plain call on `stream`, and so does a
@@ -216,7 +216,7 @@ int nova_sst_engine_set_idle_us(uint32_t us);
 #define NOVA_ENGINE_COUNTERS 22
 int nova_sst_engine_counters(uint64_t* out, size_t n);
 /* Time slice of an engine instance in us, from the next instance (0: back to
- * NOVA_SST_ENGINE_SLICE_US, default 5000; 0xFFFFFFFF: none).  An instance
+ * NOVA_SST_ENGINE_SLICE_US, default 20000; 0xFFFFFFFF: none).  An instance
  * takes no request after running this long, finishes the ones it took and
  * exits; the next one follows at once.  Bounds what a device-wide sync and
  * another library's kernels wait under steady traffic. */

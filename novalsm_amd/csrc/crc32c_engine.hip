@@ -1048,7 +1048,7 @@ struct Engine {
     // blocking stream: the null stream waits for the engine -- measured, not
     // used).  A cooperative launch that fails falls back to 0.
     queue_mode = (int)env_u64("NOVA_SST_ENGINE_QUEUE", 1);
-    // NOVA_SST_ENGINE_SLICE_US (default 5000): an instance takes no request
+    // NOVA_SST_ENGINE_SLICE_US (default 20000): an instance takes no request
     // after running this long; it finishes the ones it took and exits, and the
     // next request's waiter launches the next instance.  A device-wide sync
     // (hipDeviceSynchronize, torch.cuda.synchronize) waits for the work each
@@ -1057,7 +1057,7 @@ struct Engine {
     // at the instance boundary: both wait about one slice at most under
     // steady traffic, instead of until the traffic stops.  0: no slice.
     if (!slice_set)
-      slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 5000));
+      slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 20000));
     hipError_t e = hipSuccess;
     if (queue_mode == 2) {
       int phys = 0;
@@ -1686,7 +1686,7 @@ int nova_sst_engine_set_slice_us(uint32_t us) {
   // from the next instance; ~0u: no slice; 0: back to NOVA_SST_ENGINE_SLICE_US
   if (us == 0) {
     gp->slice_set = false;
-    gp->slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 5000));
+    gp->slice_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_SLICE_US", 20000));
   } else {
     gp->slice_set = true;
     gp->slice_us = us == ~0u ? 0u : std::min<uint32_t>(us, kMaxIdleUs);

@@ -329,7 +329,7 @@ def test_engine_leaves_other_streams_alone(torch_gpu, engine_on):
     which runs on a queue of its own, from a non-blocking stream: while two
     native threads keep it busy, a small torch op on each of 16 fresh streams
     and on the null stream finishes in milliseconds, and a device-wide sync
-    returns once the running instance ends its 5 ms time slice."""
+    returns once the running instance ends its 20 ms time slice."""
     torch = torch_gpu
     from novalsm_amd import callers
     res, errors = {}, []
@@ -356,7 +356,7 @@ def test_engine_leaves_other_streams_alone(torch_gpu, engine_on):
     float(x.sum().item())  # the null stream
     null = time.perf_counter() - t0
     t0 = time.perf_counter()
-    torch.cuda.synchronize()  # device-wide: waits for the running instance, one time slice (5 ms)
+    torch.cuda.synchronize()  # device-wide: waits for the running instance, one time slice (20 ms)
     dsync = time.perf_counter() - t0
     busy = C.engine_counters()["running"]
     t.join()
