@@ -488,6 +488,8 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_rounds<kLogVerify>())) return;
   if ((t->err = set_lds_attr_rounds<8, kLogWrite, kVarOutPos>())) return;
   if ((t->err = set_lds_attr_rounds<8, kLogVerify, kVarOutPos>())) return;
+  if ((t->err = set_lds_attrs_rounds<kLogWrite, kVarCached>())) return;
+  if ((t->err = set_lds_attrs_rounds<kLogVerify, kVarCached>())) return;
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;
@@ -675,8 +677,15 @@ template <int MODE>
 int launch_rounds(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_t chunk = 0) {
   int rc = 0;
   if (g_diag && g_diag->rounds(MODE, G, p, t, stream, chunk, &rc)) return rc;
-  if constexpr (MODE == kLogWrite || MODE == kLogVerify)
+  if constexpr (MODE == kLogWrite || MODE == kLogVerify) {
     if (p.out_pos) return launch_rounds_v<MODE, kVarOutPos>(G, p, t, stream, chunk);
+    // Short records (G <= 4 lanes each) share their first and last lines with
+    // their neighbours, which the same wave reads in the same chunk: default-
+    // policy loads keep those lines in L2 for the second reader (same-box A/B,
+    // profiles/r05_log_cached_ab.log: log512 write 27.9 -> 36.7 %, verify
+    // 36.8 -> 37.7 %; log4k at G = 8 loses 3-7 points with them and stays nt).
+    if (G <= 4) return launch_rounds_v<MODE, kVarCached>(G, p, t, stream, chunk);
+  }
   if (MODE == kStore && p.init)  // per-block init values: the general head masking
     return launch_rounds_v<kStore, kVarInit>(G, p, t, stream, chunk);
   return launch_rounds_v<MODE, 0>(G, p, t, stream, chunk);

@@ -1474,8 +1474,15 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
     if (var == kVarNarrow) return launch_rounds_v<kStore, kVarNarrow>(G, p, t, s, chunk);
   }
   const bool round_epi = var == kVarRoundEpi;  // A/B: the per-round epilogue (rounds 1-2 form)
+  if constexpr (MODE == kLogWrite || MODE == kLogVerify || MODE == kVerify) {
+    // A/B: the product kernel at 16 waves per workgroup (short log records)
+    if (var == kVarW16 && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarW16>(G, p, t, s, chunk);
+    // A/B: default-policy data loads (lines two records share stay in L2)
+    if (var == kVarCached && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarCached>(G, p, t, s, chunk);
+  }
   if constexpr (MODE == kLogWrite || MODE == kLogVerify) {
     if (p.out_pos) {  // the product's sorted large-log path (G = 8), with the ablations
+      if (var == kVarCached) return launch_rounds_v<MODE, kVarCached | kVarOutPos>(G, p, t, s, chunk);
       if (MODE == kLogVerify && var == kVarNoTail)
         return launch_rounds_v<MODE, kVarDiag | kVarNoTail | kVarOutPos>(G, p, t, s, chunk);
       if (round_epi) return launch_rounds_v<MODE, kVarDiag | kVarRoundEpi | kVarOutPos>(G, p, t, s, chunk);

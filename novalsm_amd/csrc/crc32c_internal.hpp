@@ -116,6 +116,9 @@ constexpr int kVarRoundEpi = 2048;
 // rewritten between requests) and verify loads each stored CRC with its
 // descriptor.
 constexpr int kVarEngine = 4096;
+// Rounds kernel (diagnostics A/B): 16 waves per workgroup
+// (launch bound 1024 threads: 128 VGPRs) instead of 12 (168 VGPRs).
+constexpr int kVarW16 = 8192;
 
 constexpr size_t kLdsMax = 160 * 1024;  // per CU on MI355X
 constexpr int kMaxDevices = 64;

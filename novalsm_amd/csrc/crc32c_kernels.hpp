@@ -1374,7 +1374,7 @@ __device__ __forceinline__ uint32_t shift_nb(const uint8_t* lds, uint32_t byte_t
 // the 12-wave bound (168 VGPRs) it spilled 6 VGPRs, so it launches 8 waves.
 constexpr int kInitMaxWaves = 8;
 template <int G, int MODE, int VAR = 0>
-__global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : kFlatThreads)
+__global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR & kVarW16) ? 1024 : kFlatThreads)
     crc32c_rounds_kernel(CrcParams p0) {
   CrcParams p = p0;  // the log-stream follow-up narrows the batch below
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -2723,6 +2723,7 @@ int launch_rounds_v(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint3
   p.n_chunks = (p.n_blocks + p.chunk - 1) / p.chunk;
   uint64_t nwaves = flat_waves();
   if ((VAR & kVarInit) && nwaves > (uint64_t)kInitMaxWaves) nwaves = kInitMaxWaves;  // launch bound
+  if (VAR & kVarW16) nwaves = 16;
   uint64_t wgs = (p.n_chunks + nwaves - 1) / nwaves;
   if (wgs > (uint64_t)t->cus) wgs = t->cus;
   if (wgs > 256) wgs = 256;

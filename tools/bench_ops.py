@@ -79,6 +79,8 @@ def main() -> int:
     ap.add_argument("--chunk-sweep", default="",
                     help="comma list of rounds-kernel chunk sizes (nova_diag_set_chunk_blocks), log ops")
     ap.add_argument("--no-ablations", action="store_true", help="skip the diagnostics ablations")
+    ap.add_argument("--var-ab", default="",
+                    help="comma list of rounds-kernel variants to A/B against the product (8192 16 waves, 2 cached)")
     ap.add_argument("--log-bound", action="store_true",
                     help="log write: time its composite bound (no-store pass + isolated CRC-field stores)")
     args = ap.parse_args()
@@ -125,6 +127,23 @@ def main() -> int:
                               "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}),
                   flush=True)
         C.set_tuning(0, 0)
+
+    def var_ab(op, fn, alg_bytes):
+        """Rounds-kernel A/Bs against the product, alternated: 8192 = 16 waves
+        per workgroup (128 VGPRs, a few spilled dwords),
+        2 = default-policy data loads instead of non-temporal ones."""
+        vs = [int(x) for x in args.var_ab.split(",") if x]
+        if not vs:
+            return
+        for rep in range(2):
+            for var in [0] + vs:
+                with C.diagnostics() as D:
+                    D.nova_diag_set_variant(var)
+                    sec = timed(torch, fn, args.steps, args.warmup, stream)
+                    D.nova_diag_set_variant(0)
+                print(json.dumps({"sweep": op, "variant": var, "rep": rep,
+                                  "GBps": round(alg_bytes / sec / 1e9, 1),
+                                  "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}), flush=True)
 
     def log_write_bound(buf, o, n, total, sum_rec, sec_product):
         """log write's composite bound, all in this run --
@@ -236,6 +255,7 @@ def main() -> int:
             ok = int(bad.item()) == 0 and bool(okb.cpu().numpy().all())
             emit("verify", wl, sum_len + 6 * n, sec, ok, {"image": image})
             sweep("verify", vf, sum_len + 6 * n)
+            var_ab("verify", vf, sum_len + 6 * n)
             for vv, name in (() if args.no_ablations else ((2048, "verify_round_epilogue"),)):
                 with C.diagnostics() as D:  # A/B: the per-round epilogue (rounds 1-2)
                     D.nova_diag_set_variant(vv)
@@ -302,6 +322,7 @@ def main() -> int:
                 gbs1 = sum_rec / sec1 / 1e9
                 print(json.dumps({"sweep": name, "GBps": round(gbs1, 1),
                                   "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
+            var_ab("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
             if args.log_bound:
                 log_write_bound(buf, o, n, total, sum_rec, sec)
         if "log_verify" in ops:
@@ -328,6 +349,7 @@ def main() -> int:
                 gbs1 = (sum_rec + n) / sec1 / 1e9
                 print(json.dumps({"sweep": name, "GBps": round(gbs1, 1),
                                   "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
+            var_ab("log_verify", lv, sum_rec + n)
             sweep("log_verify", lv, sum_rec + n)
         del buf
         torch.cuda.empty_cache()

@@ -23,7 +23,9 @@ STEPS=${STEPS:-smoke,pytest,bench,prof,pmc,ops}
 [[ $STEPS == *smoke* ]] && step final_smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *pytest* ]] && step final_pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 [[ $STEPS == *bench* ]] && step final_bench 600 python bench.py --detail-out gpurun_out/bench_detail.json
-[[ $STEPS == *prof* ]] && step final_rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final_prof -o run -- python3 bench.py --no-cpu-baseline
+# (the sst_engine secondary is left out: under kernel tracing the persistent
+# engine's callers stalled the run past the box's 3-minute silence limit)
+[[ $STEPS == *prof* ]] && step final_rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final_prof -o run -- python3 bench.py --no-cpu-baseline --secondary 3,4,sst4k_trailers,sst4k_verify,log4k_write,log4k_verify,log512_write,log512_verify,parity,5
 if [[ $STEPS == *pmc* ]]; then
   for cfg in ${PMC_CFGS:-2 3 4 sst4k_trailers sst4k_verify log4k_write log4k_verify log512_write log512_verify parity}; do
     rm -rf gpurun_out/pmc$cfg
