@@ -212,8 +212,10 @@ int nova_sst_engine_set_idle_us(uint32_t us);
  * of a dispatcher (us, a stalled or preempted instance); requests whose
  * waiter slept instead of spinning, and the most waiters that spin at once
  * (this process's CPUs, capped by its cgroup quota, minus 2;
- * NOVA_SST_ENGINE_SPINNERS). */
-#define NOVA_ENGINE_COUNTERS 22
+ * NOVA_SST_ENGINE_SPINNERS); 1 if the request ring is in device memory
+ * (written by the host through the PCIe BAR; NOVA_SST_ENGINE_RING=host keeps
+ * it in pinned host memory). */
+#define NOVA_ENGINE_COUNTERS 23
 int nova_sst_engine_counters(uint64_t* out, size_t n);
 /* Time slice of an engine instance in us, from the next instance (0: back to
  * NOVA_SST_ENGINE_SLICE_US, default 20000; 0xFFFFFFFF: none).  An instance

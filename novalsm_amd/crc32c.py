@@ -456,7 +456,8 @@ def engine_stats() -> dict:
 ENGINE_COUNTERS = ("requests", "launches", "fallbacks", "running", "exits_idle", "exits_yield",
                    "exits_stop", "exits_lost", "timeouts", "errors", "taken_back", "unsafe",
                    "yield_waits", "yield_bumps", "broken", "backing_off", "exits_slice", "launch_us_max",
-                   "launch_slow", "poll_gap_us_max", "sleep_waits", "max_spinners")
+                   "launch_slow", "poll_gap_us_max", "sleep_waits", "max_spinners",
+                   "ring_device")
 
 
 def engine_counters() -> dict:

@@ -14,8 +14,9 @@
 //   * one workgroup per CU (8 waves) stays resident with the M_256 tables in
 //     LDS (G = 16 lanes per block);
 //   * a submitting thread writes its request (image, descriptor arrays,
-//     outputs, op, blocks per chunk) into a ring in pinned host memory, as
-//     tagged 8-byte words, and bumps a tail word;
+//     outputs, op, blocks per chunk) into a ring as tagged 8-byte words, and
+//     bumps a tail word (the ring lives in device memory that the host writes
+//     through the PCIe BAR; pinned host memory without a large BAR);
 //   * wave 0 of workgroup 0 -- the dispatcher -- polls the next entry's words
 //     and the tail in one round trip, copies new requests into device-memory
 //     slots, maps their ticket pages to them and publishes their chunk
@@ -72,7 +73,7 @@
 //
 // Memory visibility (cdna_hip_programming.md Guideline 16):
 //   * host -> engine: requests and the tail word are read with system-scope
-//     loads (fine-grained host memory, no cache);
+//     loads (fine-grained memory, no cache);
 //   * dispatcher -> workers: slot fields and the end word are stored and
 //     loaded with agent-scope atomics (write-through, L1-bypassing), drained
 //     before the end word is advanced;
@@ -151,12 +152,25 @@ struct EngReq {  // an entry, decoded
   uint64_t base, offs, sizes, out, bad, n;
   uint32_t mode, flags, cb;
 };
-struct EngCtl {  // pinned host memory (fine-grained)
-  uint64_t htail;   // host: requests [first_seq, htail) are in the ring
-  uint32_t hstop;   // host: take no more requests, exit once the taken ones are done
+// Host -> engine words (round 5): fine-grained DEVICE memory that the host
+// writes through the PCIe BAR (a large-BAR device; else pinned host memory).
+// The dispatcher's poll then reads HBM instead of crossing PCIe: a host ->
+// GPU -> host ping-pong measured 1.90 us against 2.65 us through pinned
+// memory (tools/scratch/pingpong.hip, profiles/r05_pingpong.log).  The host
+// only writes these words, with one exception: the take-back reads its
+// cancel word back, which completes the posted write before it reads
+// `alive` (a PCIe read does not pass an earlier posted write).
+struct EngIn {
+  uint64_t htail;   // requests [first_seq, htail) are in the ring
+  uint32_t hstop;   // take no more requests, exit once the taken ones are done
   uint32_t pad0;
-  uint64_t hyield;  // host: bumped by every non-engine launch of the library (yield)
+  uint64_t hyield;  // bumped by every non-engine launch of the library (yield)
   uint64_t pad1[13];
+  EngHostReq ring[kRing];
+  uint64_t cancel[kRing];  // cancel[seq % kRing] == seq + 1: its submitter took the request back
+};
+struct EngCtl {  // engine -> host words: pinned host memory (fine-grained)
+  uint64_t pad1[16];
   uint64_t consumed;  // engine: the first seq it did not take (valid once exited)
   uint32_t exited;    // engine: this instance takes no more requests
   uint32_t error;     // engine: give-up code (1: a worker saw no new ticket for the give-up
@@ -211,8 +225,7 @@ struct EngDev {  // device memory: all zeroed once; the header before every laun
 };
 constexpr size_t kDevHeader = offsetof(EngDev, cgrp);
 struct EngParams {
-  const EngHostReq* hring;
-  const uint64_t* hcancel;  // hcancel[seq % kRing] == seq + 1: its submitter took the request back
+  const EngIn* in;          // host -> engine words
   // hdone[(seq % kRing) * 8 + g] = seq + 1 once group g's results of the request
   // are in memory (groups without tickets: at publication); the request is
   // done when all 8 are
@@ -221,7 +234,7 @@ struct EngParams {
   EngDev* dev;
   uint64_t first_seq;
   uint64_t gen;            // this instance's generation (stored to ctl->alive)
-  uint64_t yield_gen;      // ctl->hyield at launch: any other value is a yield
+  uint64_t yield_gen;      // in->hyield at launch: any other value is a yield
   uint64_t idle_ticks;     // s_memrealtime ticks (100 MHz) without a request before exiting
   uint64_t give_up_ticks;  // no new ticket (worker) / an unfinished request (dispatcher) this long: exit
   uint64_t slice_ticks;    // 0, or: take no request after running this long (then exit; the next instance follows)
@@ -303,11 +316,11 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
     uint64_t x = 0;
     {
       const uint64_t* a = nullptr;
-      if (lane < (int)kWords) a = &e.hring[seen % kRing].w[lane];
-      else if (lane == 12) a = &e.hcancel[seen % kRing];
-      else if (lane == 13) a = &e.ctl->htail;
-      else if (lane == 14) a = reinterpret_cast<const uint64_t*>(&e.ctl->hstop);  // hstop | pad0 << 32
-      else if (lane == 15) a = &e.ctl->hyield;
+      if (lane < (int)kWords) a = &e.in->ring[seen % kRing].w[lane];
+      else if (lane == 12) a = &e.in->cancel[seen % kRing];
+      else if (lane == 13) a = &e.in->htail;
+      else if (lane == 14) a = reinterpret_cast<const uint64_t*>(&e.in->hstop);  // hstop | pad0 << 32
+      else if (lane == 15) a = &e.in->hyield;
       if (lane < 16) x = ld_sys(a);
     }
     const uint32_t tag0 = (uint32_t)(seen + 1);
@@ -355,11 +368,11 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
         bool ok = false;
         if ((uint32_t)lane < want) {
           const uint64_t seq = seen + lane;
-          const EngHostReq* h = e.hring + seq % kRing;
+          const EngHostReq* h = e.in->ring + seq % kRing;
           uint64_t w[kWords];
 #pragma unroll
           for (uint32_t k = 0; k < kWords; k++) w[k] = ld_sys(&h->w[k]);
-          cancel = ld_sys(&e.hcancel[seq % kRing]);
+          cancel = ld_sys(&e.in->cancel[seq % kRing]);
           ok = true;
 #pragma unroll
           for (uint32_t k = 0; k < kWords; k++) ok = ok && (uint32_t)(w[k] >> 32) == (uint32_t)(seq + 1);
@@ -972,8 +985,8 @@ struct Engine {
   int dev = 0;
   int cus = 0;
   hipStream_t stream = nullptr;
-  EngHostReq* ring = nullptr;  // pinned
-  uint64_t* hcancel = nullptr; // pinned: seq + 1 of a request taken back
+  EngIn* in = nullptr;         // host -> engine words (device memory through the BAR, or pinned)
+  bool in_dev = false;         // `in` is device memory
   uint64_t* hdone = nullptr;   // pinned
   EngCtl* ctl = nullptr;       // pinned
   EngDev* ddev = nullptr;
@@ -1003,7 +1016,7 @@ struct Engine {
   std::atomic<int64_t> avoid_until_ns{0};     // steady clock: requests go plain until then
   // Yield registry: the launches this engine must not take the CUs from.
   // `live` once the pinned control block exists; then every non-engine launch
-  // of the library bumps ygen (stored to ctl->hyield) and records an event on
+  // of the library bumps ygen (stored to in->hyield) and records an event on
   // its stream (the stream's last one is kept).  ymu orders bumps, records and
   // the relaunch's snapshot (mu, when both are held, is taken first).
   std::atomic<bool> live{false};
@@ -1068,12 +1081,9 @@ struct Engine {
     } else {
       e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
     }
-    if (e == hipSuccess)
-      e = hipHostMalloc((void**)&ring, sizeof(EngHostReq) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) e = alloc_in(d);
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&hdone, sizeof(uint64_t) * kRing * kCntGroups, hipHostMallocCoherent | hipHostMallocMapped);
-    if (e == hipSuccess)
-      e = hipHostMalloc((void**)&hcancel, sizeof(uint64_t) * kRing, hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
       e = hipHostMalloc((void**)&ctl, sizeof(EngCtl), hipHostMallocCoherent | hipHostMallocMapped);
     if (e == hipSuccess)
@@ -1089,9 +1099,7 @@ struct Engine {
       broken = true;
       return (int)e;
     }
-    memset(ring, 0, sizeof(EngHostReq) * kRing);
     memset(hdone, 0, sizeof(uint64_t) * kRing * kCntGroups);
-    memset(hcancel, 0, sizeof(uint64_t) * kRing);
     memset(ctl, 0, sizeof(EngCtl));
     if (!idle_us) idle_us = (uint32_t)std::min<uint64_t>(kMaxIdleUs, env_u64("NOVA_SST_ENGINE_IDLE_US", 1000));
     max_spinners = spinner_budget();
@@ -1110,9 +1118,39 @@ struct Engine {
     return 0;
   }
 
+  // The host -> engine words: fine-grained device memory on a large-BAR device
+  // (the host's stores go through the BAR), checked by a store and a read
+  // back; else, or with NOVA_SST_ENGINE_RING=host (env value 0), pinned host memory.
+  hipError_t alloc_in(int d) {
+    int large_bar = 0;
+    (void)hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, d);
+    (void)hipGetLastError();
+    const char* ev = getenv("NOVA_SST_ENGINE_RING");
+    const bool want_dev = large_bar && !(ev && (!strcmp(ev, "host") || !strcmp(ev, "0")));
+    if (want_dev && hipExtMallocWithFlags((void**)&in, sizeof(EngIn), hipDeviceMallocFinegrained) == hipSuccess) {
+      if (hipMemset(in, 0, sizeof(EngIn)) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
+        volatile EngIn* vi = in;
+        vi->pad1[0] = 0x6e6f7661u;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        if (vi->pad1[0] == 0x6e6f7661u) {
+          vi->pad1[0] = 0;
+          in_dev = true;
+          return hipSuccess;
+        }
+      }
+      (void)hipFree(in);
+      in = nullptr;
+    }
+    (void)hipGetLastError();
+    in_dev = false;
+    const hipError_t e = hipHostMalloc((void**)&in, sizeof(EngIn), hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) memset(in, 0, sizeof(EngIn));
+    return e;
+  }
+
   // Registered launches not yet finished: the engine's stream waits for them
   // (under ymu), and the instance's yield value is read in the same section,
-  // so a launch registered later changes ctl->hyield for it.
+  // so a launch registered later changes in->hyield for it.
   uint64_t wait_for_yielded_locked() {
     std::lock_guard<std::mutex> lk(ymu);
     for (auto it = yev.begin(); it != yev.end();) {
@@ -1158,7 +1196,7 @@ struct Engine {
     volatile EngCtl* c = ctl;
     c->exited = 0;
     c->consumed = 0;
-    c->hstop = 0;
+    reinterpret_cast<volatile EngIn*>(in)->hstop = 0;
     c->error = 0;
     c->why = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -1169,8 +1207,7 @@ struct Engine {
       return err;
     }
     EngParams p{};
-    p.hring = ring;
-    p.hcancel = hcancel;
+    p.in = in;
     p.hdone = hdone;
     p.ctl = ctl;
     p.dev = ddev;
@@ -1252,15 +1289,23 @@ struct Engine {
   int take_back_locked(uint64_t seq) {
     volatile EngCtl* c = ctl;
     taken_back++;
-    reinterpret_cast<volatile uint64_t*>(hcancel)[seq % kRing] = seq + 1;
+    volatile EngIn* vi = in;
+    vi->cancel[seq % kRing] = seq + 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
+    // device memory: reading the word back completes the posted write before
+    // `alive` is read (the Dekker pair above)
+    if (in_dev && vi->cancel[seq % kRing] != seq + 1) {
+      unsafe++;
+      broken = true;
+      return kEngineUnsafe;
+    }
     if (done(seq)) return 0;                // done or skipped: never touched again
     if (!running) return 0;                 // no instance: the next one skips it
     if (c->alive != gen) return 0;          // not started: it will read the cancel word
     if (c->exited && c->consumed <= seq) return 0;  // exited without taking it
     // The running instance took it or may: stop it, then wait for the request
     // (run or skipped) or for the kernel's end.
-    c->hstop = 1;
+    vi->hstop = 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     const auto t0 = Clock::now();
     const auto limit = std::chrono::milliseconds(std::max<uint32_t>(timeout(), 30000));
@@ -1314,7 +1359,7 @@ int engine_stop(Engine& g) {
   std::lock_guard<std::mutex> lk(g.mu);
   if (!g.ready || !g.running) return 0;
   volatile EngCtl* c = g.ctl;
-  c->hstop = 1;
+  reinterpret_cast<volatile EngIn*>(g.in)->hstop = 1;
   const auto t0 = Clock::now();
   while (!c->exited) {
     if (Clock::now() - t0 > std::chrono::seconds(10)) return NOVA_E_NODEV;  // still running; retried later
@@ -1325,7 +1370,7 @@ int engine_stop(Engine& g) {
   const uint32_t why = c->why;
   g.exits[why < kWhyN ? why : 0]++;
   g.running = false;
-  c->hstop = 0;
+  reinterpret_cast<volatile EngIn*>(g.in)->hstop = 0;
   return e == hipSuccess ? 0 : (int)e;
 }
 
@@ -1346,7 +1391,7 @@ Engine* engine_if_live() {
 
 void bump_yield_locked(Engine& g) {
   g.ygen++;
-  reinterpret_cast<volatile uint64_t*>(&g.ctl->hyield)[0] = g.ygen;
+  reinterpret_cast<volatile EngIn*>(g.in)->hyield = g.ygen;
 }
 
 }  // namespace
@@ -1439,10 +1484,10 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
         (uint32_t)(uint64_t)out, (uint32_t)((uint64_t)out >> 32), (uint32_t)(uint64_t)bad,
         (uint32_t)((uint64_t)bad >> 32), (uint32_t)n, (flags & 0xffffu) | ((uint32_t)mode << 16) | (cb << 20)};
     const uint64_t tag = (uint64_t)(uint32_t)(seq + 1) << 32;
-    volatile uint64_t* w = g.ring[seq % kRing].w;
+    volatile uint64_t* w = reinterpret_cast<volatile EngIn*>(g.in)->ring[seq % kRing].w;
     for (uint32_t k = 0; k < kWords; k++) w[k] = tag | half[k];  // one 8-B store each
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    reinterpret_cast<volatile uint64_t*>(&g.ctl->htail)[0] = seq + 1;
+    reinterpret_cast<volatile EngIn*>(g.in)->htail = seq + 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     g.requests++;
     if (g.relaunch_if_exited_locked()) {
@@ -1614,7 +1659,8 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
       gp->exits[kWhyIdle], gp->exits[kWhyYield], gp->exits[kWhyStop], gp->exits[kWhyLost],
       gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
       (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice], gp->launch_ns_max / 1000,
-      gp->launch_slow, gp->gap_ticks_max / 100, gp->sleep_waits, (uint64_t)gp->max_spinners};
+      gp->launch_slow, gp->gap_ticks_max / 100, gp->sleep_waits, (uint64_t)gp->max_spinners,
+      (uint64_t)gp->in_dev};
   for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
   return 0;
 }

@@ -429,13 +429,14 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
                                           "exits_yield", "exits_stop", "exits_lost", "timeouts", "errors",
                                           "taken_back", "unsafe", "yield_waits", "yield_bumps", "broken",
                                           "backing_off", "exits_slice", "launch_us_max", "launch_slow",
-                                          "poll_gap_us_max", "sleep_waits", "max_spinners"};
+                                          "poll_gap_us_max", "sleep_waits", "max_spinners",
+                                          "ring_device"};
   for (int i = 0; i < NOVA_ENGINE_COUNTERS; i++) {
     if (i == 3 || i == 14 || i == 15) continue;  // states, not counts
     char b[64];
-    // launch_us_max: a maximum, not a count
+    // launch_us_max, poll_gap_us_max, max_spinners, ring_device: not counts
     snprintf(b, sizeof b, "%s\"%s\": %llu", eng.size() > 1 ? ", " : "", cn[i],
-             (unsigned long long)(i == 17 || i == 19 || i == 21 ? c1[i] : c1[i] - c0[i]));
+             (unsigned long long)(i == 17 || i == 19 || i == 21 || i == 22 ? c1[i] : c1[i] - c0[i]));
     eng += b;
   }
   eng += "}";
