@@ -239,6 +239,7 @@ struct EngParams {
   uint64_t give_up_ticks;  // no new ticket (worker) / an unfinished request (dispatcher) this long: exit
   uint64_t slice_ticks;    // 0, or: take no request after running this long (then exit; the next instance follows)
   uint64_t* htrace;        // trace (or null): per request, the tr words copied to pinned memory
+  uint32_t page_poll;      // waiting workers poll their ticket's page (NOVA_SST_ENGINE_PAGE_POLL, default 1)
   CrcParams tab;           // tables and zero line for every chunk
 };
 
@@ -412,9 +413,20 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
       }
       if ((uint32_t)lane < m) {
         const uint64_t seq = seen + lane;
-        EngSlot* S = &d->slot[seq % kRing];
         // the slot's previous request (seq - kRing) is done: its counters are free
         for (uint32_t x = 0; x < kCntGroups; x++) st_agent(&d->cgrp[seq % kRing][x][0], 0u);
+        if (e.htrace) {
+          st_agent(&d->tr[seq % kRing][0], now_ticks());
+          for (uint32_t k = 1; k < 12; k++) st_agent(&d->tr[seq % kRing][k], (uint64_t)0);
+        }
+      }
+      // the counters are zero before any page or slot names the request: a
+      // waiting worker that finds its ticket in a page runs the chunk at once,
+      // before the end word moves
+      drain_vm();
+      if ((uint32_t)lane < m) {
+        const uint64_t seq = seen + lane;
+        EngSlot* S = &d->slot[seq % kRing];
         st_agent(&S->cstart, cend + inc - nch);
         st_agent(&S->cend, cend + inc);
         st_agent(&S->base, r.base);
@@ -426,10 +438,6 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
         st_agent(&S->mode, r.mode);
         st_agent(&S->flags, r.flags);
         st_agent(&S->cb, r.cb);
-        if (e.htrace) {
-          st_agent(&d->tr[seq % kRing][0], now_ticks());
-          for (uint32_t k = 1; k < 12; k++) st_agent(&d->tr[seq % kRing][k], (uint64_t)0);
-        }
         st_agent(&S->seq1, seq + 1);
       }
       const uint64_t total = uni64(((uint64_t)(uint32_t)__shfl((int)(uint32_t)(inc >> 32), 63) << 32) |
@@ -691,11 +699,38 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
   uint64_t r = e.first_seq;  // request cursor (the wave's tickets only grow)
   uint64_t dend = 0;
   uint64_t t = claim();
+  // t's ticket page: lanes 0-15 read its 16 words (one round trip); `found`
+  // if it holds a consistent copy of a request of this instance whose
+  // tickets hold t (tickets are unique within an instance; seqs of earlier
+  // instances are below first_seq)
+  uint64_t pw = 0, pseq1 = 0, pcs = 0;
+  bool found = false;
+  auto read_page = [&]() {
+    pw = 0;
+    if (lane < (int)kPWords) pw = ld_agent(&d->page[(t >> kPageShift) & (kPages - 1)].w[lane]);
+    const uint32_t ptag = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pw >> 32), 0);
+    const bool pcons = ptag != 0 &&
+        (__builtin_amdgcn_ballot_w64(lane < (int)kPWords && (uint32_t)(pw >> 32) == ptag) & 0xffffull) == 0xffffull;
+    auto pl = [&](uint32_t k) -> uint64_t { return (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pw, (int)k); };
+    pseq1 = pcons ? (pl(kPSeqHi) << 32 | ptag) : 0;
+    pcs = pl(kPCsLo) | pl(kPCsHi) << 32;
+    found = pcons && pseq1 > e.first_seq && t >= pcs && t < pcs + pl(kPNch);
+  };
   for (;;) {
+    found = false;
     if (t >= dend) {  // wait for the ticket to be published, or for the stop
       constexpr uint32_t kPoll = poll_off<G>();
       uint64_t t0 = now_ticks();
       for (uint32_t spin = 0;; spin++) {
+        // t's page, read directly: the dispatcher writes a request's pages
+        // (after zeroing its counters) before it moves the end word, so a
+        // found page starts the chunk one end-word hop earlier
+        // (profiles/r05_engine_page_poll_ab.log); a page that does not hold
+        // t's request (t's request began mid-page) waits for the end word
+        if (e.page_poll) {
+          read_page();
+          if (found) break;
+        }
         // the workgroup's copy first; then, if no other wave of this CU is
         // reading them, the device's words (published into the copy)
         // (atomic loads: other waves write these words; a plain load could be hoisted)
@@ -760,17 +795,9 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
     // written before t was published.
     uint64_t cstart = 0, cend = 0, base = 0, offs = 0, sizes = 0, out = 0, bad = 0, n = 0;
     uint32_t mode = 0, flags = 0, cb = 0;
-    // t's page: lanes 0-15 read its 16 words (one round trip)
-    uint64_t pw = 0;
-    if (lane < (int)kPWords) pw = ld_agent(&d->page[(t >> kPageShift) & (kPages - 1)].w[lane]);
+    if (!found) read_page();  // (published: t < dend)
     auto pl = [&](uint32_t k) -> uint64_t { return (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pw, (int)k); };
-    const uint32_t ptag = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pw >> 32), 0);
-    const bool pcons = ptag != 0 &&
-        (__builtin_amdgcn_ballot_w64(lane < (int)kPWords && (uint32_t)(pw >> 32) == ptag) & 0xffffull) == 0xffffull;
-    const uint64_t pseq1 = pcons ? (pl(kPSeqHi) << 32 | ptag) : 0;
-    const uint64_t pcs = pl(kPCsLo) | pl(kPCsHi) << 32;
-    bool found = pcons && pseq1 > e.first_seq && t >= pcs && t < pcs + pl(kPNch);
-    if (found) {  // the page's copy is t's request (seqs of earlier instances are below first_seq)
+    if (found) {  // the page's copy is t's request
       r = pseq1 - 1;
       cstart = pcs;
       cend = pcs + pl(kPNch);
@@ -1218,6 +1245,8 @@ struct Engine {
     p.give_up_ticks = 20ull * 100000000ull;  // 20 s (every spin of the engine is bounded)
     p.slice_ticks = (uint64_t)slice_us * 100;
     p.htrace = trace ? htrace : nullptr;
+    static const uint32_t page_poll = (uint32_t)env_u64("NOVA_SST_ENGINE_PAGE_POLL", 1);
+    p.page_poll = page_poll;
     p.tab.tab_main = t->main[gindex(kEngG)];
     p.tab.tab_tree = t->tree;
     p.tab.tab_ft = t->ft;
