@@ -233,6 +233,11 @@ int nova_sst_engine_reset(void);
 /* Test hook, calling thread only: wait `us` after submitting a request before
  * waiting for it (a waiter descheduled past a whole ring turn). */
 void nova_sst_engine_set_wait_delay_us(uint32_t us);
+/* The calling thread's last engine request, out[0..n) (n <= 8): host ns
+ * waiting for the engine's lock, ns holding it (ring writes, a relaunch), ns
+ * waiting for the completion words; sleeps during that wait, relaunches
+ * it made; the request's seq and blocks per chunk; 1 if it ended spinning. */
+int nova_sst_engine_last_call(uint64_t* out, size_t n);
 /* Route the nova_sst_queue_* calls of this process: 1 the engine, 0 the
  * coalescing queue, -1 back to NOVA_SST_ENGINE (default: the engine). */
 int nova_sst_engine_set_enabled(int on);

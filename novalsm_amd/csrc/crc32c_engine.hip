@@ -197,7 +197,12 @@ enum EngPageWord : uint32_t {
 struct EngPage {
   uint64_t w[kPWords];
 };
-struct EngDev {  // device memory: all zeroed once; the header before every launch
+// An instance's words in device memory.  Two of them, used by alternate
+// instances (generation parity): each instance's dispatcher zeroes the OTHER
+// one as its last act, so the next instance starts on a zeroed header without
+// a memset packet ahead of its launch (a relaunch at every time slice; ~170 us
+// of waiting callers with the memset: profiles/r05_engine_slowest.log).
+struct EngHdr {
   uint64_t dend;  // chunk tickets published
   uint64_t p0[15];
   uint32_t dstop;
@@ -205,7 +210,11 @@ struct EngDev {  // device memory: all zeroed once; the header before every laun
   uint64_t reqs_done;
   uint64_t p2[15];
   uint32_t head[kCntGroups][32];  // per-group ticket heads, one 128-B line each
-  // ---- end of the per-launch header.  Below: a slot's counters are zeroed by
+};
+constexpr uint32_t kHdrWords = sizeof(EngHdr) / 8;
+struct EngDev {  // device memory: all zeroed once
+  EngHdr hdr[2];
+  // ---- below: a slot's counters are zeroed by
   // the dispatcher when it writes the slot; slots and pages from an earlier
   // instance hold seqs below the new first_seq, which the lookup never takes.
   // Chunks finished, per slot: one counter per ticket group t % 8 (1/8 of the
@@ -223,7 +232,6 @@ struct EngDev {  // device memory: all zeroed once; the header before every laun
   uint64_t tr[kRing][kTrWords];
   EngPage page[kPages];      // ticket page -> a copy of the request holding its first ticket
 };
-constexpr size_t kDevHeader = offsetof(EngDev, cgrp);
 struct EngParams {
   const EngIn* in;          // host -> engine words
   // hdone[(seq % kRing) * 8 + g] = seq + 1 once group g's results of the request
@@ -232,6 +240,8 @@ struct EngParams {
   uint64_t* hdone;
   EngCtl* ctl;
   EngDev* dev;
+  EngHdr* hdr;             // this instance's header (zeroed)
+  EngHdr* hdr_next;        // the next instance's: zeroed by this dispatcher at its exit
   uint64_t first_seq;
   uint64_t gen;            // this instance's generation (stored to ctl->alive)
   uint64_t yield_gen;      // in->hyield at launch: any other value is a yield
@@ -485,7 +495,7 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
       }
       drain_vm();  // every lane's slot and page stores are written through before the end moves
       cend += total;
-      if (lane == 0) st_agent(&d->dend, cend);
+      if (lane == 0) st_agent(&e.hdr->dend, cend);
       // groups without tickets in a request (all 8 for one taken back) are
       // done now; they count toward the dispatcher's expected completions
       uint32_t idle_groups = 0;
@@ -508,17 +518,24 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
     const uint64_t quiet = now_ticks() - last;
     if (drain || quiet > e.idle_ticks) {
       uint64_t done = 0;
-      if (lane == 0) done = ld_agent(&d->reqs_done);
+      if (lane == 0) done = ld_agent(&e.hdr->reqs_done);
       // every request taken is finished: all 8 groups of each
       const bool all_done = uni64(done) + auto_done == kCntGroups * (seen - e.first_seq);
       // a request unfinished long after the last arrival cannot finish: give up
       const bool lost = !all_done && quiet > e.give_up_ticks;
       if (all_done || lost) {
+        // the next instance's header, zeroed and drained before `exited`
+        // (every worker of this instance uses e.hdr only)
+        {
+          uint64_t* z = reinterpret_cast<uint64_t*>(e.hdr_next);
+          for (uint32_t k = (uint32_t)lane; k < kHdrWords; k += 64) st_agent(&z[k], (uint64_t)0);
+          drain_vm();
+        }
         if (lane == 0) {
           if (lost) st_sys(&e.ctl->error, 3u);
           st_sys(&e.ctl->why, lost ? kWhyLost : stop ? kWhyStop : yielded ? kWhyYield : sliced ? kWhySlice : kWhyIdle);
           st_sys(&e.ctl->maxgap, maxgap);
-          st_agent(&d->dstop, 1u);
+          st_agent(&e.hdr->dstop, 1u);
           st_sys(&e.ctl->consumed, seen);
           __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)&e.ctl->exited, 1u,
                              __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -693,7 +710,7 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
   auto claim = [&]() -> uint64_t {
     uint32_t k = 0;
     if (lane == 0)
-      k = __hip_atomic_fetch_add((g32*)&d->head[xcc][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      k = __hip_atomic_fetch_add((g32*)&e.hdr->head[xcc][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return xcc + (uint64_t)kCntGroups * uni32(k);
   };
   uint64_t r = e.first_seq;  // request cursor (the wave's tickets only grow)
@@ -747,8 +764,8 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
           uint64_t g = 0;
           uint32_t gs = 0;
           if (lane == 0) {
-            g = ld_agent(&d->dend);
-            gs = ld_agent(&d->dstop);
+            g = ld_agent(&e.hdr->dend);
+            gs = ld_agent(&e.hdr->dstop);
             // only the lock holder writes them, so a plain compare is enough
             if (g > __hip_atomic_load(lds64(kPoll), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
               __hip_atomic_store(lds64(kPoll), g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -925,7 +942,7 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
           drain_vm();
         }
         st_sys(&e.hdone[(r % kRing) * kCntGroups + grp], r + 1);
-        __hip_atomic_fetch_add((g64*)&d->reqs_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add((g64*)&e.hdr->reqs_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     // the next ticket: claimed after this chunk is counted (the claim's add
@@ -999,6 +1016,14 @@ constexpr int kEngineUnsafe = -1000;
 constexpr uint64_t kRingWaitMs = 1000;
 
 thread_local uint32_t tl_wait_delay_us = 0;  // test hook: nova_sst_engine_set_wait_delay_us
+// This thread's last engine request (nova_sst_engine_last_call): where its
+// time went on the host -- waiting for the engine's lock, holding it
+// (ring writes, a relaunch), waiting for the completion words -- how many
+// of the waits slept, and whether the wait relaunched the engine.
+struct LastCall {
+  uint64_t lock_ns = 0, held_ns = 0, wait_ns = 0, sleeps = 0, relaunched = 0, seq = 0, cb = 0, spun = 0;
+};
+thread_local LastCall tl_last;
 
 uint64_t stream_key(hipStream_t s) {
   if (s == hipStreamPerThread)  // one alias per thread: key by the thread
@@ -1006,8 +1031,25 @@ uint64_t stream_key(hipStream_t s) {
   return (uint64_t)(uintptr_t)s;
 }
 
+// The engine's host lock: held for ~1 us per request (ring words), ~70 us for
+// a relaunch.  Waiters spin (then yield) instead of sleeping on a futex: at
+// 16 callers a woken waiter waited 0.3-8 ms for a CPU
+// (profiles/r05_engine_slowest.log: lock waits of the slowest calls).
+struct SpinMutex {
+  std::atomic<bool> f{false};
+  void lock() {
+    for (uint32_t i = 0; f.exchange(true, std::memory_order_acquire); i++)
+      while (f.load(std::memory_order_relaxed)) {
+        if (++i < 4096) __builtin_ia32_pause();
+        else std::this_thread::yield();
+      }
+  }
+  bool try_lock() { return !f.load(std::memory_order_relaxed) && !f.exchange(true, std::memory_order_acquire); }
+  void unlock() { f.store(false, std::memory_order_release); }
+};
+
 struct Engine {
-  std::mutex mu;
+  SpinMutex mu;
   bool ready = false, broken = false, running = false;
   int dev = 0;
   int cus = 0;
@@ -1210,15 +1252,11 @@ struct Engine {
   int launch_locked_(uint64_t first) {
     // No host wait for the previous instance: its dispatcher has exited (it
     // took no more requests and finished the ones it took), its workers only
-    // see the stop and end, and the header reset and the new instance follow
-    // it in stream order.  (A stream sync here cost every relaunch -- every
-    // time slice, every yield -- a host round trip.)
-    hipError_t e = hipMemsetAsync(ddev, 0, kDevHeader, stream);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      running = false;
-      return (int)e;
-    }
+    // see the stop and end, and the new instance follows it in stream order.
+    // (A stream sync here cost every relaunch -- every time slice, every
+    // yield -- a host round trip.)  Its header was zeroed by the previous
+    // instance's dispatcher (EngHdr), or at init.
+    hipError_t e = hipSuccess;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     volatile EngCtl* c = ctl;
     c->exited = 0;
@@ -1238,6 +1276,8 @@ struct Engine {
     p.hdone = hdone;
     p.ctl = ctl;
     p.dev = ddev;
+    p.hdr = &ddev->hdr[(gen + 1) & 1];
+    p.hdr_next = &ddev->hdr[gen & 1];
     p.first_seq = first;
     p.gen = gen + 1;
     p.yield_gen = wait_for_yielded_locked();
@@ -1385,7 +1425,7 @@ Engine* engine_for_device(int* err) {
 }
 
 int engine_stop(Engine& g) {
-  std::lock_guard<std::mutex> lk(g.mu);
+  std::lock_guard<SpinMutex> lk(g.mu);
   if (!g.ready || !g.running) return 0;
   volatile EngCtl* c = g.ctl;
   reinterpret_cast<volatile EngIn*>(g.in)->hstop = 1;
@@ -1483,8 +1523,12 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   if (g.backing_off()) return NOVA_E_NODEV;
   uint64_t seq = 0;
   bool failed = false;
+  LastCall lc;
+  const auto t_lock = Clock::now();
   {
-    std::unique_lock<std::mutex> lk(g.mu);
+    std::unique_lock<SpinMutex> lk(g.mu);
+    const auto t_held = Clock::now();
+    lc.lock_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_held - t_lock).count();
     if (g.broken) return NOVA_E_NODEV;
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -1523,6 +1567,9 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
       g.errors++;
       failed = true;
     }
+    lc.seq = seq;
+    lc.cb = cb;
+    lc.held_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t_held).count();
   }
   if (tl_wait_delay_us)  // test hook: this waiter starts late (past a ring turn)
     std::this_thread::sleep_for(std::chrono::microseconds(tl_wait_delay_us));
@@ -1542,13 +1589,14 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
     if (g.done(seq)) break;
     if (!spinning || (spin & 255) == 255) {
       if (c->error) {
-        std::lock_guard<std::mutex> lk(g.mu);
+        std::lock_guard<SpinMutex> lk(g.mu);
         g.errors++;
         failed = true;
         break;
       }
       if (c->exited) {
-        std::lock_guard<std::mutex> lk(g.mu);
+        std::lock_guard<SpinMutex> lk(g.mu);
+        lc.relaunched++;
         if (!g.done(seq) && g.relaunch_if_exited_locked()) {
           g.errors++;
           failed = true;
@@ -1556,7 +1604,7 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
         }
       }
       if (Clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
-        std::lock_guard<std::mutex> lk(g.mu);
+        std::lock_guard<SpinMutex> lk(g.mu);
         g.timeouts++;
         failed = true;
         break;
@@ -1574,17 +1622,21 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
       g.sleep_waits++;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(8));
+    lc.sleeps++;
     if (g.spinners.load(std::memory_order_relaxed) < g.max_spinners) {  // a spinner left: take its place
       if (g.spinners.fetch_add(1) < g.max_spinners) spinning = true;
       else g.spinners.fetch_sub(1);
     }
   }
   if (spinning) g.spinners.fetch_sub(1);
+  lc.spun = spinning ? 1 : 0;
+  lc.wait_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+  tl_last = lc;
   if (slack >= 0) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
   if (failed) {
     int rc = 0;
     {
-      std::lock_guard<std::mutex> lk(g.mu);
+      std::lock_guard<SpinMutex> lk(g.mu);
       rc = g.take_back_locked(seq);
     }
     g.back_off();
@@ -1637,7 +1689,7 @@ void engine_count_fallback() {
   int err = 0;
   Engine* g = engine_for_device(&err);
   if (!g) return;
-  std::lock_guard<std::mutex> lk(g->mu);
+  std::lock_guard<SpinMutex> lk(g->mu);
   g->fallbacks++;
 }
 
@@ -1649,7 +1701,7 @@ int nova_sst_engine_start(void) {
   int err = 0;
   Engine* gp = engine_for_device(&err);
   if (!gp) return err;
-  std::lock_guard<std::mutex> lk(gp->mu);
+  std::lock_guard<SpinMutex> lk(gp->mu);
   if (gp->broken) return NOVA_E_NODEV;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -1668,7 +1720,7 @@ int nova_sst_engine_stats(uint64_t* requests, uint64_t* launches, uint64_t* fall
   int err = 0;
   Engine* gp = engine_for_device(&err);
   if (!gp) return err;
-  std::lock_guard<std::mutex> lk(gp->mu);
+  std::lock_guard<SpinMutex> lk(gp->mu);
   if (requests) *requests = gp->requests;
   if (launches) *launches = gp->gen;
   if (fallbacks) *fallbacks = gp->fallbacks;
@@ -1681,7 +1733,7 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
   Engine* gp = engine_for_device(&err);
   if (!gp) return err;
   if (!out) return NOVA_E_INVAL;
-  std::lock_guard<std::mutex> lk(gp->mu);
+  std::lock_guard<SpinMutex> lk(gp->mu);
   const uint64_t v[NOVA_ENGINE_COUNTERS] = {
       gp->requests, gp->gen, gp->fallbacks,
       (uint64_t)(gp->running && gp->ctl && !((volatile EngCtl*)gp->ctl)->exited ? 1 : 0),
@@ -1698,7 +1750,7 @@ int nova_sst_engine_set_trace(int on) {
   int err = 0;
   Engine* gp = engine_for_device(&err);
   if (!gp) return err;
-  std::lock_guard<std::mutex> lk(gp->mu);
+  std::lock_guard<SpinMutex> lk(gp->mu);
   gp->trace = on != 0;  // from the next instance
   std::lock_guard<std::mutex> lt(gp->tmu);
   gp->tr_n = 0;
@@ -1747,7 +1799,7 @@ int nova_sst_engine_set_idle_us(uint32_t us) {
   int err = 0;
   Engine* gp = engine_for_device(&err);
   if (!gp) return err;
-  std::lock_guard<std::mutex> lk(gp->mu);
+  std::lock_guard<SpinMutex> lk(gp->mu);
   // the next instance; at most 1 s, below the workers' 20 s give-up
   gp->idle_us = us ? std::min<uint32_t>(us, kMaxIdleUs) : 1000;
   return 0;
@@ -1757,7 +1809,7 @@ int nova_sst_engine_set_slice_us(uint32_t us) {
   int err = 0;
   Engine* gp = engine_for_device(&err);
   if (!gp) return err;
-  std::lock_guard<std::mutex> lk(gp->mu);
+  std::lock_guard<SpinMutex> lk(gp->mu);
   // from the next instance; ~0u: no slice; 0: back to NOVA_SST_ENGINE_SLICE_US
   if (us == 0) {
     gp->slice_set = false;
@@ -1779,6 +1831,14 @@ int nova_sst_engine_set_timeout_ms(uint32_t ms) {
 
 void nova_sst_engine_set_wait_delay_us(uint32_t us) { tl_wait_delay_us = us; }
 
+int nova_sst_engine_last_call(uint64_t* out, size_t n) {
+  if (!out) return NOVA_E_INVAL;
+  const uint64_t v[8] = {tl_last.lock_ns, tl_last.held_ns, tl_last.wait_ns, tl_last.sleeps,
+                         tl_last.relaunched, tl_last.seq, tl_last.cb, tl_last.spun};
+  for (size_t i = 0; i < n && i < 8; i++) out[i] = v[i];
+  return 0;
+}
+
 int nova_sst_engine_yield(void* stream) {
   nova_dev::engine_yield_begin();
   nova_dev::engine_yield_end((hipStream_t)stream);
@@ -1789,7 +1849,7 @@ int nova_sst_engine_reset(void) {
   int err = 0;
   Engine* gp = engine_for_device(&err);
   if (!gp) return err;
-  std::lock_guard<std::mutex> lk(gp->mu);
+  std::lock_guard<SpinMutex> lk(gp->mu);
   gp->failures.store(0);
   gp->avoid_until_ns.store(0);
   return 0;

@@ -58,6 +58,7 @@ constexpr uint64_t kCounters = 1u << 20;  // verify: one zeroed mismatch counter
 
 struct Call {
   double t0, t1;  // seconds after the window's start
+  uint64_t lc[8];  // engine path: nova_sst_engine_last_call
 };
 
 struct Table {
@@ -266,7 +267,7 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
   for (int t = 0; t < T; t++) {
     th.emplace_back([&, t] {
       Table& tb = tabs[t];
-      tb.calls.reserve(1 << 20);
+      tb.calls.reserve(1 << 17);
       ready++;
       while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
       while (!stop.load(std::memory_order_relaxed)) {
@@ -279,8 +280,9 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
         }
         tb.set_calls[tb.ncalls % kSets]++;
         tb.ncalls++;
-        tb.calls.push_back({std::chrono::duration<double>(a - t_start).count(),
-                            std::chrono::duration<double>(b - t_start).count()});
+        Call cl{std::chrono::duration<double>(a - t_start).count(), std::chrono::duration<double>(b - t_start).count(), {}};
+        if (cfg->path == 1) (void)nova_sst_engine_last_call(cl.lc, 8);
+        tb.calls.push_back(cl);
       }
     });
   }
@@ -350,6 +352,7 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
   double bytes = 0;
   uint64_t calls_in = 0, total_calls = 0;
   std::vector<std::pair<double, double>> slow;  // (latency us, start s)
+  std::vector<std::pair<double, const Call*>> slowc;  // (latency us, call)
   for (auto& tb : tabs) {
     if (tb.rc && !rc) rc = tb.rc;
     total_calls += tb.ncalls;
@@ -358,6 +361,7 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
       if (c.t0 >= 0 && c.t1 <= window) {
         lat.push_back((c.t1 - c.t0) * 1e6);
         slow.push_back({(c.t1 - c.t0) * 1e6, c.t0});
+        slowc.push_back({(c.t1 - c.t0) * 1e6, &c});
         calls_in++;
       }
     }
@@ -409,6 +413,20 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
     sl += b;
   }
   sl += "]";
+  // the slowest engine calls, where their host time went (us): lock wait,
+  // lock held, completion wait, sleeps, relaunches in the wait, spun at the end
+  std::sort(slowc.begin(), slowc.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  std::string sd = "[";
+  for (size_t i = 0; cfg->path == 1 && i < slowc.size() && i < 5; i++) {
+    const uint64_t* l = slowc[i].second->lc;
+    char b[256];
+    snprintf(b, sizeof b, "%s{\"us\": %.1f, \"at_s\": %.4f, \"lock_us\": %.1f, \"held_us\": %.1f, \"wait_us\": %.1f, "
+             "\"sleeps\": %llu, \"relaunched\": %llu, \"spun\": %llu}", i ? ", " : "", slowc[i].first,
+             slowc[i].second->t0, l[0] / 1e3, l[1] / 1e3, l[2] / 1e3, (unsigned long long)l[3],
+             (unsigned long long)l[4], (unsigned long long)l[7]);
+    sd += b;
+  }
+  sd += "]";
   std::string plain = "null";
   if (pl) {
     const char* names[3] = {"verify_blocks", "log_verify_records", "crc32c_batch"};
@@ -463,14 +481,14 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
       "{\"op\": \"%s\", \"path\": \"%s\", \"threads\": %d, \"blocks_per_table\": %llu, \"table_bytes\": %llu, "
       "\"window_s\": %.3f, \"warm_s\": %.3f, \"calls\": %llu, \"calls_in_window\": %llu, "
       "\"aggregate_GBps\": %.1f, \"frac_of_8TBps\": %.4f, \"p50_us\": %.1f, \"p90_us\": %.1f, \"p99_us\": %.1f, "
-      "\"p999_us\": %.1f, \"max_us\": %.1f, \"max_over_p50\": %.2f, \"slowest_us_at_s\": %s, "
+      "\"p999_us\": %.1f, \"max_us\": %.1f, \"max_over_p50\": %.2f, \"slowest_us_at_s\": %s, \"slowest_detail\": %s, "
       "\"engine\": %s, \"trace\": %s, \"cpu_throttled_periods\": %llu, \"cpu_throttled_us\": %llu, \"plain\": %s, "
       "\"wrong_results\": %llu, \"verified\": %s, \"rc\": %d}",
       verify ? "verify" : "trailers", cfg->path == 0 ? "direct" : cfg->path == 1 ? "engine" : "queue", T,
       (unsigned long long)cfg->blocks, (unsigned long long)(T ? tabs[0].algo_bytes : 0), window, cfg->warm_s,
       (unsigned long long)total_calls, (unsigned long long)calls_in, bytes / window / 1e9,
       bytes / window / 8e12, p50, pct(lat, 0.9), pct(lat, 0.99), pct(lat, 0.999), lat.empty() ? 0.0 : lat.back(),
-      p50 > 0 ? (lat.empty() ? 0.0 : lat.back()) / p50 : 0.0, sl.c_str(), eng.c_str(), tr.c_str(),
+      p50 > 0 ? (lat.empty() ? 0.0 : lat.back()) / p50 : 0.0, sl.c_str(), sd.c_str(), eng.c_str(), tr.c_str(),
       (unsigned long long)(thr1 - thr0), (unsigned long long)(thr_us1 - thr_us0), plain.c_str(),
       (unsigned long long)wrong, verified ? "true" : "false", rc);
   for (auto& tb : tabs) free_table(tb);
