@@ -571,13 +571,20 @@ uint64_t flat_waves() {
 // 77 -> 31 us, 64K blocks 83 -> 70 us; 256K blocks unchanged).
 //
 // Logs pass their mean record span (bytes per record) as bytes_per_block.
-// Short records run in 4-lane groups: twice the records per round halves the
-// per-record steps.  Measured crossover over payloads U[1,512] .. U[1,4096] B
-// (profiles/r03_log_lanes_sweep.log): verify gains 1.5-11 points below ~1 KiB
-// mean span and loses 7 at 2 KiB; write, which also pays a scattered store per
-// record, gains only below ~400 B (+3.5 at 263 B, -2 at 520 B).
-constexpr uint64_t kLogNarrowVerify = 1280;
-constexpr uint64_t kLogNarrowWrite = 400;
+// Short records run in narrower lane groups: more records per round, fewer
+// padded steps per record.  Groups of 2 and 4 lanes load their records with
+// the default policy (launch_rounds), which keeps the lines two records share
+// in L2; with it the crossovers moved (round 5, payloads U[1,256] ..
+// U[1,4096] B, % of 8 TB/s, profiles/r05_log_lanes_cached.log):
+//   mean span      135 B  263 B  391 B  520 B  775 B  1031 B  2055 B
+//   write G=2/4/8  25/22/15  38/36/26  43/43/33  44/46/37  45/49/44  45/49/48  49/52/57
+//   verify G=2/4/8 26/22/14  42/38/25  47/47/33  47/50/39  48/55/50  50/57/56  52/57/66
+// (round 3, nt loads: 4 lanes won below ~1 KiB for verify and only below
+// ~400 B for write, profiles/r03_log_lanes_sweep.log).
+constexpr uint64_t kLogNarrowVerify = 1280;  // 4 lanes below
+constexpr uint64_t kLogNarrowWrite = 1280;
+constexpr uint64_t kLogPairVerify = 420;  // 2 lanes below
+constexpr uint64_t kLogPairWrite = 350;
 Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, bool large,
           uint32_t cus) {
   const bool log = mode == kLogWrite || mode == kLogVerify;
@@ -600,7 +607,8 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, b
   }
   if (pl.kernel == kRoundsK && log && tk == kAuto && tg == 0 && bytes_per_block &&
       bytes_per_block < (mode == kLogVerify ? kLogNarrowVerify : kLogNarrowWrite)) {
-    pl.G = 4;  // short records: 4-lane groups (log verify then runs without the pre-sort)
+    // short records: 4-lane groups, or 2 (log verify then runs without the pre-sort)
+    pl.G = bytes_per_block < (mode == kLogVerify ? kLogPairVerify : kLogPairWrite) ? 2 : 4;
   }
   if (pl.kernel == kRoundsK && log && tk == kAuto && tg == 0 && g_tune_chunk.load() == 0) {
     // log records (~2 KiB): 16-record chunks below 32 chunks' worth per wave

@@ -52,3 +52,4 @@ def test_request_tickets_split_over_groups(diag):
             assert share == want, (cs, ce)
         assert used == sum(1 for x in share if x), (cs, ce, share)
         assert max(share) - min(share) <= 1
+

@@ -364,3 +364,28 @@ def test_engine_leaves_other_streams_alone(torch_gpu, engine_on):
     assert res["bg"]["verified"], res["bg"]
     assert busy == 1  # the engine was resident throughout
     assert max(lat) < 0.1 and null < 0.1 and dsync < 0.05, (lat, null, dsync)
+
+
+@pytest.mark.parametrize("env", [{"NOVA_SST_ENGINE_RING": "host"}, {"NOVA_SST_ENGINE_PAGE_POLL": "0"}],
+                         ids=["host_ring", "no_page_poll"])
+def test_engine_alternate_paths(torch_gpu, env):
+    """The request ring in pinned host memory (the path of a device without a
+    large BAR) and workers that wait for the end word only (no page polls):
+    8 native callers for 0.5 s in a child process (the settings are read when
+    the engine starts), every result exact, nothing falls back."""
+    import os
+    import subprocess
+    import sys
+    code = ("import json, sys; sys.path.insert(0, %r); from novalsm_amd import callers; "
+            "print(json.dumps(callers.run('verify', 8, 4096, 0.5, 'engine', warm_s=0.1, seed=11)))"
+            % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True,
+                       text=True, timeout=100)
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert p.returncode == 0 and line, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    r = json.loads(line[-1])
+    assert r["verified"] and r["wrong_results"] == 0 and r["rc"] == 0, r
+    e = r["engine"]
+    assert e["fallbacks"] == 0 and e["timeouts"] == 0 and e["errors"] == 0, e
+    assert e["ring_device"] == (0 if "NOVA_SST_ENGINE_RING" in env else e["ring_device"]), e
+    assert r["calls_in_window"] >= 100, r

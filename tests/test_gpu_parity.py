@@ -2030,13 +2030,14 @@ def test_log_sorted_windows(torch_gpu, oracle, order):
         run()
 
 
-@pytest.mark.parametrize("pmax", [64, 600, 1500, 3000])
+@pytest.mark.parametrize("pmax", [64, 600, 800, 1500, 2400, 3000])
 def test_log_plan_by_record_size(torch_gpu, oracle, pmax):
     """The default log plan picks its group width from the mean record span
-    (buf_len / n): 4-lane groups for write below 400 B and for verify below
-    1280 B, 8-lane groups with the windowed pre-sort above.
-    Each side of both thresholds: write is bit-exact over the image, verify is
-    clean, and finds exactly the records whose payload was corrupted."""
+    (buf_len / n): 2-lane groups for write below 350 B and for verify below
+    420 B, 4-lane groups below 1280 B, 8-lane groups (verify: with the windowed
+    pre-sort) above.  Each side of every threshold: write is
+    bit-exact over the image, verify is clean, and finds exactly the records
+    whose payload was corrupted."""
     from novalsm_amd.synth import log_image
     torch = torch_gpu
     rng = np.random.default_rng(pmax)
@@ -2045,6 +2046,11 @@ def test_log_plan_by_record_size(torch_gpu, oracle, pmax):
     plen = rng.integers(1, pmax + 1, n)
     host, offs, _, _ = log_image(31, plen)
     assert len(offs) >= 1 << 16
+    span = host.size // len(offs)
+    for verify, pair in ((False, 350), (True, 420)):
+        g = 2 if span < pair else 4 if span < 1280 else 8
+        k = C.describe(len(offs) + 1, host.size // (len(offs) + 1), 0, log=True, log_verify=verify)["kernel"]
+        assert k.startswith(f"crc32c_rounds_kernel<{g}, "), (span, verify, k)
     # plus a probe at the end of the file: TRUNCATED, so nothing may be stored
     # for it (its header bytes read as a length past the block)
     offs = np.append(offs, np.uint64(host.size))

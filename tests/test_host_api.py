@@ -253,3 +253,17 @@ def test_split_plan(n, length, variable, large, piece, slots):
         lanes = ctypes.c_int(-1)
         seg = ctypes.c_uint32(0)
         assert C.load().nova_crc32c_plan(n, length, ctypes.byref(lanes), ctypes.byref(seg)) == 5
+
+
+@pytest.mark.parametrize("span,write_g,verify_g", [
+    (39, 2, 2), (263, 2, 2), (349, 2, 2), (350, 4, 2), (419, 4, 2), (420, 4, 4), (1279, 4, 4),
+    (1280, 8, 8), (2055, 8, 8)])
+def test_log_plan_lanes_by_span(span, write_g, verify_g):
+    """The log plan's group width by mean record span (crc32c_device.hip plan(),
+    round-5 crossovers, profiles/r05_log_lanes_cached.log): nova_crc32c_describe
+    runs the planner on the host."""
+    C.load(build_if_missing=True)
+    w = C.describe(300000, span, 0, log=True)["kernel"]
+    v = C.describe(300000, span, 0, log=True, log_verify=True)["kernel"]
+    assert w.startswith(f"crc32c_rounds_kernel<{write_g}, 3>"), (span, w)
+    assert v.startswith(f"crc32c_rounds_kernel<{verify_g}, 4>"), (span, v)

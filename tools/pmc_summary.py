@@ -36,8 +36,8 @@ STEP_KERNELS = {
     "sst4k_verify": ["crc32c_rounds_kernel<8, 2>"],
     "log4k_write": ["crc32c_rounds_kernel<8, 3>"],
     "log4k_verify": ["crc32c_rounds_kernel<8, 4>", "log_sort_kernel", "log_unperm_kernel"],
-    "log512_write": ["crc32c_rounds_kernel<4, 3>"],
-    "log512_verify": ["crc32c_rounds_kernel<4, 4>"],
+    "log512_write": ["crc32c_rounds_kernel<2, 3>"],
+    "log512_verify": ["crc32c_rounds_kernel<2, 4>"],
     "parity": ["xor_parity_kernel<8, 1>"],
 }
 SQ_COUNTERS = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
