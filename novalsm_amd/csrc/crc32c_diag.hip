@@ -1479,6 +1479,11 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
     if (var == kVarW16 && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarW16>(G, p, t, s, chunk);
     // A/B: default-policy data loads (lines two records share stay in L2)
     if (var == kVarCached && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarCached>(G, p, t, s, chunk);
+    // A/B: empty steps folded (the product's load policy by G, as launch_rounds)
+    if (var == kVarFoldEmpty && !p.out_pos && !p.perm) {
+      if (MODE != kVerify && G <= 4) return launch_rounds_v<MODE, kVarFoldEmpty | kVarCached>(G, p, t, s, chunk);
+      return launch_rounds_v<MODE, kVarFoldEmpty>(G, p, t, s, chunk);
+    }
   }
   if constexpr (MODE == kLogWrite || MODE == kLogVerify) {
     if (p.out_pos) {  // the product's sorted large-log path (G = 8), with the ablations

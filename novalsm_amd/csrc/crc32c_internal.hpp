@@ -119,6 +119,9 @@ constexpr int kVarEngine = 4096;
 // Rounds kernel (diagnostics A/B): 16 waves per workgroup
 // (launch bound 1024 threads: 128 VGPRs) instead of 12 (168 VGPRs).
 constexpr int kVarW16 = 8192;
+// Rounds kernel (diagnostics A/B): fold the empty steps a wave issues while
+// its next chunk's descriptors load, as rounds 1-4 did (the product skips them).
+constexpr int kVarFoldEmpty = 16384;
 
 constexpr size_t kLdsMax = 160 * 1024;  // per CU on MI355X
 constexpr int kMaxDevices = 64;

@@ -1920,7 +1920,9 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
     X.ninit = v ? g_ninit : 0u;
     X.valid = v;
     X.last = last;
-    X.skip = (run && r_step == 0) ? r_sk : 0u;  // wave-uniform
+    // wave-uniform; 4 (never a round's skip: r_sk <= 3) marks an empty step,
+    // which fold skips (kVarFoldEmpty: folds its zeros, the round-4 form)
+    X.skip = !run ? ((VAR & kVarFoldEmpty) ? 0u : 4u) : (r_step == 0 ? r_sk : 0u);
     if (run) {
       g_lp += kStep;
       if (++r_step == r_S) fl |= kBatch && r_clast ? (fRoundDone | fChunkEnd) : fRoundDone;
@@ -2040,6 +2042,13 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
     // wave holds a region piece (they read the zero line into zero registers),
     // so a round costs its longest block's lines, not whole 4-swath steps.
     const uint32_t sk = (uint32_t)__builtin_amdgcn_readfirstlane((int)Y.skip);
+    if (sk >= 4) {
+      // an empty step (the load side waited for the next chunk's descriptors):
+      // no region piece, nothing to fold -- give the SIMD's issue slots to the
+      // other waves instead of folding zeros (64 table lookups per lane)
+      __builtin_amdgcn_s_sleep(1);
+      return;
+    }
     if (Y.last) {  // wave-uniform: the region's last line may end past E
       if (sk < 1) swath4<VAR>(lds, c0, c1, c2, c3, d0, lo0, lo1, lo2, lo3);
       if (sk < 2) swath4<VAR>(lds, c0, c1, c2, c3, d1, lo0, lo1, lo2, lo3);

@@ -1387,7 +1387,9 @@ def test_queue_batched_trailers_adjacent_tables(torch_gpu, oracle, size):
             s = torch.cuda.Stream()
             with torch.cuda.stream(s):
                 gate.wait()
-                for _ in range(4):
+                # ~6 ms of queue calls: the callers' threads wake from the barrier
+                # late on a busy host (a millisecond and more on the GPU boxes)
+                for _ in range(16):
                     C.queue_verify_blocks(bimg, b_o, b_l, b_ok, stream=s)
         except Exception as e:  # pragma: no cover
             errors.append(e)
@@ -1405,14 +1407,14 @@ def test_queue_batched_trailers_adjacent_tables(torch_gpu, oracle, size):
             for x in th:
                 x.join()
             qa = C.queue_stats()
-            assert qa["requests"] - qb["requests"] == len(ns) + 4
-            if qa["batches"] - qb["batches"] < len(ns) + 4:
+            assert qa["requests"] - qb["requests"] == len(ns) + 16
+            if qa["batches"] - qb["batches"] < len(ns) + 16:
                 break
     finally:
         C.queue_set_slots(0)
         C.engine_set_enabled(-1)
     assert not errors, errors
-    assert qa["batches"] - qb["batches"] < len(ns) + 4, "the calls never shared a batch"
+    assert qa["batches"] - qb["batches"] < len(ns) + 16, "the calls never shared a batch"
     after = buf.cpu().numpy()
     expect = before.copy()
     for k, (o, ln, total) in enumerate(lays):

@@ -79,6 +79,7 @@ def main() -> int:
     ap.add_argument("--chunk-sweep", default="",
                     help="comma list of rounds-kernel chunk sizes (nova_diag_set_chunk_blocks), log ops")
     ap.add_argument("--no-ablations", action="store_true", help="skip the diagnostics ablations")
+    ap.add_argument("--lanes", type=int, default=0, help="force lanes per block/record (nova_crc32c_set_tuning)")
     ap.add_argument("--var-ab", default="",
                     help="comma list of rounds-kernel variants to A/B against the product (8192 16 waves, 2 cached)")
     ap.add_argument("--log-bound", action="store_true",
@@ -90,6 +91,8 @@ def main() -> int:
     import bench
 
     assert C.load().nova_device_init() == 0
+    if args.lanes:
+        C.set_tuning(args.lanes, 0)
     orc = load_oracle()
     stream = torch.cuda.current_stream()
     ops = args.ops.split(",")
