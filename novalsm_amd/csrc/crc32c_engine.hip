@@ -214,9 +214,8 @@ struct EngHdr {
 constexpr uint32_t kHdrWords = sizeof(EngHdr) / 8;
 struct EngDev {  // device memory: all zeroed once
   EngHdr hdr[2];
-  // ---- below: a slot's counters are zeroed by
-  // the dispatcher when it writes the slot; slots and pages from an earlier
-  // instance hold seqs below the new first_seq, which the lookup never takes.
+  // ---- below: slots and pages from an earlier instance hold seqs below the
+  // new first_seq, which the lookup never takes.
   // Chunks finished, per slot: one counter per ticket group t % 8 (1/8 of the
   // request's adds per address).  Same-address atomics serialize in memory;
   // one counter for all of a 1024-chunk request put ~1024 of them on the
@@ -224,7 +223,15 @@ struct EngDev {  // device memory: all zeroed once
   // completion word in host memory (hdone, 8 per request): a second-level
   // counter of the groups -- one more dependent device atomic on every
   // request's critical path -- is not needed.
-  uint32_t cgrp[kRing][kCntGroups][32];  // 128-B line each
+  // Two banks per slot: request seq counts in bank (seq / kRing) & 1, and the
+  // dispatcher, taking it, zeroes the OTHER bank -- the next occupant's
+  // (seq + kRing, published only once seq is done, after the drain that
+  // publishes seq).  So a request's counters were zeroed and drained one ring
+  // turn before it was taken, and a worker that finds its page before the end
+  // word moves never adds to a counter whose zeroing is still in flight; a
+  // request left unfinished (an instance that gave up) dirties only a bank the
+  // slot's next occupant zeroes.
+  uint32_t cgrp[kRing][2][kCntGroups][32];  // 128-B line each
   EngSlot slot[kRing];
   // trace (s_memrealtime): 0 dispatched, 2 last chunk done; chunk 0's wave:
   // 3 ticket seen, 1 slot found, 4 body done, 5 drained, 6 counted; the last
@@ -423,17 +430,18 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
       }
       if ((uint32_t)lane < m) {
         const uint64_t seq = seen + lane;
-        // the slot's previous request (seq - kRing) is done: its counters are free
-        for (uint32_t x = 0; x < kCntGroups; x++) st_agent(&d->cgrp[seq % kRing][x][0], 0u);
+        // the slot's previous request (seq - kRing) is done: the bank it
+        // counted in is the next occupant's (see EngDev::cgrp)
+        const uint32_t other = (uint32_t)((seq / kRing) & 1u) ^ 1u;
+        for (uint32_t x = 0; x < kCntGroups; x++) st_agent(&d->cgrp[seq % kRing][other][x][0], 0u);
         if (e.htrace) {
           st_agent(&d->tr[seq % kRing][0], now_ticks());
           for (uint32_t k = 1; k < 12; k++) st_agent(&d->tr[seq % kRing][k], (uint64_t)0);
         }
       }
-      // the counters are zero before any page or slot names the request: a
-      // waiting worker that finds its ticket in a page runs the chunk at once,
-      // before the end word moves
-      drain_vm();
+      // trace: the stamps are zero before a worker that finds its page early
+      // stores its own
+      if (e.htrace) drain_vm();
       if ((uint32_t)lane < m) {
         const uint64_t seq = seen + lane;
         EngSlot* S = &d->slot[seq % kRing];
@@ -740,8 +748,9 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
       uint64_t t0 = now_ticks();
       for (uint32_t spin = 0;; spin++) {
         // t's page, read directly: the dispatcher writes a request's pages
-        // (after zeroing its counters) before it moves the end word, so a
-        // found page starts the chunk one end-word hop earlier
+        // before it moves the end word (its counters were zeroed a ring turn
+        // earlier: EngDev::cgrp), so a found page starts the chunk one
+        // end-word hop earlier
         // (profiles/r05_engine_page_poll_ab.log); a page that does not hold
         // t's request (t's request began mid-page) waits for the end word
         if (e.page_poll) {
@@ -914,7 +923,7 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
       // this group's share: t' in [cstart, cend), t' % 8 == grp
       const uint32_t grp = xcc;
       const uint64_t mine = engine_group_share(cstart, cend, grp);
-      const uint32_t prev = __hip_atomic_fetch_add((g32*)&d->cgrp[r % kRing][grp][0], 1u, __ATOMIC_RELAXED,
+      const uint32_t prev = __hip_atomic_fetch_add((g32*)&d->cgrp[r % kRing][(r / kRing) & 1u][grp][0], 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t ts_count = e.htrace ? now_ticks() : 0;
       if (e.htrace && c == 0) {
