@@ -1480,6 +1480,8 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
     // A/B: default-policy data loads (lines two records share stay in L2)
     if (var == kVarCached && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarCached>(G, p, t, s, chunk);
     // A/B: empty steps folded (the product's load policy by G, as launch_rounds)
+    if (var == kVarLdSys && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarLdSys>(G, p, t, s, chunk);
+    if (var == kVarLdDev && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarLdDev>(G, p, t, s, chunk);
     if (var == kVarFoldEmpty && !p.out_pos && !p.perm) {
       if (MODE != kVerify && G <= 4) return launch_rounds_v<MODE, kVarFoldEmpty | kVarCached>(G, p, t, s, chunk);
       return launch_rounds_v<MODE, kVarFoldEmpty>(G, p, t, s, chunk);
@@ -1488,6 +1490,8 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
   if constexpr (MODE == kLogWrite || MODE == kLogVerify) {
     if (p.out_pos) {  // the product's sorted large-log path (G = 8), with the ablations
       if (var == kVarCached) return launch_rounds_v<MODE, kVarCached | kVarOutPos>(G, p, t, s, chunk);
+      if (var == kVarLdSys) return launch_rounds_v<MODE, kVarLdSys | kVarOutPos>(G, p, t, s, chunk);
+      if (var == kVarLdDev) return launch_rounds_v<MODE, kVarLdDev | kVarOutPos>(G, p, t, s, chunk);
       if (MODE == kLogVerify && var == kVarNoTail)
         return launch_rounds_v<MODE, kVarDiag | kVarNoTail | kVarOutPos>(G, p, t, s, chunk);
       if (round_epi) return launch_rounds_v<MODE, kVarDiag | kVarRoundEpi | kVarOutPos>(G, p, t, s, chunk);

@@ -122,6 +122,12 @@ constexpr int kVarW16 = 8192;
 // Rounds kernel (diagnostics A/B): fold the empty steps a wave issues while
 // its next chunk's descriptors load, as rounds 1-4 did (the product skips them).
 constexpr int kVarFoldEmpty = 16384;
+// Data-load cache policy A/Bs (diagnostics): system scope (a volatile 16-B
+// load: sc0 sc1) and device scope (two 8-B agent-scope atomic loads: sc1, L1
+// bypassed, L2 allocated as usual), against nt (product at 8+ lanes) and the
+// default policy (kVarCached, product for log records at 2-4 lanes).
+constexpr int kVarLdSys = 32768;
+constexpr int kVarLdDev = 65536;
 
 constexpr size_t kLdsMax = 160 * 1024;  // per CU on MI355X
 constexpr int kMaxDevices = 64;

@@ -101,10 +101,21 @@ typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 template <int VAR = 0>
 __device__ __forceinline__ uint4 gload16(uint64_t addr) {
   u32x4 v;
-  if constexpr ((VAR & kVarCached) != 0)
+  if constexpr ((VAR & kVarCached) != 0) {
     v = *reinterpret_cast<gu32x4*>(addr);
-  else
+  } else if constexpr ((VAR & kVarLdSys) != 0) {  // diagnostics A/B: sc0 sc1 (system scope)
+    v = *reinterpret_cast<volatile gu32x4*>(addr);
+  } else if constexpr ((VAR & kVarLdDev) != 0) {  // diagnostics A/B: sc1 (device scope), 2 x 8 B
+    typedef __attribute__((address_space(1))) uint64_t gu64a;
+    const uint64_t lo = __hip_atomic_load(reinterpret_cast<gu64a*>(addr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hi = __hip_atomic_load(reinterpret_cast<gu64a*>(addr + 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v.x = (uint32_t)lo;
+    v.y = (uint32_t)(lo >> 32);
+    v.z = (uint32_t)hi;
+    v.w = (uint32_t)(hi >> 32);
+  } else {
     v = __builtin_nontemporal_load(reinterpret_cast<gu32x4*>(addr));
+  }
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
