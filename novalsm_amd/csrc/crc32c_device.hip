@@ -488,8 +488,10 @@ void init_device(int dev, DevTables* t) {
   if ((t->err = set_lds_attrs_rounds<kLogVerify>())) return;
   if ((t->err = set_lds_attr_rounds<8, kLogWrite, kVarOutPos>())) return;
   if ((t->err = set_lds_attr_rounds<8, kLogVerify, kVarOutPos>())) return;
-  if ((t->err = set_lds_attrs_rounds<kLogWrite, kVarCached>())) return;
-  if ((t->err = set_lds_attrs_rounds<kLogVerify, kVarCached>())) return;
+  if ((t->err = set_lds_attr_rounds<2, kLogWrite, kVarCached>())) return;  // (2 and 4 lanes only)
+  if ((t->err = set_lds_attr_rounds<4, kLogWrite, kVarCached>())) return;
+  if ((t->err = set_lds_attr_rounds<2, kLogVerify, kVarCached>())) return;
+  if ((t->err = set_lds_attr_rounds<4, kLogVerify, kVarCached>())) return;
   if ((t->err = set_lds_attrs_mode<kStore>())) return;
   if ((t->err = set_lds_attrs_mode<kTrailer>())) return;
   if ((t->err = set_lds_attrs_mode<kVerify>())) return;

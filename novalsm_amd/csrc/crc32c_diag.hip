@@ -1475,23 +1475,20 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
   }
   const bool round_epi = var == kVarRoundEpi;  // A/B: the per-round epilogue (rounds 1-2 form)
   if constexpr (MODE == kLogWrite || MODE == kLogVerify || MODE == kVerify) {
-    // A/B: the product kernel at 16 waves per workgroup (short log records)
-    if (var == kVarW16 && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarW16>(G, p, t, s, chunk);
-    // A/B: default-policy data loads (lines two records share stay in L2)
-    if (var == kVarCached && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarCached>(G, p, t, s, chunk);
-    // A/B: empty steps folded (the product's load policy by G, as launch_rounds)
-    if (var == kVarLdSys && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarLdSys>(G, p, t, s, chunk);
-    if (var == kVarLdDev && !p.out_pos && !p.perm) return launch_rounds_v<MODE, kVarLdDev>(G, p, t, s, chunk);
-    if (var == kVarFoldEmpty && !p.out_pos && !p.perm) {
-      if (MODE != kVerify && G <= 4) return launch_rounds_v<MODE, kVarFoldEmpty | kVarCached>(G, p, t, s, chunk);
-      return launch_rounds_v<MODE, kVarFoldEmpty>(G, p, t, s, chunk);
-    }
+    // (16 waves per workgroup, kVarW16, and the system / device-scope load
+    // policies, kVarLdSys / kVarLdDev, were measured in round 5 and lost
+    // everywhere: profiles/r05_log_w16_ab.log, r05_load_policy_ab.log.  Their
+    // instantiations are no longer built: the diagnostics TU's compile time.)
+    // A/B: default-policy data loads (lines two records share stay in L2;
+    // log records: instantiated at 2 and 4 lanes only, launch_rounds_g)
+    if (var == kVarCached && !p.out_pos && !p.perm && (MODE == kVerify || G <= 4))
+      return launch_rounds_v<MODE, kVarCached>(G, p, t, s, chunk);
+    // (empty steps folded, kVarFoldEmpty: measured in round 5,
+    // profiles/r05_log_empty_steps_ab.log; no longer instantiated)
   }
   if constexpr (MODE == kLogWrite || MODE == kLogVerify) {
     if (p.out_pos) {  // the product's sorted large-log path (G = 8), with the ablations
       if (var == kVarCached) return launch_rounds_v<MODE, kVarCached | kVarOutPos>(G, p, t, s, chunk);
-      if (var == kVarLdSys) return launch_rounds_v<MODE, kVarLdSys | kVarOutPos>(G, p, t, s, chunk);
-      if (var == kVarLdDev) return launch_rounds_v<MODE, kVarLdDev | kVarOutPos>(G, p, t, s, chunk);
       if (MODE == kLogVerify && var == kVarNoTail)
         return launch_rounds_v<MODE, kVarDiag | kVarNoTail | kVarOutPos>(G, p, t, s, chunk);
       if (round_epi) return launch_rounds_v<MODE, kVarDiag | kVarRoundEpi | kVarOutPos>(G, p, t, s, chunk);
@@ -1503,8 +1500,16 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
     if (var == kVarNoTail) return launch_rounds_v<MODE, kVarDiag | kVarNoTail>(G, p, t, s, chunk);
   }
   // the whole-piece store forms live in the per-round epilogue
-  if (p.tr_flag || round_epi) return launch_rounds_v<MODE, kVarDiag | kVarRoundEpi>(G, p, t, s, chunk);
-  if (p.wvar || p.gate) return launch_rounds_v<MODE, kVarDiag>(G, p, t, s, chunk);
+  // (log records at 2-4 lanes: the product's default-policy loads, as launch_rounds)
+  constexpr bool kLogMode = MODE == kLogWrite || MODE == kLogVerify;
+  if (p.tr_flag || round_epi) {
+    if (kLogMode && G <= 4) return launch_rounds_v<MODE, kVarDiag | kVarRoundEpi | kVarCached>(G, p, t, s, chunk);
+    return launch_rounds_v<MODE, kVarDiag | kVarRoundEpi>(G, p, t, s, chunk);
+  }
+  if (p.wvar || p.gate) {
+    if (kLogMode && G <= 4) return launch_rounds_v<MODE, kVarDiag | kVarCached>(G, p, t, s, chunk);
+    return launch_rounds_v<MODE, kVarDiag>(G, p, t, s, chunk);
+  }
   if (p.perm) {  // sorted by the whole-batch pre-pass: the product kernels
     if (MODE == kStore && p.init) return launch_rounds_v<kStore, kVarInit>(G, p, t, s, chunk);
     return launch_rounds_v<MODE, 0>(G, p, t, s, chunk);

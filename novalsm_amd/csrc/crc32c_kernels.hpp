@@ -2678,6 +2678,12 @@ int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream
     if (G != 8) return NOVA_E_INVAL;
     hipLaunchKernelGGL((crc32c_rounds_kernel<8, MODE, VAR>), grid, block, lds, stream, p);
     return (int)hipGetLastError();
+  } else if constexpr ((VAR & kVarCached) != 0 && (MODE == kLogWrite || MODE == kLogVerify)) {
+    // default-policy log records run at 2 or 4 lanes only (launch_rounds)
+    if (G == 2) hipLaunchKernelGGL((crc32c_rounds_kernel<2, MODE, VAR>), grid, block, lds, stream, p);
+    else if (G == 4) hipLaunchKernelGGL((crc32c_rounds_kernel<4, MODE, VAR>), grid, block, lds, stream, p);
+    else return NOVA_E_INVAL;
+    return (int)hipGetLastError();
   } else {
   switch (G) {
     case 2: hipLaunchKernelGGL((crc32c_rounds_kernel<2, MODE, VAR>), grid, block, lds, stream, p); break;
