@@ -156,7 +156,7 @@ struct EngReq {  // an entry, decoded
 // writes through the PCIe BAR (a large-BAR device; else pinned host memory).
 // The dispatcher's poll then reads HBM instead of crossing PCIe: a host ->
 // GPU -> host ping-pong measured 1.90 us against 2.65 us through pinned
-// memory (tools/scratch/pingpong.hip, profiles/r05_pingpong.log).  The host
+// memory (tools/pingpong.hip, profiles/r05_pingpong.log).  The host
 // only writes these words, with one exception: the take-back reads its
 // cancel word back, which completes the posted write before it reads
 // `alive` (a PCIe read does not pass an earlier posted write).

@@ -1,8 +1,11 @@
 // Host <-> GPU ping-pong latency probe (engine dispatch latency, round 5).
 // One wave polls a flag word for the host's value k, then writes k back to a
 // pinned host word; the host waits for the echo and sends k+1.  Flag word in
-//   A: pinned host memory (the engine's ring today), GPU polls over PCIe;
-//   B: fine-grained device memory written by the host through the BAR.
+//   A: pinned host memory (the engine's ring until round 5), GPU polls over PCIe;
+//   B: fine-grained device memory written by the host through the BAR (the
+//      engine's ring since, crc32c_engine.hip EngIn).
+// Build and run on the GPU box:
+//   hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/pingpong.hip -o tools/pingpong && ./tools/pingpong
 // Every kernel spin is bounded (2 s of s_memrealtime), so the grid drains.
 #include <hip/hip_runtime.h>
 
