@@ -389,3 +389,74 @@ def test_engine_alternate_paths(torch_gpu, env):
     assert e["fallbacks"] == 0 and e["timeouts"] == 0 and e["errors"] == 0, e
     assert e["ring_device"] == (0 if "NOVA_SST_ENGINE_RING" in env else e["ring_device"]), e
     assert r["calls_in_window"] >= 100, r
+
+
+def test_engine_mixed_request_sizes(torch_gpu, oracle, engine_on):
+    """Tiny and large requests in flight together: 6 threads, each with tables
+    of 1, 2, 7, 64, 65, 300, 1024 and 5000 blocks, alternating verify (one
+    corrupted block) and trailer writes (trailer bytes scrubbed first) 6 times
+    over.  Small requests leave most ticket groups without tickets (their
+    completion words are written at publication), share ticket pages with
+    their neighbours and count in either completion bank; every result equals
+    the plain path's (trailers) or the expectation (verify)."""
+    import threading
+    from bench import sst4k_layout
+    torch = torch_gpu
+    sizes = [1, 2, 7, 64, 65, 300, 1024, 5000]
+    tabs = []
+    for k, n in enumerate(sizes):
+        offs_np, lens_np, total = sst4k_layout(n, 70 + k)
+        img = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        C.fill_splitmix64(img, 7000 + k)
+        offs = torch.from_numpy(offs_np.view(np.int64)).cuda()
+        lens = torch.from_numpy(lens_np.view(np.int32)).cuda()
+        C.write_trailers(img, offs, lens)  # the plain path: the reference image
+        torch.cuda.synchronize()
+        ends = torch.from_numpy((offs_np.astype(np.int64) + lens_np.astype(np.int64))).cuda()
+        tabs.append(dict(n=n, offs=offs, lens=lens, want=img.clone(), ends=ends,
+                         j=(5 * n) // 7, cut=int(offs_np[(5 * n) // 7]) + 2))
+    want0 = tabs[0]["want"].cpu().numpy()
+    assert oracle.verify(want0[int(tabs[0]["offs"][0]):int(tabs[0]["ends"][0]) + 5].tobytes())
+    errors = []
+
+    def work(t):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                mine = [dict(tb, img=tb["want"].clone()) for tb in tabs]
+                s.synchronize()
+                for rep in range(6):
+                    for k in range((t + rep) % len(sizes), (t + rep) % len(sizes) + len(sizes)):
+                        tb = mine[k % len(sizes)]
+                        if (rep + k) % 2:
+                            for b in range(5):  # scrub the trailers, then write them
+                                tb["img"][tb["ends"] + b] = 0xEE
+                            C.queue_write_trailers(tb["img"], tb["offs"], tb["lens"], stream=s)
+                            if not torch.equal(tb["img"], tb["want"]):
+                                errors.append((t, rep, tb["n"], "trailers"))
+                                return
+                        else:
+                            tb["img"][tb["cut"]] ^= 0x40
+                            ok = torch.full((tb["n"],), 7, dtype=torch.uint8, device="cuda")
+                            nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+                            C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, nb, stream=s)
+                            okh = ok.cpu().numpy()
+                            exp = np.ones(tb["n"], np.uint8)
+                            exp[tb["j"]] = 0
+                            if not np.array_equal(okh, exp) or int(nb.item()) != 1:
+                                errors.append((t, rep, tb["n"], "verify", np.nonzero(okh != exp)[0][:4]))
+                                return
+                            tb["img"][tb["cut"]] ^= 0x40
+        except Exception as e:  # pragma: no cover
+            errors.append((t, repr(e)))
+
+    c0 = C.engine_counters()
+    th = [threading.Thread(target=work, args=(t,)) for t in range(6)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    c1 = C.engine_counters()
+    assert not errors, errors[:4]
+    assert c1["requests"] - c0["requests"] >= 6 * 6 * len(sizes), (c0, c1)
+    assert c1["fallbacks"] == c0["fallbacks"] and c1["timeouts"] == c0["timeouts"], (c0, c1)
