@@ -384,6 +384,33 @@ def parity_copy_ceiling(torch, C, buf, fo, plen, stream, args) -> dict:
     return best
 
 
+def read_ceiling(torch, C, buf, nbytes: int, stream) -> dict:
+    """Config 2's own bound, in the same run ("also report against
+    a measured device read-only streaming ceiling"): a kernel that only reads
+    the same bytes and XOR-folds them (read_ceiling_kernel of the diagnostics
+    library), non-temporal loads, 4-16 in flight per lane, over a few grids; the
+    fastest form is the ceiling (tools/read_probe.hip swept 72 shapes: 88.9 %
+    at best, profiles/r05_read_ceiling.log)."""
+    D = C.load_diag()
+    sink = torch.empty(1024 * 1024, dtype=torch.int32, device=buf.device)
+    best, forms = None, {}
+    for u, wgs, t1024 in ((8, 256, False), (4, 1024, False), (16, 256, False), (8, 256, True)):
+        v = u | 0x100 | (0x200 if t1024 else 0)
+
+        def f(v=v, wgs=wgs):
+            rc = D.nova_diag_read_ceiling(buf.data_ptr(), nbytes, sink.data_ptr(), wgs, v, stream.cuda_stream)
+            assert rc == 0, rc
+        sec = _events_avg_s(torch, f, stream)
+        gbs = nbytes / sec / 1e9
+        forms[f"u{u}_wg{wgs}_t{1024 if t1024 else 256}"] = round(gbs, 1)
+        if best is None or gbs > best["achieved"]:
+            best = {"kind": "read-only nt stream of the same bytes (read_ceiling_kernel, diagnostics library)",
+                    "achieved": round(gbs, 1), "unit": "GB/s", "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+    best["forms_GBps"] = forms
+    del sink
+    return best
+
+
 def h2d_ceiling(torch, host, dev_tmp, chunk: int, n_streams: int = 3) -> dict:
     """Config 5's own bound, in the same run: pinned-host -> HBM copies of the
     same bytes with hipMemcpyAsync (torch copy_, non_blocking), as one copy and
@@ -663,6 +690,8 @@ def run_device_config(cfg: int, args, ctx: Ctx) -> dict:
         oks = ctx.all_gather_f64(1.0 if ok else 0.0)  # every rank learns whether any shard failed
         verified = bool(min(oks) > 0)
 
+    if cfg == 2 and not ctx.on and not getattr(args, "no_read_ceiling", False):
+        ceiling = read_ceiling(torch, C, buf, bytes_step, stream)
     achieved = bytes_step / avg_launch_s / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4)}
