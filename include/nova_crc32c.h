@@ -306,7 +306,11 @@ int nova_xor_parity(const void* base, const uint64_t* frag_offsets, size_t n_fra
  * Synchronous.  Pageable memory is registered (hipHostRegister) for the
  * duration of the call.
  *
- * BASELINE config 5, fixed stride: chunks of chunk_blocks blocks. */
+ * BASELINE config 5, fixed stride: chunks of chunk_blocks blocks.  Its
+ * copies run in order on one copy stream and its kernels on another, chunk
+ * by chunk through events, with n_streams (at least 2) device buffers in
+ * rotation (NOVA_STREAM_HOST_PIPE=0: the round-4 form, each of n_streams
+ * streams copying, checksumming and copying back its own chunks). */
 int nova_crc32c_stream_host(const void* host_base, uint64_t stride, uint32_t len,
                             size_t n_blocks, uint32_t* host_out, uint32_t flags,
                             size_t chunk_blocks, int n_streams);
