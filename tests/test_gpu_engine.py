@@ -460,3 +460,32 @@ def test_engine_mixed_request_sizes(torch_gpu, oracle, engine_on):
     assert not errors, errors[:4]
     assert c1["requests"] - c0["requests"] >= 6 * 6 * len(sizes), (c0, c1)
     assert c1["fallbacks"] == c0["fallbacks"] and c1["timeouts"] == c0["timeouts"], (c0, c1)
+
+
+def test_engine_empty_and_single_block_requests(torch_gpu, oracle, engine_on):
+    """Edge sizes through the engine: an empty table returns at once without a
+    request (the counter is left alone), a one-block table and a block of 0
+    bytes (its CRC covers the type byte only) verify and write exactly."""
+    torch = torch_gpu
+    img = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    e = torch.empty(0, dtype=torch.int64, device="cuda")
+    ok = torch.empty(0, dtype=torch.uint8, device="cuda")
+    nb = torch.full((1,), 5, dtype=torch.int32, device="cuda")
+    r0 = C.engine_counters()["requests"]
+    C.queue_verify_blocks(img, e, e.to(torch.int32), ok, nb)
+    C.queue_write_trailers(img, e, e.to(torch.int32))
+    assert C.engine_counters()["requests"] == r0 and int(nb.item()) == 5
+    C.fill_splitmix64(img, 99)
+    for lens in ([1000], [0], [0, 17, 0]):
+        offs_np = np.cumsum([0] + [ln + 5 for ln in lens[:-1]]).astype(np.int64)
+        offs = torch.from_numpy(offs_np).cuda()
+        ln_t = torch.tensor(lens, dtype=torch.int32, device="cuda")
+        C.queue_write_trailers(img, offs, ln_t)
+        host = img.cpu().numpy()
+        for o, ln in zip(offs_np, lens):
+            blk = host[int(o):int(o) + ln + 5].tobytes()
+            assert oracle.trailer(blk[:ln], 0, False) == blk[ln:], (lens, ln)
+        okv = torch.full((len(lens),), 9, dtype=torch.uint8, device="cuda")
+        nb.zero_()
+        C.queue_verify_blocks(img, offs, ln_t, okv, nb)
+        assert okv.cpu().numpy().tolist() == [1] * len(lens) and int(nb.item()) == 0, lens
