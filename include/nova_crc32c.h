@@ -191,6 +191,12 @@ int nova_sst_queue_set_slots(int slots);
 /* Coalescing queue (NOVA_SST_ENGINE=0): batches launched, requests served,
  * most tables in one batch (this device). */
 int nova_sst_queue_stats(uint64_t* batches, uint64_t* requests, uint64_t* max_tables_per_batch);
+/* Test hook for the coalescing queue (NOVA_SST_ENGINE=0 or
+ * nova_sst_engine_set_enabled(0)): hold = 1 keeps every queued request from
+ * leading a batch (callers queue up), 0 releases them (the front one leads and
+ * takes the compatible ones behind it), -1 changes nothing; *queued (may be
+ * NULL) gets the number of requests waiting in the queue. */
+int nova_sst_queue_hold(int hold, uint64_t* queued);
 
 /* The engine of this device: start it now (it also starts on the first
  * queued call), stop it (waits for requests in flight; the next call starts
@@ -214,8 +220,10 @@ int nova_sst_engine_set_idle_us(uint32_t us);
  * (this process's CPUs, capped by its cgroup quota, minus 2;
  * NOVA_SST_ENGINE_SPINNERS); 1 if the request ring is in device memory
  * (written by the host through the PCIe BAR; NOVA_SST_ENGINE_RING=host keeps
- * it in pinned host memory). */
-#define NOVA_ENGINE_COUNTERS 23
+ * it in pinned host memory); requests whose completion words the host wrote
+ * after the instance that took them ended without finishing them (a "lost"
+ * exit or a worker error; their ring slots would never free otherwise). */
+#define NOVA_ENGINE_COUNTERS 24
 int nova_sst_engine_counters(uint64_t* out, size_t n);
 /* Time slice of an engine instance in us, from the next instance (0: back to
  * NOVA_SST_ENGINE_SLICE_US, default 20000; 0xFFFFFFFF: none).  An instance
@@ -233,6 +241,12 @@ int nova_sst_engine_reset(void);
 /* Test hook, calling thread only: wait `us` after submitting a request before
  * waiting for it (a waiter descheduled past a whole ring turn). */
 void nova_sst_engine_set_wait_delay_us(uint32_t us);
+/* Test hook: the engine's give-up time in us, from the next instance (0: the
+ * default 20 s).  A dispatcher with a request unfinished this long after the
+ * last arrival exits "lost" and its workers stop: a way to make an instance end
+ * with a request it took unfinished (its submitter takes it back, DESIGN.md
+ * 3.5g). */
+int nova_sst_engine_set_give_up_us(uint32_t us);
 /* The calling thread's last engine request, out[0..n) (n <= 8): host ns
  * waiting for the engine's lock, ns holding it (ring writes, a relaunch), ns
  * waiting for the completion words; sleeps during that wait, relaunches

@@ -62,6 +62,7 @@ _SIG = {
     "nova_sst_queue_verify_blocks": (_i32, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "nova_sst_queue_stats": (_i32, [_vp, _vp, _vp]),
     "nova_sst_queue_set_slots": (_i32, [ctypes.c_int]),
+    "nova_sst_queue_hold": (_i32, [ctypes.c_int, _vp]),
     "nova_sst_engine_start": (_i32, []),
     "nova_sst_engine_stop": (_i32, []),
     "nova_sst_engine_stats": (_i32, [_vp, _vp, _vp, _vp]),
@@ -76,6 +77,7 @@ _SIG = {
     "nova_sst_engine_yield": (_i32, [_vp]),
     "nova_sst_engine_reset": (_i32, []),
     "nova_sst_engine_set_wait_delay_us": (None, [_u32]),
+    "nova_sst_engine_set_give_up_us": (_i32, [_u32]),
     "nova_crc32c_stream_host": (_i32, [_vp, _u64, _u32, _sz, _vp, _u32, _sz, _i32]),
     "nova_crc32c_batch_host": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _sz, _i32]),
     "nova_sstable_write_trailers_host": (_i32, [_vp, _vp, _vp, _sz, _u32, _sz, _i32]),
@@ -105,6 +107,7 @@ _DIAG_SIG = {
     "nova_diag_set_parity_variant": (None, [_i32]),
     "nova_diag_set_rounds_sort": (None, [_i32]),
     "nova_diag_set_log_window": (None, [_i32]),
+    "nova_diag_set_log_key": (None, [_i32]),
     "nova_diag_host_extend_loop": (_u32, [_vp, _sz, ctypes.c_uint64]),
     "nova_diag_lane_xor_probe": (_i32, [_vp, _vp, _vp, _vp]),
     "nova_diag_copy_ceiling": (_i32, [_vp, _vp, _sz, _vp, _vp, _i32, _i32, _vp]),
@@ -206,6 +209,7 @@ def diagnostics():
         D.nova_diag_set_variable_kernel(0)
         D.nova_diag_set_rounds_sort(2)
         D.nova_diag_set_log_window(0)
+        D.nova_diag_set_log_key(0)
         D.nova_diag_set_trailer_single_pass(0)
         D.nova_diag_set_parity_variant(0)
         D.nova_diag_set_burst_lanes(0)
@@ -427,6 +431,14 @@ def queue_set_slots(slots: int) -> None:
     _check(_L().nova_sst_queue_set_slots(int(slots)), "nova_sst_queue_set_slots")
 
 
+def queue_hold(hold: int) -> int:
+    """Test hook: 1 holds the coalescing queue (no queued request leads a
+    batch), 0 releases it, -1 only reads; returns the requests waiting."""
+    v = ctypes.c_uint64(0)
+    _check(_L().nova_sst_queue_hold(int(hold), ctypes.byref(v)), "nova_sst_queue_hold")
+    return int(v.value)
+
+
 def queue_stats() -> dict:
     v = [ctypes.c_uint64(0) for _ in range(3)]
     _check(_L().nova_sst_queue_stats(*[ctypes.byref(x) for x in v]), "nova_sst_queue_stats")
@@ -457,7 +469,7 @@ ENGINE_COUNTERS = ("requests", "launches", "fallbacks", "running", "exits_idle",
                    "exits_stop", "exits_lost", "timeouts", "errors", "taken_back", "unsafe",
                    "yield_waits", "yield_bumps", "broken", "backing_off", "exits_slice", "launch_us_max",
                    "launch_slow", "poll_gap_us_max", "sleep_waits", "max_spinners",
-                   "ring_device")
+                   "ring_device", "host_marked_done")
 
 
 def engine_counters() -> dict:
@@ -493,6 +505,13 @@ def engine_reset() -> None:
 def engine_set_wait_delay_us(us: int) -> None:
     """Test hook (calling thread): start waiting for a submitted request `us` late."""
     _L().nova_sst_engine_set_wait_delay_us(int(us))
+
+
+def engine_set_give_up_us(us: int) -> None:
+    """Test hook: the engine's give-up time in us from the next instance (0:
+    the default 20 s); a dispatcher with a request unfinished that long after
+    the last arrival exits "lost"."""
+    _check(_L().nova_sst_engine_set_give_up_us(int(us)), "nova_sst_engine_set_give_up_us")
 
 
 def engine_set_enabled(on: int) -> None:

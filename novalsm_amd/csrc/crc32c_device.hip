@@ -166,10 +166,15 @@ __global__ void __launch_bounds__(256) split_finish_kernel(CrcParams p, int mode
 // counting sort in LDS (order within a line count is arbitrary).
 constexpr uint32_t kLogSortWin = 1024;  // records per window (at most; g_tune_logwin)
 constexpr uint32_t kLogSortBins = 288;  // line counts (a 32 KiB log block is 256 lines of 128 B)
+// keymode (diagnostics A/B, nova_diag_set_log_key; product 0): 0 counting
+// sort by line count, order within a count arbitrary; 1 the same, stable
+// (file order within a count); 2 / 3 stable on the line count / 2 or / 4.
 __global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint64_t* __restrict__ offs,
                                                        uint64_t n, uint64_t buf_len, uint32_t line,
-                                                       uint32_t win, uint32_t* __restrict__ perm) {
+                                                       uint32_t win, uint32_t* __restrict__ perm,
+                                                       uint32_t keymode) {
   __shared__ uint32_t cnt[kLogSortBins];
+  __shared__ uint16_t kk[kLogSortWin];  // keymode > 0: every record's key, for the stable ranks
   const uint64_t w0 = (uint64_t)blockIdx.x * win;
   for (uint32_t b = threadIdx.x; b < kLogSortBins; b += blockDim.x) cnt[b] = 0;
   __syncthreads();
@@ -190,7 +195,9 @@ __global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint
       const uint64_t Le = (E + line - 1) & ~(uint64_t)(line - 1);
       const uint64_t S = Le > first ? (Le - first) / line : 1;  // lines (the rounds kernel's cost)
       key[k] = S < kLogSortBins ? (uint32_t)S : kLogSortBins - 1;
+      if (keymode >= 2) key[k] >>= keymode - 1;
       atomicAdd(&cnt[key[k]], 1u);
+      if (keymode) kk[threadIdx.x + 256u * k] = (uint16_t)key[k];
     }
   }
   __syncthreads();
@@ -203,6 +210,19 @@ __global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint
     }
   }
   __syncthreads();
+  if (keymode) {  // stable: rank = the bin's start + earlier records of the same key
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint32_t j = threadIdx.x + 256u * k;
+      const uint64_t i = w0 + j;
+      if (j < win && i < n) {
+        uint32_t r = cnt[key[k]];
+        for (uint32_t x = 0; x < j; x++) r += kk[x] == key[k] ? 1u : 0u;
+        perm[w0 + r] = (uint32_t)i;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const uint64_t i = w0 + threadIdx.x + 256u * k;
@@ -367,6 +387,7 @@ thread_local std::atomic<int> g_tune_parity{0};
 thread_local std::atomic<int> g_tune_kernel{0};
 thread_local std::atomic<int> g_tune_sort{2};
 thread_local std::atomic<int> g_tune_logwin{0};
+thread_local std::atomic<int> g_tune_logkey{0};  // log_sort_kernel keymode (diagnostics)
 thread_local std::atomic<int> g_tune_trailer_1pass{0};
 thread_local std::atomic<int> g_tune_burst{0};
 thread_local std::atomic<int> g_tune_split{0};
@@ -605,7 +626,9 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, b
   if (ts) pl.seg = ts & ~15u;
   if (pl.kernel == kFlatK || pl.kernel == kRoundsK) {
     pl.seg = 0;
-    if (pl.G == 1) pl.G = 2;  // at most 32 groups per wave (chunk >= 2 groups <= 64)
+    // at most 32 groups per wave (chunk >= 2 groups <= 64); one lane per log
+    // record is a diagnostics A/B (rounds_diag)
+    if (pl.G == 1 && !(g_diag && log && pl.kernel == kRoundsK)) pl.G = 2;
   }
   if (pl.kernel == kRoundsK && log && tk == kAuto && tg == 0 && bytes_per_block &&
       bytes_per_block < (mode == kLogVerify ? kLogNarrowVerify : kLogNarrowWrite)) {
@@ -941,7 +964,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // cost ~7 points even in file order and more out of it; the
   // sort is a diagnostics option there.
   const bool lsort_mode = mode == kLogVerify || (mode == kLogWrite && g_diag && g_tune_logwin.load() < 0);
-  if (pl.kernel == kRoundsK && lsort_mode && G == 8 &&
+  if (pl.kernel == kRoundsK && lsort_mode && (G == 8 || (G == 1 && g_diag)) &&
       p.n_blocks >= kLogSortMin && p.n_blocks < (1ull << 32) && lsort >= 2 &&
       !log_sc.alloc(p.n_blocks * (mode == kLogWrite ? 9 : 5), stream)) {
     const uint64_t n = p.n_blocks;
@@ -952,8 +975,9 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     uint32_t* crc_pos = perm + n;  // log write only
     uint8_t* st_pos = reinterpret_cast<uint8_t*>(mode == kLogWrite ? crc_pos + n : perm + n);
     const uint64_t wgs = (n + win - 1) / win;
+    const int km = g_diag ? g_tune_logkey.load() : 0;
     hipLaunchKernelGGL(log_sort_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, p.offsets, n,
-                       (uint64_t)p.buf_len, 16u * (uint32_t)G, win, perm);
+                       (uint64_t)p.buf_len, 16u * (uint32_t)G, win, perm, (uint32_t)(km >= 0 && km <= 3 ? km : 0));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     CrcParams q = p;

@@ -1419,6 +1419,11 @@ int hook_init_device(DevTables* t) {
   if ((e = set_lds_attr_rounds<8, kLogWrite, kVarDiag | kVarOutPos>())) return e;
   if ((e = set_lds_attr_rounds<8, kLogVerify, kVarDiag | kVarOutPos>())) return e;
   if ((e = set_lds_attr_rounds<8, kLogVerify, kVarDiag | kVarNoTail | kVarOutPos>())) return e;
+  // one lane per log record (round 6 A/B; file order, and the sorted windows)
+  if ((e = set_lds_attr_rounds<1, kLogWrite, kVarDiag | kVarCached>())) return e;
+  if ((e = set_lds_attr_rounds<1, kLogVerify, kVarDiag | kVarCached>())) return e;
+  if ((e = set_lds_attr_rounds<1, kLogWrite, kVarDiag | kVarCached | kVarOutPos>())) return e;
+  if ((e = set_lds_attr_rounds<1, kLogVerify, kVarDiag | kVarCached | kVarOutPos>())) return e;
   if ((e = set_lds_attrs_mode<kStore, kVarNoLookup>())) return e;
   if ((e = set_lds_attrs_mode<kStore, kVarNarrow>())) return e;
   if ((e = set_lds_attrs_mode<kStore, kVarCached>())) return e;
@@ -1472,6 +1477,15 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
   if constexpr (MODE == kStore) {
     if (var == kVarNoLookup) return launch_rounds_v<kStore, kVarNoLookup>(G, p, t, s, chunk);
     if (var == kVarNarrow) return launch_rounds_v<kStore, kVarNarrow>(G, p, t, s, chunk);
+  }
+  if constexpr (MODE == kLogWrite || MODE == kLogVerify) {
+    // one lane per record (round 6 A/B, nova_crc32c_set_tuning(1, 0)): 64
+    // records per round on 16-B lines, default-policy loads; large logs take
+    // the sorted windows (run(), results by position) like G = 8
+    if (G == 1) {
+      if (p.out_pos) return launch_rounds_v<MODE, kVarDiag | kVarCached | kVarOutPos>(1, p, t, s, chunk);
+      return launch_rounds_v<MODE, kVarDiag | kVarCached>(1, p, t, s, chunk);
+    }
   }
   const bool round_epi = var == kVarRoundEpi;  // A/B: the per-round epilogue (rounds 1-2 form)
   if constexpr (MODE == kLogWrite || MODE == kLogVerify || MODE == kVerify) {
@@ -1655,6 +1669,8 @@ void nova_diag_set_parity_variant(int variant) { g_tune_parity.store(variant); }
 void nova_diag_set_rounds_sort(int on) { g_tune_sort.store(on); }
 
 void nova_diag_set_log_window(int records) { g_tune_logwin.store(records); }
+// log_sort_kernel's key (0 the product's; 1 stable; 2 / 3 stable on lines / 2, / 4)
+void nova_diag_set_log_key(int mode) { g_tune_logkey.store(mode); }
 
 // Holds every CU for `us` microseconds: one workgroup per CU with the whole
 // 160 KiB of LDS, spinning on the real-time counter -- a kernel of another

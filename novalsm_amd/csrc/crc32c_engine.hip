@@ -1082,6 +1082,11 @@ struct Engine {
   uint64_t launch_ns_max = 0, launch_slow = 0;  // host time in launch_locked: the largest (not the first), launches over 1 ms
   uint64_t gap_ticks_max = 0;                   // the dispatchers' longest gap between two polls
   uint32_t idle_us = 0, waves = 0;
+  uint32_t give_up_us = 0;                    // 0: 20 s (nova_sst_engine_set_give_up_us, a test hook)
+  // Take-backs waiting (with mu released) for an instance to end: no instance
+  // is launched meanwhile, so the stream's last work stays the one waited for.
+  int tb_active = 0;
+  uint64_t host_done = 0;                     // requests whose completion words the host wrote (take_back_locked)
   std::atomic<uint32_t> timeout_ms{0};        // 0: NOVA_SST_ENGINE_TIMEOUT_MS (default 10000)
   // Waiting (round 5): at most max_spinners waiters spin; the others poll in
   // short sleeps.  16 waiters spinning on a 16-CPU cgroup quota exhausted it
@@ -1291,7 +1296,8 @@ struct Engine {
     p.gen = gen + 1;
     p.yield_gen = wait_for_yielded_locked();
     p.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
-    p.give_up_ticks = 20ull * 100000000ull;  // 20 s (every spin of the engine is bounded)
+    // 20 s (every spin of the engine is bounded); shorter only through the test hook
+    p.give_up_ticks = give_up_us ? (uint64_t)give_up_us * 100 : 20ull * 100000000ull;
     p.slice_ticks = (uint64_t)slice_us * 100;
     p.htrace = trace ? htrace : nullptr;
     static const uint32_t page_poll = (uint32_t)env_u64("NOVA_SST_ENGINE_PAGE_POLL", 1);
@@ -1332,6 +1338,9 @@ struct Engine {
   int relaunch_if_exited_locked() {
     volatile EngCtl* c = ctl;
     if (running && !c->exited) return 0;
+    // a take-back is waiting for the instance to end (mu released): the
+    // waiters' polls relaunch once it is through
+    if (tb_active) return 0;
     uint64_t first = inst_first;
     if (running) {
       first = c->consumed;
@@ -1361,10 +1370,41 @@ struct Engine {
     return t ? t : env;
   }
 
+  // Request seq's completion words, written by the host for a request that an
+  // ended instance took and left unfinished (a "lost" exit, a worker error):
+  // no later instance revisits it (they start at `consumed`, past it), so
+  // without them its ring slot would never free and every request reaching
+  // that slot would wait kRingWaitMs and fall back.  The words
+  // only grow; an ended instance writes no more of them.
+  void host_mark_done(uint64_t seq) {
+    volatile uint64_t* h = hdone + (seq % kRing) * kCntGroups;
+    for (uint32_t g = 0; g < kCntGroups; g++)
+      if (h[g] < seq + 1) h[g] = seq + 1;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    host_done++;
+  }
+
+  // The instance whose end a take-back waited for has ended (its stream is
+  // idle) with request seq not done.  It took the request (consumed > seq):
+  // mark it done from the host.  It did not record its exit (an aborted
+  // kernel): the engine is not used again.
+  void after_instance_end(uint64_t seq) {
+    volatile EngCtl* c = ctl;
+    if (done(seq)) return;
+    if (c->exited) {
+      if (c->consumed > seq) host_mark_done(seq);  // (<= seq: a later instance skips it)
+    } else {
+      broken = true;
+    }
+  }
+
   // Take request seq back (its submitter failed to get a result): returns 0
   // once the engine can no longer touch it (the plain call may run), or
-  // kEngineUnsafe.  Under mu: no instance is launched meanwhile.
-  int take_back_locked(uint64_t seq) {
+  // kEngineUnsafe.  Called with lk (on mu) held; while it waits for the
+  // instance to end it releases lk in 50-us steps (other
+  // submitters and waiters are not held off for up to 30 s), and tb_active
+  // keeps any instance from being launched meanwhile.
+  int take_back_locked(uint64_t seq, std::unique_lock<SpinMutex>& lk) {
     volatile EngCtl* c = ctl;
     taken_back++;
     volatile EngIn* vi = in;
@@ -1387,18 +1427,28 @@ struct Engine {
     std::atomic_thread_fence(std::memory_order_seq_cst);
     const auto t0 = Clock::now();
     const auto limit = std::chrono::milliseconds(std::max<uint32_t>(timeout(), 30000));
+    tb_active++;
+    int rc = 0;
     for (;;) {
-      if (done(seq)) return 0;
+      if (done(seq)) break;
       const hipError_t q = hipStreamQuery(stream);
-      if (q == hipSuccess) return 0;  // the instance (the stream's last work) has ended
+      if (q == hipSuccess) {  // the instance (the stream's last work) has ended
+        after_instance_end(seq);
+        break;
+      }
       (void)hipGetLastError();
       if (Clock::now() - t0 > limit) {
         unsafe++;
         broken = true;  // an engine that neither finishes nor ends: not used again
-        return kEngineUnsafe;
+        rc = kEngineUnsafe;
+        break;
       }
+      lk.unlock();
       std::this_thread::sleep_for(std::chrono::microseconds(50));
+      lk.lock();
     }
+    tb_active--;
+    return rc;
   }
 
   // After a failed request: back off (100 ms, doubling to 12.8 s; reset by a success).
@@ -1645,8 +1695,8 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
   if (failed) {
     int rc = 0;
     {
-      std::lock_guard<SpinMutex> lk(g.mu);
-      rc = g.take_back_locked(seq);
+      std::unique_lock<SpinMutex> lk(g.mu);
+      rc = g.take_back_locked(seq, lk);
     }
     g.back_off();
     g.inflight.fetch_sub(1);
@@ -1750,7 +1800,7 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
       gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
       (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice], gp->launch_ns_max / 1000,
       gp->launch_slow, gp->gap_ticks_max / 100, gp->sleep_waits, (uint64_t)gp->max_spinners,
-      (uint64_t)gp->in_dev};
+      (uint64_t)gp->in_dev, gp->host_done};
   for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
   return 0;
 }
@@ -1839,6 +1889,15 @@ int nova_sst_engine_set_timeout_ms(uint32_t ms) {
 }
 
 void nova_sst_engine_set_wait_delay_us(uint32_t us) { tl_wait_delay_us = us; }
+
+int nova_sst_engine_set_give_up_us(uint32_t us) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<SpinMutex> lk(gp->mu);
+  gp->give_up_us = us;  // from the next instance
+  return 0;
+}
 
 int nova_sst_engine_last_call(uint64_t* out, size_t n) {
   if (!out) return NOVA_E_INVAL;

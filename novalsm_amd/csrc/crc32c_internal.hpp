@@ -191,6 +191,7 @@ extern thread_local std::atomic<int> g_tune_kernel;      // VarKernel (0 = auto)
 extern thread_local std::atomic<int> g_tune_sort;
 // log sort window in records (0 = 512); negative: -window, and log write sorts too
 extern thread_local std::atomic<int> g_tune_logwin;
+extern thread_local std::atomic<int> g_tune_logkey;
 extern thread_local std::atomic<int> g_tune_trailer_1pass;  // trailer / log-write store forms
 extern thread_local std::atomic<int> g_tune_burst;       // 0 auto, 16/64/65 force, -1 off
 extern thread_local std::atomic<int> g_tune_split;       // 0 auto, 1 force, -1 off

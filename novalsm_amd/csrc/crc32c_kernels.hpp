@@ -2674,12 +2674,25 @@ int launch_stream_v(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
 // ---- rounds kernel (whole variable-length blocks in lockstep rounds) ----------
 template <int MODE, int VAR>
 int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
-  if constexpr ((VAR & kVarOutPos) != 0) {  // large logs only: G = 8
+  if constexpr ((VAR & kVarOutPos) != 0) {  // large logs only: G = 8 (diagnostics: also 1)
+    if constexpr ((VAR & kVarDiag) != 0 && (VAR & kVarCached) != 0) {
+      if (G == 1) {
+        hipLaunchKernelGGL((crc32c_rounds_kernel<1, MODE, VAR>), grid, block, lds, stream, p);
+        return (int)hipGetLastError();
+      }
+    }
     if (G != 8) return NOVA_E_INVAL;
     hipLaunchKernelGGL((crc32c_rounds_kernel<8, MODE, VAR>), grid, block, lds, stream, p);
     return (int)hipGetLastError();
   } else if constexpr ((VAR & kVarCached) != 0 && (MODE == kLogWrite || MODE == kLogVerify)) {
-    // default-policy log records run at 2 or 4 lanes only (launch_rounds)
+    // default-policy log records run at 2 or 4 lanes only (launch_rounds);
+    // one lane per record is a diagnostics A/B (round 6)
+    if constexpr ((VAR & kVarDiag) != 0) {
+      if (G == 1) {
+        hipLaunchKernelGGL((crc32c_rounds_kernel<1, MODE, VAR>), grid, block, lds, stream, p);
+        return (int)hipGetLastError();
+      }
+    }
     if (G == 2) hipLaunchKernelGGL((crc32c_rounds_kernel<2, MODE, VAR>), grid, block, lds, stream, p);
     else if (G == 4) hipLaunchKernelGGL((crc32c_rounds_kernel<4, MODE, VAR>), grid, block, lds, stream, p);
     else return NOVA_E_INVAL;
@@ -2725,7 +2738,9 @@ inline void rounds_params(int G, CrcParams& p, DevTables* t) {
 // p.perm: the caller's order of blocks (null in the product).
 template <int MODE, int VAR>
 int launch_rounds_v(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_t chunk = 0) {
-  if (G < 2) G = 2;
+  // one lane per block: diagnostics-only log instantiations (launch_rounds_g)
+  constexpr bool kG1 = (VAR & kVarDiag) != 0 && (VAR & kVarCached) != 0 && (MODE == kLogWrite || MODE == kLogVerify);
+  if (G < 2 && !kG1) G = 2;
   rounds_params(G, p, t);
   {
     const int so = g_tune_sort.load();

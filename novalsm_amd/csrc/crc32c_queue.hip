@@ -221,6 +221,9 @@ struct Queue {
     return n;
   }
   int set_slots = 0;  // under mu
+  // Test hook (nova_sst_queue_hold): while held no request leads, so callers
+  // queue up deterministically; releasing wakes the front one.
+  bool held = false;  // under mu
   int slots() const { return set_slots ? set_slots : env_slots(); }
   int free_slot(int ns) const {
     for (int k = 0; k < ns; k++)
@@ -239,7 +242,7 @@ struct Queue {
       if (r.done) return r.rc;
       // (a popped request waits for done; front() of an empty deque is undefined;
       // the slot count is read on every wake: nova_sst_queue_set_slots may raise it)
-      if (!q.empty() && q.front() == &r && (si = free_slot(slots())) >= 0) break;
+      if (!held && !q.empty() && q.front() == &r && (si = free_slot(slots())) >= 0) break;
       r.cv.wait(lk);
     }
     // leader: take the compatible requests at the queue's front (r first)
@@ -365,6 +368,22 @@ int nova_sst_queue_set_slots(int slots) {
   std::lock_guard<std::mutex> lk(q.mu);
   q.set_slots = slots;
   q.wake_front();  // more slots: the front request may lead now
+  return 0;
+}
+
+int nova_sst_queue_hold(int hold, uint64_t* queued) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) {
+    (void)hipGetLastError();
+    return NOVA_E_NODEV;
+  }
+  Queue& q = g_q[dev];
+  std::lock_guard<std::mutex> lk(q.mu);
+  if (hold >= 0) {
+    q.held = hold != 0;
+    if (!q.held) q.wake_front();
+  }
+  if (queued) *queued = (uint64_t)q.q.size();
   return 0;
 }
 

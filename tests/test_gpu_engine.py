@@ -276,6 +276,50 @@ def test_engine_take_back_when_held_off(torch_gpu, oracle, engine_on):
     C.engine_stop()
 
 
+def test_engine_lost_request_frees_its_slot(torch_gpu, oracle, engine_on):
+    """an instance that took a request and ended without
+    finishing it (here a "lost" exit: the give-up time cut to 30 us by a test
+    hook, so the dispatcher gives up on a 128K-block table still running) left
+    that request's completion words unwritten; no later instance revisits it,
+    so its ring slot never freed and the request reaching that slot a ring
+    turn later waited 1 s and fell back.  Now the take-back writes them once
+    the instance has ended (host_marked_done): the failed call's results are
+    exact (plain call), and more than a ring turn of engine calls after it
+    all run on the engine -- no fallback, no 1-s stall."""
+    torch = torch_gpu
+    C.engine_stop()
+    big = _sst_table(torch, oracle, 131072, 81, victims=(3, 120000))
+    small = _sst_table(torch, oracle, 1, 82)
+    ok = torch.empty(big["n"], dtype=torch.uint8, device="cuda")
+    nb = torch.zeros(1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    c0 = C.engine_counters()
+    try:
+        C.engine_set_give_up_us(30)
+        C.engine_set_idle_us(10)
+        C.queue_verify_blocks(big["img"], big["offs"], big["lens"], ok, nb)
+    finally:
+        C.engine_set_give_up_us(0)
+        C.engine_set_idle_us(0)
+    assert np.array_equal(ok.cpu().numpy(), big["want"]) and int(nb.item()) == 2
+    c1 = C.engine_counters()
+    assert c1["exits_lost"] - c0["exits_lost"] >= 1 or c1["errors"] - c0["errors"] >= 1, (c0, c1)
+    assert c1["fallbacks"] - c0["fallbacks"] == 1 and c1["taken_back"] - c0["taken_back"] == 1, (c0, c1)
+    assert c1["host_marked_done"] - c0["host_marked_done"] == 1 and not c1["broken"], (c0, c1)
+    C.engine_reset()  # end the backoff
+    ok1 = torch.empty(1, dtype=torch.uint8, device="cuda")
+    worst = 0.0
+    for _ in range(RING + 64):
+        t0 = time.perf_counter()
+        C.queue_verify_blocks(small["img"], small["offs"], small["lens"], ok1)
+        worst = max(worst, time.perf_counter() - t0)
+    assert int(ok1.cpu()[0]) == 1
+    c2 = C.engine_counters()
+    assert c2["fallbacks"] == c1["fallbacks"] and c2["requests"] - c1["requests"] == RING + 64, (c1, c2)
+    assert worst < 0.5, worst  # no ring-full wait (kRingWaitMs = 1 s)
+    C.engine_stop()
+
+
 def test_engine_stop_under_traffic(torch_gpu, oracle, engine_on):
     """nova_sst_engine_stop while four threads keep calling: the stop takes
     effect (the dispatcher stops taking requests even though new ones keep

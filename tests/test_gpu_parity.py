@@ -1340,6 +1340,7 @@ def test_queue_batched_trailers_adjacent_tables(torch_gpu, oracle, size):
     rewritten whole."""
     torch = torch_gpu
     import threading
+    import time
     from bench import sst4k_layout
     ns = [5000, 4500, 5100, 4900] if size == "one_pass" else [70000, 66000, 68000, 65000]
     lays = [sst4k_layout(n, 60 + k) for k, n in enumerate(ns)]
@@ -1360,61 +1361,40 @@ def test_queue_batched_trailers_adjacent_tables(torch_gpu, oracle, size):
                       torch.from_numpy(o.view(np.int64)).cuda(), torch.from_numpy(ln.view(np.int32)).cuda()))
     errors = []
 
-    def work(k, gate):
+    def work(k):
         try:
             v, o, ln = views[k]
             s = torch.cuda.Stream()
             with torch.cuda.stream(s):
-                gate.wait()
                 C.queue_write_trailers(v, o, ln, stream=s)
             s.synchronize()
         except Exception as e:  # pragma: no cover
             errors.append(e)
 
-    # a long call holds the queue's one batch slot while the four callers
-    # enqueue behind it; the next leader then takes all four in one batch
-    nb_blk = 1 << 19
-    b_offs, b_lens, b_total = sst4k_layout(nb_blk, 7)
-    bimg = torch.empty(b_total + 64, dtype=torch.uint8, device="cuda")
-    C.fill_splitmix64(bimg, 77)
-    b_o = torch.from_numpy(b_offs.view(np.int64)).cuda()
-    b_l = torch.from_numpy(b_lens.view(np.int32)).cuda()
-    b_ok = torch.empty(nb_blk, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-
-    def blocker(gate):
-        try:
-            s = torch.cuda.Stream()
-            with torch.cuda.stream(s):
-                gate.wait()
-                # ~6 ms of queue calls: the callers' threads wake from the barrier
-                # late on a busy host (a millisecond and more on the GPU boxes)
-                for _ in range(16):
-                    C.queue_verify_blocks(bimg, b_o, b_l, b_ok, stream=s)
-        except Exception as e:  # pragma: no cover
-            errors.append(e)
-
+    # the queue is held (test hook) until all four callers
+    # are enqueued, then released: the front one leads and takes all four in
+    # ONE batch -- deterministic, no timing window, no retries.
     try:
-        for attempt in range(6):  # until the four calls shared a batch (timing)
-            buf.copy_(torch.from_numpy(before))
-            torch.cuda.synchronize()
-            qb = C.queue_stats()
-            gate = threading.Barrier(len(ns) + 1)
-            th = [threading.Thread(target=blocker, args=(gate,))]
-            th += [threading.Thread(target=work, args=(k, gate)) for k in range(len(ns))]
-            for x in th:
-                x.start()
-            for x in th:
-                x.join()
-            qa = C.queue_stats()
-            assert qa["requests"] - qb["requests"] == len(ns) + 16
-            if qa["batches"] - qb["batches"] < len(ns) + 16:
-                break
+        qb = C.queue_stats()
+        assert C.queue_hold(1) == 0
+        th = [threading.Thread(target=work, args=(k,)) for k in range(len(ns))]
+        for x in th:
+            x.start()
+        deadline = time.perf_counter() + 30.0
+        while C.queue_hold(-1) < len(ns) and time.perf_counter() < deadline and not errors:
+            time.sleep(0.001)
+        queued = C.queue_hold(0)
+        for x in th:
+            x.join()
+        qa = C.queue_stats()
     finally:
+        C.queue_hold(0)
         C.queue_set_slots(0)
         C.engine_set_enabled(-1)
+    assert queued == len(ns), queued
+    assert qa["requests"] - qb["requests"] == len(ns), (qb, qa)
     assert not errors, errors
-    assert qa["batches"] - qb["batches"] < len(ns) + 16, "the calls never shared a batch"
+    assert qa["batches"] - qb["batches"] == 1, (qb, qa)  # one batch of all four tables
     after = buf.cpu().numpy()
     expect = before.copy()
     for k, (o, ln, total) in enumerate(lays):

@@ -99,16 +99,20 @@ def main() -> int:
     rows = []
 
     def sort_sweep(op, fn, alg_bytes):
-        # entries "sort" or "sort:window" (nova_diag_set_rounds_sort / _log_window)
+        # entries "sort", "sort:window" or "sort:window:key" (nova_diag_set_rounds_sort /
+        # _log_window / _log_key)
         for v in [x for x in args.sort_sweep.split(",") if x]:
-            so, _, win = v.partition(":")
+            so, win, key = (v.split(":") + ["0", "0"])[:3]
             with C.diagnostics() as D:
                 D.nova_diag_set_rounds_sort(int(so))
                 D.nova_diag_set_log_window(int(win or 0))
+                D.nova_diag_set_log_key(int(key or 0))
                 sec = timed(torch, fn, args.steps, args.warmup, stream)
                 D.nova_diag_set_rounds_sort(2)
                 D.nova_diag_set_log_window(0)
+                D.nova_diag_set_log_key(0)
             print(json.dumps({"sweep": op, "rounds_sort": int(so), "log_window": int(win or 0),
+                              "log_key": int(key or 0),
                               "GBps": round(alg_bytes / sec / 1e9, 1),
                               "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}), flush=True)
 
