@@ -626,9 +626,7 @@ Plan plan(uint64_t n_blocks, uint64_t bytes_per_block, bool uniform, int mode, b
   if (ts) pl.seg = ts & ~15u;
   if (pl.kernel == kFlatK || pl.kernel == kRoundsK) {
     pl.seg = 0;
-    // at most 32 groups per wave (chunk >= 2 groups <= 64); one lane per log
-    // record is a diagnostics A/B (rounds_diag)
-    if (pl.G == 1 && !(g_diag && log && pl.kernel == kRoundsK)) pl.G = 2;
+    if (pl.G == 1) pl.G = 2;  // at most 32 groups per wave (chunk >= 2 groups <= 64)
   }
   if (pl.kernel == kRoundsK && log && tk == kAuto && tg == 0 && bytes_per_block &&
       bytes_per_block < (mode == kLogVerify ? kLogNarrowVerify : kLogNarrowWrite)) {
@@ -964,7 +962,10 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
   // cost ~7 points even in file order and more out of it; the
   // sort is a diagnostics option there.
   const bool lsort_mode = mode == kLogVerify || (mode == kLogWrite && g_diag && g_tune_logwin.load() < 0);
-  if (pl.kernel == kRoundsK && lsort_mode && (G == 8 || (G == 1 && g_diag)) &&
+  // (diagnostics A/B, round 6: short records at 2-4 lanes in sorted windows
+  // when a window is set, nova_diag_set_log_window)
+  const bool lsort_g = G == 8 || (g_diag && G <= 4 && g_tune_logwin.load() != 0);
+  if (pl.kernel == kRoundsK && lsort_mode && lsort_g &&
       p.n_blocks >= kLogSortMin && p.n_blocks < (1ull << 32) && lsort >= 2 &&
       !log_sc.alloc(p.n_blocks * (mode == kLogWrite ? 9 : 5), stream)) {
     const uint64_t n = p.n_blocks;

@@ -1091,8 +1091,12 @@ constexpr int kNotTaken = -999;               // a hook found nothing to do
 // stores; 4 = the same non-temporal; 5 = whole-piece form without result
 // writes; 6 = no result writes; 7 = no per-block epilogue and no writes
 // (timing ablations: 5, 6 and 7 write nothing) -> CrcParams::wvar.
+// 8 / 9 / 10 = log records: the decode stage reads no tail line / no header
+// (lengths from the next offset) / neither (timing ablations: WRONG results,
+// written as usual, so the traffic is the product's minus those loads);
+// 11 = sorted windows in the XCD-contiguous chunk order (results right).
 uint32_t wvar_of(int tkn) {
-  return tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : tkn == 7 ? 3u : 0u;
+  return tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : tkn == 7 ? 3u : (tkn >= 8 && tkn <= 11) ? (uint32_t)(tkn - 4) : 0u;
 }
 
 template <int G, int MODE, int VAR = 0>
@@ -1419,11 +1423,11 @@ int hook_init_device(DevTables* t) {
   if ((e = set_lds_attr_rounds<8, kLogWrite, kVarDiag | kVarOutPos>())) return e;
   if ((e = set_lds_attr_rounds<8, kLogVerify, kVarDiag | kVarOutPos>())) return e;
   if ((e = set_lds_attr_rounds<8, kLogVerify, kVarDiag | kVarNoTail | kVarOutPos>())) return e;
-  // one lane per log record (round 6 A/B; file order, and the sorted windows)
-  if ((e = set_lds_attr_rounds<1, kLogWrite, kVarDiag | kVarCached>())) return e;
-  if ((e = set_lds_attr_rounds<1, kLogVerify, kVarDiag | kVarCached>())) return e;
-  if ((e = set_lds_attr_rounds<1, kLogWrite, kVarDiag | kVarCached | kVarOutPos>())) return e;
-  if ((e = set_lds_attr_rounds<1, kLogVerify, kVarDiag | kVarCached | kVarOutPos>())) return e;
+  // short log records at 2-4 lanes in sorted windows (round 6 A/B)
+  if ((e = set_lds_attr_rounds<2, kLogWrite, kVarDiag | kVarCached | kVarOutPos>())) return e;
+  if ((e = set_lds_attr_rounds<2, kLogVerify, kVarDiag | kVarCached | kVarOutPos>())) return e;
+  if ((e = set_lds_attr_rounds<4, kLogWrite, kVarDiag | kVarCached | kVarOutPos>())) return e;
+  if ((e = set_lds_attr_rounds<4, kLogVerify, kVarDiag | kVarCached | kVarOutPos>())) return e;
   if ((e = set_lds_attrs_mode<kStore, kVarNoLookup>())) return e;
   if ((e = set_lds_attrs_mode<kStore, kVarNarrow>())) return e;
   if ((e = set_lds_attrs_mode<kStore, kVarCached>())) return e;
@@ -1479,13 +1483,9 @@ int rounds_diag(int G, CrcParams& p, DevTables* t, hipStream_t s, uint32_t chunk
     if (var == kVarNarrow) return launch_rounds_v<kStore, kVarNarrow>(G, p, t, s, chunk);
   }
   if constexpr (MODE == kLogWrite || MODE == kLogVerify) {
-    // one lane per record (round 6 A/B, nova_crc32c_set_tuning(1, 0)): 64
-    // records per round on 16-B lines, default-policy loads; large logs take
-    // the sorted windows (run(), results by position) like G = 8
-    if (G == 1) {
-      if (p.out_pos) return launch_rounds_v<MODE, kVarDiag | kVarCached | kVarOutPos>(1, p, t, s, chunk);
-      return launch_rounds_v<MODE, kVarDiag | kVarCached>(1, p, t, s, chunk);
-    }
+    // short records at 2-4 lanes in sorted windows (round 6 A/B; run() takes
+    // the windows when a window is set): default-policy loads, results by position
+    if (G <= 4 && p.out_pos) return launch_rounds_v<MODE, kVarDiag | kVarCached | kVarOutPos>(G, p, t, s, chunk);
   }
   const bool round_epi = var == kVarRoundEpi;  // A/B: the per-round epilogue (rounds 1-2 form)
   if constexpr (MODE == kLogWrite || MODE == kLogVerify || MODE == kVerify) {

@@ -84,7 +84,10 @@ struct CrcParams {
   const uint8_t* tr_last;
   uint32_t out_pos;  // host: launch the kVarOutPos instantiation (log records in p.perm's order)
   uint32_t wvar;  // diagnostics (timing, kVarDiag): 1 = whole-piece stores non-temporal,
-                  // 2 = no result writes, 3 = no per-block epilogue and no writes
+                  // 2 = no result writes, 3 = no per-block epilogue and no writes;
+                  // log records: 4 / 5 / 6 = the decode stage reads no tail line /
+                  // no header / neither (WRONG results, written); 7 = the
+                  // XCD-contiguous chunk order with a permutation too
 };
 
 // Kernel variants (diagnostics / tuning; 0 = production).

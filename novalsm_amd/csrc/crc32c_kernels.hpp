@@ -1458,7 +1458,8 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
   // Same-box A/B (profiles/r04_ab_xcd_chunk_order*.log): SSTable verify +0.5
   // points, trailers +0.4; log verify's sorted windows (p.perm) lost 5 points
   // with it and keep the interleaved order.
-  const uint32_t xper = (nwg % 8 == 0 && !p.perm) ? nwg / 8 : 0;
+  // (diagnostics A/B, wvar 7: the XCD-contiguous order for sorted windows too)
+  const uint32_t xper = (nwg % 8 == 0 && (!p.perm || (kDiag && p.wvar == 7))) ? nwg / 8 : 0;
   auto xslot = [&](uint32_t v) -> uint32_t { return xper ? (v % 8) * xper + v / 8 : v; };
   auto chunk_of = [&](uint32_t v, uint32_t idx) -> uint64_t {
     const uint64_t c = ((uint64_t)idx + nwaves) * nwg + xslot(v);
@@ -1517,6 +1518,9 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
   uint32_t e_n = 0, e_rec = 0, e_aux = 0, e_ok = 0, e_tr = 0;
   typedef __attribute__((address_space(1))) const uint32_t gcu32;
   auto tail_issue = [&](uint64_t u0, uint32_t n, bool ok) {
+    // (diagnostics timing ablation, wvar 4 / 6: the decode stage reads no
+    // tail line -- the tail bytes read as zeros, WRONG CRCs)
+    if (kDiag && (p.wvar == 4 || p.wvar == 6)) ok = false;
     const uint64_t u1 = u0 + n, E = u1 & ~15ull;
     // verify: the stored CRC starts at u1 (the line is needed even when nb = 0)
     t_tl = gload16<VAR | kVarCached>((ok && (kTail2 || (u1 & 15))) ? E : zl);
@@ -1596,13 +1600,24 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
       } else if constexpr (MODE == kLogWrite) {
         t_aux = p.init[t_rec & p.imask];  // whole-piece eligibility (log_window_kernel)
       }
+      if constexpr (kLog && kDiag) {  // (timing ablation wvar 5 / 6: gap to the next record)
+        if (p.wvar == 5 || p.wvar == 6) {
+          const uint64_t nx = (uint64_t)t_rec + 1 < p.n_blocks ? (uint64_t)t_rec + 1 : (uint64_t)t_rec;
+          const uint64_t gap = p.offsets[nx & p.omask] - o;
+          t_len = gap >= 8 && gap < 65536 + 7 ? (uint32_t)(gap - 7) : 1u;
+        }
+      }
       stage = 3;
     } else if (st == 3) {
       const uint64_t a = base + (((uint64_t)t_ohi << 32) | t_olo) + (uint64_t)t_rec * p.stride;
       if constexpr (kLog) {
         // a header past its log block / the image is not read (bounds, status)
         const uint64_t o = ((uint64_t)t_ohi << 32) | t_olo;
-        const uint8_t* h = log_header_fits(o, p.buf_len) ? (const uint8_t*)a : p.zline;
+        // (diagnostics timing ablation, wvar 5 / 6: no header loads; the
+        // length comes from the next record's offset, stage 2 -- WRONG statuses
+        // at block ends and for verify's stored CRCs)
+        const bool nohdr = kDiag && (p.wvar == 5 || p.wvar == 6);
+        const uint8_t* h = (log_header_fits(o, p.buf_len) && !nohdr) ? (const uint8_t*)a : p.zline;
         typedef __attribute__((address_space(1))) const uint32_t __attribute__((aligned(1))) gu32u;
         hw1 = *(gu32u*)(h + 3);
         if constexpr (MODE == kLogVerify) hw0 = *(gu32u*)h;
@@ -1635,7 +1650,11 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
     } else if (st == 4) {
       const uint64_t o = ((uint64_t)t_ohi << 32) | t_olo;
       n_u0 = base + o + 6;  // CRC input: type byte + payload
-      const uint32_t length = (hw1 >> 8) & 0xffffu;  // db/log_format.h:27-30
+      uint32_t length = (hw1 >> 8) & 0xffffu;  // db/log_format.h:27-30
+      if (kDiag && (p.wvar == 5 || p.wvar == 6)) {  // (timing ablation: no header loads)
+        length = t_len;
+        hw1 = (length << 8) | (1u << 24);  // a FULL record
+      }
       const uint32_t ls = log_header_fits(o, p.buf_len)
                               ? log_status(o, length, MODE == kLogVerify ? hw1 >> 24 : 1u, p.buf_len)
                               : log_nohdr_status(o, p.buf_len);
@@ -1952,7 +1971,7 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
     typedef __attribute__((address_space(1))) uint8_t gu8;
     typedef __attribute__((address_space(1))) uint32_t gu32;
     const bool ok = e_ok != 0;
-    const bool wr = ok && (!kDiag || p.wvar < 2);
+    const bool wr = ok && (!kDiag || p.wvar < 2 || p.wvar >= 4);
     const uint64_t u1 = e_u0 + e_n;
     const uint32_t nb = (uint32_t)(u1 & 15u);
     uint32_t R = shift_nb<kMainBytes>(lds, kByteTab, lapply(lds + kMainBytes, vbuf[lane]), nb) ^ e_tr;
@@ -2166,7 +2185,7 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
         // writes the CRC field of the records whose status is OK)
         typedef __attribute__((address_space(1))) uint32_t gu32;
         typedef __attribute__((address_space(1))) uint8_t gu8;
-        if (!kDiag || p.wvar < 2) {
+        if (!kDiag || p.wvar < 2 || p.wvar >= 4) {
           *(gu32*)(p.out + wb_pos) = wb_v;
           *(gu8*)(p.ok_out + wb_pos) = (uint8_t)wb_st;
         }
@@ -2184,7 +2203,7 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
         else if (!kDiag || p.wvar != 2)
           *(__attribute__((address_space(1))) u32x4*)wb_a = w;
       } else {
-        if (!kDiag || p.wvar < 2) write_result<MODE>(p, wb_a, wb_v);
+        if (!kDiag || p.wvar < 2 || p.wvar >= 4) write_result<MODE>(p, wb_a, wb_v);
       }
       wb_on = false;
     }
@@ -2674,10 +2693,11 @@ int launch_stream_v(int G, CrcParams& p, DevTables* t, hipStream_t stream) {
 // ---- rounds kernel (whole variable-length blocks in lockstep rounds) ----------
 template <int MODE, int VAR>
 int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const CrcParams& p) {
-  if constexpr ((VAR & kVarOutPos) != 0) {  // large logs only: G = 8 (diagnostics: also 1)
+  if constexpr ((VAR & kVarOutPos) != 0) {  // large logs only: G = 8 (diagnostics A/B: 2, 4)
     if constexpr ((VAR & kVarDiag) != 0 && (VAR & kVarCached) != 0) {
-      if (G == 1) {
-        hipLaunchKernelGGL((crc32c_rounds_kernel<1, MODE, VAR>), grid, block, lds, stream, p);
+      if (G == 2 || G == 4) {  // short records in sorted windows, default-policy loads
+        if (G == 2) hipLaunchKernelGGL((crc32c_rounds_kernel<2, MODE, VAR>), grid, block, lds, stream, p);
+        else hipLaunchKernelGGL((crc32c_rounds_kernel<4, MODE, VAR>), grid, block, lds, stream, p);
         return (int)hipGetLastError();
       }
     }
@@ -2685,14 +2705,7 @@ int launch_rounds_g(int G, dim3 grid, dim3 block, size_t lds, hipStream_t stream
     hipLaunchKernelGGL((crc32c_rounds_kernel<8, MODE, VAR>), grid, block, lds, stream, p);
     return (int)hipGetLastError();
   } else if constexpr ((VAR & kVarCached) != 0 && (MODE == kLogWrite || MODE == kLogVerify)) {
-    // default-policy log records run at 2 or 4 lanes only (launch_rounds);
-    // one lane per record is a diagnostics A/B (round 6)
-    if constexpr ((VAR & kVarDiag) != 0) {
-      if (G == 1) {
-        hipLaunchKernelGGL((crc32c_rounds_kernel<1, MODE, VAR>), grid, block, lds, stream, p);
-        return (int)hipGetLastError();
-      }
-    }
+    // default-policy log records run at 2 or 4 lanes only (launch_rounds)
     if (G == 2) hipLaunchKernelGGL((crc32c_rounds_kernel<2, MODE, VAR>), grid, block, lds, stream, p);
     else if (G == 4) hipLaunchKernelGGL((crc32c_rounds_kernel<4, MODE, VAR>), grid, block, lds, stream, p);
     else return NOVA_E_INVAL;
@@ -2738,9 +2751,7 @@ inline void rounds_params(int G, CrcParams& p, DevTables* t) {
 // p.perm: the caller's order of blocks (null in the product).
 template <int MODE, int VAR>
 int launch_rounds_v(int G, CrcParams& p, DevTables* t, hipStream_t stream, uint32_t chunk = 0) {
-  // one lane per block: diagnostics-only log instantiations (launch_rounds_g)
-  constexpr bool kG1 = (VAR & kVarDiag) != 0 && (VAR & kVarCached) != 0 && (MODE == kLogWrite || MODE == kLogVerify);
-  if (G < 2 && !kG1) G = 2;
+  if (G < 2) G = 2;
   rounds_params(G, p, t);
   {
     const int so = g_tune_sort.load();

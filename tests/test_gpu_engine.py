@@ -278,8 +278,9 @@ def test_engine_take_back_when_held_off(torch_gpu, oracle, engine_on):
 
 def test_engine_lost_request_frees_its_slot(torch_gpu, oracle, engine_on):
     """an instance that took a request and ended without
-    finishing it (here a "lost" exit: the give-up time cut to 30 us by a test
-    hook, so the dispatcher gives up on a 128K-block table still running) left
+    finishing it (here a "lost" exit: give-up and idle times cut to 1 us by
+    test hooks, so the dispatcher gives up on a 128K-block table ~1 us after
+    taking it, and its workers stop) left
     that request's completion words unwritten; no later instance revisits it,
     so its ring slot never freed and the request reaching that slot a ring
     turn later waited 1 s and fell back.  Now the take-back writes them once
@@ -295,8 +296,8 @@ def test_engine_lost_request_frees_its_slot(torch_gpu, oracle, engine_on):
     torch.cuda.synchronize()
     c0 = C.engine_counters()
     try:
-        C.engine_set_give_up_us(30)
-        C.engine_set_idle_us(10)
+        C.engine_set_give_up_us(1)
+        C.engine_set_idle_us(1)
         C.queue_verify_blocks(big["img"], big["offs"], big["lens"], ok, nb)
     finally:
         C.engine_set_give_up_us(0)

@@ -82,6 +82,9 @@ def main() -> int:
     ap.add_argument("--lanes", type=int, default=0, help="force lanes per block/record (nova_crc32c_set_tuning)")
     ap.add_argument("--var-ab", default="",
                     help="comma list of rounds-kernel variants to A/B against the product (8192 16 waves, 2 cached)")
+    ap.add_argument("--decode-ablations", action="store_true",
+                    help="log ops: time the decode stage without its tail-line / header loads "
+                         "(timing ablations, WRONG results; nova_diag_set_trailer_single_pass 8/9/10)")
     ap.add_argument("--log-bound", action="store_true",
                     help="log write: time its composite bound (no-store pass + isolated CRC-field stores)")
     args = ap.parse_args()
@@ -98,22 +101,46 @@ def main() -> int:
     ops = args.ops.split(",")
     rows = []
 
-    def sort_sweep(op, fn, alg_bytes):
-        # entries "sort", "sort:window" or "sort:window:key" (nova_diag_set_rounds_sort /
-        # _log_window / _log_key)
+    def sort_sweep(op, fn, alg_bytes, check=None, reset=None):
+        # entries "sort", "sort:window", "sort:window:key" or "sort:window:key:ablation"
+        # (nova_diag_set_rounds_sort / _log_window / _log_key / _trailer_single_pass)
         for v in [x for x in args.sort_sweep.split(",") if x]:
-            so, win, key = (v.split(":") + ["0", "0"])[:3]
+            so, win, key, abl = (v.split(":") + ["0", "0", "0"])[:4]
+            if reset is not None:
+                reset()
             with C.diagnostics() as D:
+                if args.lanes:  # (the diagnostics library keeps its own tuning)
+                    D.nova_crc32c_set_tuning(args.lanes, 0)
                 D.nova_diag_set_rounds_sort(int(so))
                 D.nova_diag_set_log_window(int(win or 0))
                 D.nova_diag_set_log_key(int(key or 0))
+                D.nova_diag_set_trailer_single_pass(int(abl or 0))
                 sec = timed(torch, fn, args.steps, args.warmup, stream)
                 D.nova_diag_set_rounds_sort(2)
                 D.nova_diag_set_log_window(0)
                 D.nova_diag_set_log_key(0)
+                D.nova_diag_set_trailer_single_pass(0)
+            extra = {} if check is None else {"results_ok": bool(check())}
             print(json.dumps({"sweep": op, "rounds_sort": int(so), "log_window": int(win or 0),
-                              "log_key": int(key or 0),
+                              "log_key": int(key or 0), "ablation": int(abl or 0), **extra,
                               "GBps": round(alg_bytes / sec / 1e9, 1),
+                              "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}), flush=True)
+
+    def decode_ablations(op, fn, alg_bytes):
+        """The rounds kernel's decode stage reads each record's header and tail
+        line a whole chunk before its data pass reads the same lines; timed
+        without them (WRONG results, written as usual): 8 no tail line, 9 no
+        header (lengths from the next offset), 10 neither."""
+        if not args.decode_ablations:
+            return
+        for tk, name in ((8, "no_tail_line"), (9, "no_header"), (10, "no_tail_no_header")):
+            with C.diagnostics() as D:
+                if args.lanes:
+                    D.nova_crc32c_set_tuning(args.lanes, 0)
+                D.nova_diag_set_trailer_single_pass(tk)
+                sec = timed(torch, fn, args.steps, args.warmup, stream)
+                D.nova_diag_set_trailer_single_pass(0)
+            print(json.dumps({"sweep": op, "decode_ablation": name, "GBps": round(alg_bytes / sec / 1e9, 1),
                               "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}), flush=True)
 
     def chunk_sweep(op, fn, alg_bytes):
@@ -315,8 +342,19 @@ def main() -> int:
                 want = orc.mask(orc.extend(orc.value(rec[6:7].tobytes()), rec[7:].tobytes()))
                 ok &= int.from_bytes(rec[:4].tobytes(), "little") == want
             emit("log_write", wl, sum_rec, sec, ok)
+
+            def check_write():  # the sampled records' CRC fields against the oracle
+                good = True
+                for i in sample:
+                    a, L = int(offs_np[i]), int(lens_np[i])
+                    rec = buf[a:a + 7 + L].cpu().numpy()
+                    want = orc.mask(orc.extend(orc.value(rec[6:7].tobytes()), rec[7:].tobytes()))
+                    good &= int.from_bytes(rec[:4].tobytes(), "little") == want
+                return good
             sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
-            sort_sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
+            # (each entry starts from CRC fields whose first byte is cleared: it must rewrite them)
+            sort_sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec, check_write,
+                       lambda: buf.__setitem__(o, 0))
             chunk_sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
             for var, name in (() if args.no_ablations else ((3, "log_write_pieces"), (4, "log_write_pieces_nt"),
                               (5, "log_write_pieces_no_writes"), (6, "log_write_no_writes"),
@@ -330,6 +368,7 @@ def main() -> int:
                 print(json.dumps({"sweep": name, "GBps": round(gbs1, 1),
                                   "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
             var_ab("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
+            decode_ablations("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
             if args.log_bound:
                 log_write_bound(buf, o, n, total, sum_rec, sec)
         if "log_verify" in ops:
@@ -343,7 +382,9 @@ def main() -> int:
             sec = timed(torch, lv, args.steps, args.warmup, stream)
             ok = int(bad.item()) == 0 and bool((okb.cpu().numpy() == C.LOG_OK).all())
             emit("log_verify", wl, sum_rec + n, sec, ok)
-            sort_sweep("log_verify", lv, sum_rec + n)
+            sort_sweep("log_verify", lv, sum_rec + n,
+                       lambda: int(bad.item()) == 0 and bool((okb.cpu().numpy() == C.LOG_OK).all()),
+                       lambda: okb.fill_(0xEE))
             chunk_sweep("log_verify", lv, sum_rec + n)
             for var, name in (() if args.no_ablations else
                               ((0, "log_verify_no_writes"), (256, "log_verify_no_tail_loads_no_writes"))):
@@ -357,6 +398,7 @@ def main() -> int:
                 print(json.dumps({"sweep": name, "GBps": round(gbs1, 1),
                                   "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
             var_ab("log_verify", lv, sum_rec + n)
+            decode_ablations("log_verify", lv, sum_rec + n)
             sweep("log_verify", lv, sum_rec + n)
         del buf
         torch.cuda.empty_cache()

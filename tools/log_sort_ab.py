@@ -82,6 +82,29 @@ def split(args) -> int:
     return 0
 
 
+def aligned_layout(total_target: int, seed: int, pmax: int, align: int):
+    """FULL records of U[1,pmax] B payloads, each at a multiple of `align`
+    bytes, none crossing a 32 KiB log block (the gap bytes are zeros)."""
+    from novalsm_amd.synth import splitmix64_words
+    blk = 32768
+    mean = 7 + (pmax + 1) // 2
+    slot_mean = (mean + align - 1) // align * align
+    n = total_target // slot_mean
+    r = splitmix64_words(seed, 0, n)
+    plens = ((r % np.uint64(pmax)) + np.uint64(1)).astype(np.int64)
+    slots = (7 + plens + align - 1) // align * align
+    offs = np.zeros(n, np.int64)
+    pos = 0
+    sl = slots.tolist()
+    rec = (7 + plens).tolist()
+    for i in range(n):
+        if pos // blk != (pos + rec[i] - 1) // blk:  # would cross a block: next block
+            pos = (pos // blk + 1) * blk
+        offs[i] = pos
+        pos += sl[i]
+    return (offs.astype(np.uint64), plens.astype(np.uint64), np.ones(n, np.uint8), int(pos))
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="2:0:0")
@@ -92,6 +115,10 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=1, help="alternations of the variant list (timing only)")
     ap.add_argument("--split", default="", help="rocprofv3 output dir to split per variant")
     ap.add_argument("--info", default="gpurun_out/log_sort_ab_info.json")
+    ap.add_argument("--align", type=int, default=0,
+                    help="place every record at a multiple of this many bytes (no line shared "
+                         "by two records: an A/B of the boundary lines' cost), records never "
+                         "crossing a 32 KiB block")
     args = ap.parse_args()
     if args.split:
         return split(args)
@@ -100,7 +127,10 @@ def main() -> int:
     from bench_ops import log_layout, timed
 
     assert C.load().nova_device_init() == 0
-    offs_np, lens_np, types_np, total = log_layout(4 << 30, args.seed, args.payload_max)
+    if args.align:
+        offs_np, lens_np, types_np, total = aligned_layout(4 << 30, args.seed, args.payload_max, args.align)
+    else:
+        offs_np, lens_np, types_np, total = log_layout(4 << 30, args.seed, args.payload_max)
     n = len(offs_np)
     buf = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
     C.fill_splitmix64(buf, 41)

@@ -23,9 +23,13 @@ STEPS=${STEPS:-pytest,sort,g1,pmc}
 [[ $STEPS == *pytest* ]] && step s1_pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
 [[ $STEPS == *sort* ]] && step s1_log_sort_ab 400 python -u tools/log_sort_ab.py --variants "$VARS" --rounds 2
 if [[ $STEPS == *g1* ]]; then
-  for g in 2 1 2 1; do
-    step s1_log512_g$g 300 python -u tools/bench_ops.py --ops log_write,log_verify --no-ablations --log-payload-max 512 --lanes $g
-    grep '"op"' gpurun_out/s1_log512_g$g.log | sed "s/^/G=$g /" >> gpurun_out/s1_log512_lanes.log
+  # one lane per record: file order, and sorted windows (negative: log write sorts too)
+  for rep in 1 2; do
+    for g in 2 1; do
+      SW=""; [ $g = 1 ] && SW="--sort-sweep 2:-1024,2:-256,2:256,2:512"
+      step s1_log512_g${g}_$rep 400 python -u tools/bench_ops.py --ops log_write,log_verify --no-ablations --log-payload-max 512 --lanes $g $SW
+      grep '"op"\|"sweep"' gpurun_out/s1_log512_g${g}_$rep.log | sed "s/^/G=$g /" >> gpurun_out/s1_log512_lanes.log
+    done
   done
 fi
 if [[ $STEPS == *pmc* ]]; then
