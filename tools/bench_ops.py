@@ -82,6 +82,8 @@ def main() -> int:
     ap.add_argument("--lanes", type=int, default=0, help="force lanes per block/record (nova_crc32c_set_tuning)")
     ap.add_argument("--var-ab", default="",
                     help="comma list of rounds-kernel variants to A/B against the product (8192 16 waves, 2 cached)")
+    ap.add_argument("--waves-sweep", default="",
+                    help="comma list of waves per workgroup for the variable kernels (diagnostics)")
     ap.add_argument("--decode-ablations", action="store_true",
                     help="log ops: time the decode stage without its tail-line / header loads "
                          "(timing ablations, WRONG results; nova_diag_set_trailer_single_pass 8/9/10)")
@@ -142,6 +144,21 @@ def main() -> int:
                 D.nova_diag_set_trailer_single_pass(0)
             print(json.dumps({"sweep": op, "decode_ablation": name, "GBps": round(alg_bytes / sec / 1e9, 1),
                               "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}), flush=True)
+
+    def waves_sweep(op, fn, alg_bytes):
+        """Waves per workgroup of the rounds kernel (nova_diag_set_stream_waves;
+        the product runs 12), alternated with the product twice."""
+        ws = [int(x) for x in args.waves_sweep.split(",") if x]
+        for rep in range(2 if ws else 0):
+            for w in [0] + ws:
+                with C.diagnostics() as D:
+                    if args.lanes:
+                        D.nova_crc32c_set_tuning(args.lanes, 0)
+                    D.nova_diag_set_stream_waves(w)
+                    sec = timed(torch, fn, args.steps, args.warmup, stream)
+                    D.nova_diag_set_stream_waves(0)
+                print(json.dumps({"sweep": op, "waves": w, "rep": rep, "GBps": round(alg_bytes / sec / 1e9, 1),
+                                  "frac": round(alg_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}), flush=True)
 
     def chunk_sweep(op, fn, alg_bytes):
         for c in [int(x) for x in args.chunk_sweep.split(",") if x]:
@@ -369,6 +386,7 @@ def main() -> int:
                                   "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
             var_ab("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
             decode_ablations("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
+            waves_sweep("log_write", lambda: C.log_write_crcs(buf, o, stream=stream), sum_rec)
             if args.log_bound:
                 log_write_bound(buf, o, n, total, sum_rec, sec)
         if "log_verify" in ops:
@@ -399,6 +417,7 @@ def main() -> int:
                                   "frac": round(gbs1 / HBM_PEAK_GBS, 4)}), flush=True)
             var_ab("log_verify", lv, sum_rec + n)
             decode_ablations("log_verify", lv, sum_rec + n)
+            waves_sweep("log_verify", lv, sum_rec + n)
             sweep("log_verify", lv, sum_rec + n)
         del buf
         torch.cuda.empty_cache()
