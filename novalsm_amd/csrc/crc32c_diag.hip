@@ -1095,8 +1095,10 @@ constexpr int kNotTaken = -999;               // a hook found nothing to do
 // (lengths from the next offset) / neither (timing ablations: WRONG results,
 // written as usual, so the traffic is the product's minus those loads);
 // 11 = sorted windows in the XCD-contiguous chunk order (results right).
+// 12 / 13 = the rounds kernel's step work (timing ablations, WRONG results):
+// no head masking / no group fold at a round's end.
 uint32_t wvar_of(int tkn) {
-  return tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : tkn == 7 ? 3u : (tkn >= 8 && tkn <= 11) ? (uint32_t)(tkn - 4) : 0u;
+  return tkn == 4 ? 1u : (tkn == 5 || tkn == 6) ? 2u : tkn == 7 ? 3u : (tkn >= 8 && tkn <= 13) ? (uint32_t)(tkn - 4) : 0u;
 }
 
 template <int G, int MODE, int VAR = 0>

@@ -2017,7 +2017,10 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
     }
     if constexpr (MODE == kVerify || MODE == kLogVerify) {
       const uint64_t b = __builtin_amdgcn_ballot_w64(bad);  // one atomic per chunk
-      if (b && lane == 0 && p.n_bad) atomicAdd(p.n_bad, (uint32_t)__builtin_popcountll(b));
+      // (the timing ablations that compute WRONG CRCs count nothing: every
+      // chunk's atomic on one word would time the counter, not the kernel)
+      const bool wrong = kDiag && p.wvar >= 4 && p.wvar != 7;
+      if (b && lane == 0 && p.n_bad && !wrong) atomicAdd(p.n_bad, (uint32_t)__builtin_popcountll(b));
     }
   };
 
@@ -2029,7 +2032,8 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
   uint32_t wb_pos = 0, wb_st = 0;       // kVarOutPos log write: position, status
   auto fold = [&](FlatSet& Y) {
     uint4 d0 = Y.d0, d1 = Y.d1, d2 = Y.d2, d3 = Y.d3;
-    if (__builtin_amdgcn_ballot_w64(Y.head)) {  // wave-uniform: some group's head step
+    // (diagnostics timing ablation, wvar 8: no head masking -- WRONG CRCs)
+    if (!(kDiag && p.wvar == 8) && __builtin_amdgcn_ballot_w64(Y.head)) {  // wave-uniform: some group's head step
       // h = u0 - (lane's piece of swath 0 of the step); pieces wholly before u0
       // came from the zero line, so only [u0, u0+4) and the bytes before u0 in
       // u0's piece need work.  Non-head groups keep their data (h <= -16).
@@ -2112,11 +2116,16 @@ __global__ void __launch_bounds__((VAR & kVarInit) ? kInitMaxWaves * 64 : (VAR &
       // position p in lane p, which reads lane (p + e) mod G.
       const uint32_t e = (uint32_t)(Y.u1 >> 4) & (uint32_t)(G - 1);
       const int src = (grp * G) + (int)(((uint32_t)q + e) & (uint32_t)(G - 1));
-      c0 = __shfl(c0, src);
-      c1 = __shfl(c1, src);
-      c2 = __shfl(c2, src);
-      c3 = __shfl(c3, src);
-      const uint32_t v = group_fold<G>(lds, c0, c1, c2, c3, q);
+      uint32_t v;
+      if (kDiag && p.wvar == 9) {  // (timing ablation: no group fold -- WRONG CRCs)
+        v = c0 ^ c1 ^ c2 ^ c3;
+      } else {
+        c0 = __shfl(c0, src);
+        c1 = __shfl(c1, src);
+        c2 = __shfl(c2, src);
+        c3 = __shfl(c3, src);
+        v = group_fold<G>(lds, c0, c1, c2, c3, q);
+      }
       c0 = c1 = c2 = c3 = 0;
       if constexpr (kBatch) {
         if (q == 0 && Y.valid) vbuf[Y.slot] = v;

@@ -46,15 +46,15 @@ def timed(torch, fn, steps, warmup, stream):
     return sum(ms) / len(ms) / 1e3
 
 
-def log_layout(total_target: int, seed: int, pmax: int = 4096):
+def log_layout(total_target: int, seed: int, pmax: int = 4096, pmin: int = 1):
     """A log file of ~total_target bytes as log::Writer lays it out
     (db/log_writer.cc:53-97, novalsm_amd/synth.log_layout): logical records of
-    U[1,pmax] B payload from splitmix64(seed), fragmented at 32 KiB blocks.
+    U[pmin,pmax] B payload from splitmix64(seed), fragmented at 32 KiB blocks.
     Returns the physical records' (offsets, payload lengths, types, total)."""
     from novalsm_amd.synth import splitmix64_words, log_layout as writer_layout
-    n = total_target // (7 + (pmax + 1) // 2)
+    n = total_target // (7 + (pmax + pmin) // 2)
     r = splitmix64_words(seed, 0, n)
-    plens = ((r % np.uint64(pmax)) + np.uint64(1)).astype(np.int64)
+    plens = ((r % np.uint64(pmax - pmin + 1)) + np.uint64(pmin)).astype(np.int64)
     offs, lens, types, _, total = writer_layout(plens)
     return offs, lens.astype(np.uint64), types, total
 
@@ -75,7 +75,8 @@ def main() -> int:
                     help="log ops: comma list of nova_diag_set_rounds_sort values (0 in order, "
                          "2 windows + chunks, 3 windows only)")
     ap.add_argument("--log-seed", type=int, default=6, help="log image: payload-length seed")
-    ap.add_argument("--log-payload-max", type=int, default=4096, help="log image: payloads U[1,max] B")
+    ap.add_argument("--log-payload-max", type=int, default=4096, help="log image: payloads U[min,max] B")
+    ap.add_argument("--log-payload-min", type=int, default=1, help="log image: payloads U[min,max] B")
     ap.add_argument("--chunk-sweep", default="",
                     help="comma list of rounds-kernel chunk sizes (nova_diag_set_chunk_blocks), log ops")
     ap.add_argument("--no-ablations", action="store_true", help="skip the diagnostics ablations")
@@ -132,10 +133,12 @@ def main() -> int:
         """The rounds kernel's decode stage reads each record's header and tail
         line a whole chunk before its data pass reads the same lines; timed
         without them (WRONG results, written as usual): 8 no tail line, 9 no
-        header (lengths from the next offset), 10 neither."""
+        header (lengths from the next offset), 10 neither.  The step work, the
+        same way: 12 no head masking, 13 no group fold at a round's end."""
         if not args.decode_ablations:
             return
-        for tk, name in ((8, "no_tail_line"), (9, "no_header"), (10, "no_tail_no_header")):
+        for tk, name in ((8, "no_tail_line"), (9, "no_header"), (10, "no_tail_no_header"),
+                         (12, "no_head_masking"), (13, "no_group_fold")):
             with C.diagnostics() as D:
                 if args.lanes:
                     D.nova_crc32c_set_tuning(args.lanes, 0)
@@ -336,7 +339,8 @@ def main() -> int:
 
     if "log_write" in ops or "log_verify" in ops:
         pmax = args.log_payload_max
-        offs_np, lens_np, types_np, total = log_layout(4 << 30, args.log_seed, pmax)
+        pmin = args.log_payload_min
+        offs_np, lens_np, types_np, total = log_layout(4 << 30, args.log_seed, pmax, pmin)
         n = len(offs_np)
         buf = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
         C.fill_splitmix64(buf, 41)
@@ -347,7 +351,7 @@ def main() -> int:
         buf[o + 5] = (ln >> 8).to(torch.uint8)
         buf[o + 6] = torch.from_numpy(types_np).cuda()
         sum_rec = int(lens_np.sum()) + 7 * n
-        wl = f"log image: {n} records, payload U[1,{pmax}] B, {total / 2**30:.2f} GiB"
+        wl = f"log image: {n} records, payload U[{pmin},{pmax}] B, {total / 2**30:.2f} GiB"
         sample = np.linspace(0, n - 1, 129).astype(np.int64)
         if "log_write" in ops:
             sec = timed(torch, lambda: C.log_write_crcs(buf, o, stream=stream), args.steps,
