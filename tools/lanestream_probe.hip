@@ -9,12 +9,16 @@
 //   steps    16-B loads per lane per step (4: 64 B), two steps in flight
 //   waves    per workgroup (8, 12); one workgroup per CU (LDS image)
 //   nt       non-temporal loads (1) or the default policy (0)
-//   compute  the swath's lookups on every 16 B (1) or none (0)
+//   compute  the swath's lookups on every 16 B (1) or none (0); with the
+//            argument "depth": the lookups K times per piece and 1 or 2 steps
+//            of loads in flight, printed as compute = K (one step in flight)
+//            or 10 K + 2 (two steps): 1 / 12, 2 / 22, 3 / 32
 // Prints one JSON line per shape: best-of-5 time, GB/s, % of 8 TB/s.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/lanestream_probe.hip -o tools/bin/lanestream_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <string>
 #include <vector>
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u4;
@@ -54,8 +58,10 @@ __device__ __forceinline__ void swath(unsigned& c0, unsigned& c1, unsigned& c2, 
 // shape G (1, 2, 4, 8): 64 / G streams per wave, lane q of a G-lane group
 // reading piece q of each 16G-byte swath of its group's run (the rounds
 // kernel's shape at G lanes per record); shape 64: coalesced wave-lines
-// (1 KiB per instruction, the stream kernel's shape)
-template <bool NT, bool COMPUTE>
+// (1 KiB per instruction, the stream kernel's shape).  K: the swath's lookups
+// K times per piece (K = 3: about the rounds kernel's issue work per step at
+// 2 lanes); DEPTH: steps of loads in flight while a step folds (1 or 2).
+template <bool NT, bool COMPUTE, int K = 1, int DEPTH = 1>
 __global__ void __launch_bounds__(768) probe_kernel(const u4* __restrict__ a, size_t n16, size_t run16,
                                                     int shape, unsigned* out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -71,6 +77,19 @@ __global__ void __launch_bounds__(768) probe_kernel(const u4* __restrict__ a, si
   // wave-lines (coalesced); units are strided over the grid's waves
   const size_t unit16 = 64 * run16;
   const size_t units = n16 / unit16;
+  auto fold = [&](u4 y0, u4 y1, u4 y2, u4 y3) {
+    if constexpr (COMPUTE) {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        swath(c0, c1, c2, c3, y0, lo);
+        swath(c0, c1, c2, c3, y1, lo);
+        swath(c0, c1, c2, c3, y2, lo);
+        swath(c0, c1, c2, c3, y3, lo);
+      }
+    } else {
+      acc ^= y0 ^ y1 ^ y2 ^ y3;
+    }
+  };
   for (size_t u = gw; u < units; u += tw) {
     const u4* base = a + u * unit16;
     const size_t G = (size_t)shape, grp = lane / G, q = lane % G;
@@ -78,21 +97,29 @@ __global__ void __launch_bounds__(768) probe_kernel(const u4* __restrict__ a, si
       return base + grp * (run16 * G) + k * G + q;
     };
     u4 x0 = ld<NT>(addr(0)), x1 = ld<NT>(addr(1)), x2 = ld<NT>(addr(2)), x3 = ld<NT>(addr(3));
-    for (size_t k = 4; k <= run16; k += 4) {
-      u4 y0 = x0, y1 = x1, y2 = x2, y3 = x3;
-      if (k < run16) {
-        x0 = ld<NT>(addr(k));
-        x1 = ld<NT>(addr(k + 1));
-        x2 = ld<NT>(addr(k + 2));
-        x3 = ld<NT>(addr(k + 3));
+    if constexpr (DEPTH == 1) {
+      for (size_t k = 4; k <= run16; k += 4) {
+        u4 y0 = x0, y1 = x1, y2 = x2, y3 = x3;
+        if (k < run16) {
+          x0 = ld<NT>(addr(k));
+          x1 = ld<NT>(addr(k + 1));
+          x2 = ld<NT>(addr(k + 2));
+          x3 = ld<NT>(addr(k + 3));
+        }
+        fold(y0, y1, y2, y3);
       }
-      if constexpr (COMPUTE) {
-        swath(c0, c1, c2, c3, y0, lo);
-        swath(c0, c1, c2, c3, y1, lo);
-        swath(c0, c1, c2, c3, y2, lo);
-        swath(c0, c1, c2, c3, y3, lo);
-      } else {
-        acc ^= y0 ^ y1 ^ y2 ^ y3;
+    } else {  // two steps in flight: fold step k-8 while k-4 and k are loading
+      u4 z0 = ld<NT>(addr(4)), z1 = ld<NT>(addr(5)), z2 = ld<NT>(addr(6)), z3 = ld<NT>(addr(7));
+      for (size_t k = 8; k <= run16 + 4; k += 4) {
+        u4 y0 = x0, y1 = x1, y2 = x2, y3 = x3;
+        x0 = z0, x1 = z1, x2 = z2, x3 = z3;
+        if (k < run16) {
+          z0 = ld<NT>(addr(k));
+          z1 = ld<NT>(addr(k + 1));
+          z2 = ld<NT>(addr(k + 2));
+          z3 = ld<NT>(addr(k + 3));
+        }
+        fold(y0, y1, y2, y3);
       }
     }
   }
@@ -100,7 +127,7 @@ __global__ void __launch_bounds__(768) probe_kernel(const u4* __restrict__ a, si
   if (x == 0x9e3779b9u) out[blockIdx.x] = x;
 }
 
-int main() {
+int main(int argc, char** argv) {
   const size_t bytes = 4ull << 30, n16 = bytes / 16;
   u4* a = nullptr;
   unsigned* out = nullptr;
@@ -129,20 +156,33 @@ int main() {
            shape, run_b, waves, nt, comp, best, gbs, gbs / 8000.0);
     fflush(stdout);
   };
-  for (int comp = 0; comp <= 1; comp++)
-    for (int shape : {1, 2, 4, 8, 64})
-      for (size_t rb : {4096ul, 8192ul})
-        for (int waves : {8, 12})
-          for (int nt = 0; nt <= 1; nt++) {
-            if (shape == 64 && rb != 8192) continue;
-            if (comp) {
-              if (nt) run(probe_kernel<true, true>, shape, rb, waves, nt, comp);
-              else run(probe_kernel<false, true>, shape, rb, waves, nt, comp);
-            } else {
-              if (nt) run(probe_kernel<true, false>, shape, rb, waves, nt, comp);
-              else run(probe_kernel<false, false>, shape, rb, waves, nt, comp);
+  if (argc > 1 && std::string(argv[1]) == "depth") {
+    // two lanes per stream, default policy, 8 KiB per lane: issue work per
+    // step (K) against steps of loads in flight (DEPTH)
+    for (int waves : {8, 12}) {
+      run(probe_kernel<false, true, 1, 1>, 2, 8192, waves, 0, 1);
+      run(probe_kernel<false, true, 1, 2>, 2, 8192, waves, 0, 12);
+      run(probe_kernel<false, true, 2, 1>, 2, 8192, waves, 0, 2);
+      run(probe_kernel<false, true, 2, 2>, 2, 8192, waves, 0, 22);
+      run(probe_kernel<false, true, 3, 1>, 2, 8192, waves, 0, 3);
+      run(probe_kernel<false, true, 3, 2>, 2, 8192, waves, 0, 32);
+    }
+  } else {
+    for (int comp = 0; comp <= 1; comp++)
+      for (int shape : {1, 2, 4, 8, 64})
+        for (size_t rb : {4096ul, 8192ul})
+          for (int waves : {8, 12})
+            for (int nt = 0; nt <= 1; nt++) {
+              if (shape == 64 && rb != 8192) continue;
+              if (comp) {
+                if (nt) run(probe_kernel<true, true>, shape, rb, waves, nt, comp);
+                else run(probe_kernel<false, true>, shape, rb, waves, nt, comp);
+              } else {
+                if (nt) run(probe_kernel<true, false>, shape, rb, waves, nt, comp);
+                else run(probe_kernel<false, false>, shape, rb, waves, nt, comp);
+              }
             }
-          }
+  }
   (void)hipFree(a);
   (void)hipFree(out);
   return 0;
