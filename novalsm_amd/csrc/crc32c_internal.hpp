@@ -87,7 +87,9 @@ struct CrcParams {
                   // 2 = no result writes, 3 = no per-block epilogue and no writes;
                   // log records: 4 / 5 / 6 = the decode stage reads no tail line /
                   // no header / neither (WRONG results, written); 7 = the
-                  // XCD-contiguous chunk order with a permutation too
+                  // XCD-contiguous chunk order with a permutation too; 8 / 9 =
+                  // no head masking / no group fold at a round's end (WRONG
+                  // results, written); 4-6, 8, 9 count no mismatches
 };
 
 // Kernel variants (diagnostics / tuning; 0 = production).
