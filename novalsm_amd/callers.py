@@ -4,8 +4,10 @@ device-resident SSTable image back to back -- through the persistent engine
 (nova_sst_queue_*), the coalescing queue, or direct calls with a stream sync --
 optionally beside one thread of plain calls (block verify, log verify, CRC
 batch).  Used by bench.py's sst_engine secondary, tools/concurrent_sst.py and
-the mixed-caller GPU test.  Every call's result is checked natively
-(sst_callers.cpp header); the returned dict says whether all were right.
+the mixed-caller GPU test.  Results are checked natively, as the
+sst_callers.cpp header states exactly: every verify call's mismatch count and
+flags, the trailers' final image, every plain call's result; the returned dict
+says whether all were right.
 """
 from __future__ import annotations
 
