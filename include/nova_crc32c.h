@@ -247,6 +247,11 @@ void nova_sst_engine_set_wait_delay_us(uint32_t us);
  * with a request it took unfinished (its submitter takes it back, DESIGN.md
  * 3.5g). */
 int nova_sst_engine_set_give_up_us(uint32_t us);
+/* Test hook: from the next instance, on != 0 makes the engine's workers run no
+ * chunk (the dispatcher still takes requests), so with a short give-up time the
+ * instance ends "lost" with every request it took unfinished, deterministically.
+ * Not for production use. */
+int nova_sst_engine_set_drop_chunks(uint32_t on);
 /* The calling thread's last engine request, out[0..n) (n <= 8): host ns
  * waiting for the engine's lock, ns holding it (ring writes, a relaunch), ns
  * waiting for the completion words; sleeps during that wait, relaunches

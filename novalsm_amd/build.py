@@ -87,6 +87,16 @@ def build(force: bool = False, verbose: bool = False, extra: list[str] | None = 
     diag_obj = os.path.join(LIB_DIR, "crc32c_diag.o")
     if diag:
         jobs[diag_obj] = _compile_cmd(cc, DIAG_SOURCE, diag_obj, [], extra)
+    # objects stay in lib/ (git- and gpurun-ignored): one whose source and the
+    # shared headers are older than it is not compiled again
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [__file__]
+    def fresh(obj: str, src: str) -> bool:
+        if force or not os.path.exists(obj):
+            return False
+        t = os.path.getmtime(obj)
+        return all(os.path.getmtime(d) <= t for d in hdrs + [os.path.join(CSRC, src)] if os.path.exists(d))
+    srcs = {os.path.join(LIB_DIR, os.path.splitext(s)[0] + ".o"): s for s in SOURCES + [DIAG_SOURCE]}
+    jobs = {o: c for o, c in jobs.items() if not fresh(o, srcs[o])}
     procs = []
     for obj, cmd in jobs.items():
         if verbose:
@@ -101,8 +111,6 @@ def build(force: bool = False, verbose: bool = False, extra: list[str] | None = 
         subprocess.run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +
                        ["-lpthread"], check=True)
         os.replace(tmp, lib)
-    for o in jobs:
-        os.remove(o)
     build_callers(cc)
     return LIB
 

@@ -78,6 +78,7 @@ _SIG = {
     "nova_sst_engine_reset": (_i32, []),
     "nova_sst_engine_set_wait_delay_us": (None, [_u32]),
     "nova_sst_engine_set_give_up_us": (_i32, [_u32]),
+    "nova_sst_engine_set_drop_chunks": (_i32, [_u32]),
     "nova_crc32c_stream_host": (_i32, [_vp, _u64, _u32, _sz, _vp, _u32, _sz, _i32]),
     "nova_crc32c_batch_host": (_i32, [_vp, _vp, _vp, _vp, _vp, _sz, _u32, _sz, _i32]),
     "nova_sstable_write_trailers_host": (_i32, [_vp, _vp, _vp, _sz, _u32, _sz, _i32]),
@@ -512,6 +513,13 @@ def engine_set_give_up_us(us: int) -> None:
     the default 20 s); a dispatcher with a request unfinished that long after
     the last arrival exits "lost"."""
     _check(_L().nova_sst_engine_set_give_up_us(int(us)), "nova_sst_engine_set_give_up_us")
+
+
+def engine_set_drop_chunks(on: bool) -> None:
+    """Test hook: from the next instance the engine's workers run no chunk, so
+    with a short give-up time an instance ends "lost" with the requests it took
+    unfinished."""
+    _check(_L().nova_sst_engine_set_drop_chunks(1 if on else 0), "nova_sst_engine_set_drop_chunks")
 
 
 def engine_set_enabled(on: int) -> None:

@@ -11,7 +11,7 @@
 // 14-29 % of the HBM roofline.
 //
 // The engine pays the launch and the table fill once per burst of requests:
-//   * one workgroup per CU (8 waves) stays resident with the M_256 tables in
+//   * one workgroup per CU (12 waves) stays resident with the M_256 tables in
 //     LDS (G = 16 lanes per block);
 //   * a submitting thread writes its request (image, descriptor arrays,
 //     outputs, op, blocks per chunk) into a ring as tagged 8-byte words, and
@@ -26,10 +26,10 @@
 //     per XCD: group = workgroup index % 8, which is the XCD a workgroup runs
 //     on under the round-robin dispatch; MI355X_MICROARCH.md "dequeue"),
 //     finds the ticket's request (its cursor slot and the ticket's page, one
-//     round trip), runs the chunk (engine_chunk: rounds of 4 blocks, all of a
-//     block's loads at once), counts it on its group's counter line and only
-//     then claims its next ticket (the claim's add is contended; before the
-//     chunk, every load of the chunk would wait for it);
+//     round trip), runs the chunk (engine_chunk: rounds of 4 blocks, a
+//     block's loads in two passes), counts it on its group's counter line and
+//     only then claims its next ticket (the claim's add is contended; before
+//     the chunk, every load of the chunk would wait for it);
 //   * the last chunk of a group writes that group's completion word of the
 //     request in pinned host memory (the dispatcher writes those of groups
 //     without tickets); the submitter spins until all 8 are set (a test for
@@ -112,10 +112,15 @@ using namespace nova_dev;
 
 constexpr uint32_t kRing = 1024;  // requests in flight (host ring and device slots)
 constexpr int kEngG = 16;         // lanes per block (units kernel: G = 16)
-// Launch bound: 8 waves per CU (182 VGPRs).  A 12-wave build (168 VGPRs)
-// spilled and measured 5-20 % slower (profiles/r04_engine_conc_v4.log).
-constexpr int kEngMaxWaves = 8;
-constexpr int kEngWaves = 8;
+// Launch bound: 12 waves per CU, two passes of kEK12 swaths per 4 KiB block
+// (157 VGPRs).  Round 4's 12-wave build kept the one-pass loads (kEK) and
+// spilled; the 8-wave one-pass build (211 VGPRs) stays for
+// NOVA_SST_ENGINE_WAVES <= 8.  Round 6, same boxes (profiles/r06_engine_waves.log):
+// verify at 16 callers 4.55-4.68 -> 5.12-5.28 TB/s, 8 callers 4.33-4.35 ->
+// 4.60-4.70; trailers 4.35-4.43 -> 4.72-4.82 / 4.24 -> 4.39-4.47.
+constexpr int kEngMaxWaves = 12;
+constexpr int kEngWaves8 = 8;
+constexpr int kEngWaves = 12;
 constexpr uint32_t kCntGroups = kEngGroups;
 constexpr uint32_t kTrWords = 16;
 // Ticket pages: page[p] holds a copy of the request holding ticket kPage * p
@@ -257,6 +262,7 @@ struct EngParams {
   uint64_t slice_ticks;    // 0, or: take no request after running this long (then exit; the next instance follows)
   uint64_t* htrace;        // trace (or null): per request, the tr words copied to pinned memory
   uint32_t page_poll;      // waiting workers poll their ticket's page (NOVA_SST_ENGINE_PAGE_POLL, default 1)
+  uint32_t drop_chunks;    // test hook: the workers run no chunk (nova_sst_engine_set_drop_chunks)
   CrcParams tab;           // tables and zero line for every chunk
 };
 
@@ -571,6 +577,7 @@ __device__ __forceinline__ void engine_dispatch(const EngParams& e) {
 // Every load of caller memory is non-temporal and every result store is
 // write-through (the engine outlives the caller's writes and reads).
 constexpr int kEK = 18;  // swaths per pass: 4.5 KiB (4096 + 255 + 5 B blocks: one pass)
+constexpr int kEK12 = 9;  // the 12-wave build: 2 passes per 4 KiB block (157 VGPRs)
 
 // A trailer [type][LE32 masked crc] written through (sc1, as st_through's
 // agent-scope stores compile): the type byte, then the CRC as one unaligned
@@ -584,7 +591,7 @@ __device__ __forceinline__ void engine_store_trailer(uint8_t* d, uint32_t type, 
   asm volatile("global_store_dword %0, %1, off sc1" ::"v"(d + 1), "v"(w) : "memory");
 }
 
-template <int MODE>
+template <int MODE, int EK>
 __device__ __forceinline__ void engine_chunk(const uint8_t* lds, const CrcParams& p, uint64_t c) {
   constexpr int G = kEngG;
   constexpr uint64_t kS = 16ull * G;
@@ -641,16 +648,16 @@ __device__ __forceinline__ void engine_chunk(const uint8_t* lds, const CrcParams
     // since a round may pair a block over 1 GiB with short ones whose start
     // then lies more than 2^30 bytes after the round's first piece
     int64_t urel = (int64_t)(u0 - first), arel = (int64_t)(A0 - first);
-    for (uint32_t k0 = 0; k0 < Kw; k0 += kEK) {
-      uint4 d[kEK];
+    for (uint32_t k0 = 0; k0 < Kw; k0 += EK) {
+      uint4 d[EK];
 #pragma unroll
-      for (int i = 0; i < kEK; i++) {
+      for (int i = 0; i < EK; i++) {
         const bool in = valid && k0 + i < Kw && (int64_t)(kS * i) >= arel;
         d[i] = gload16(in ? first + (uint64_t)i * kS : zl);
       }
       if (k0 == 0 && b0 + kGroups < b_hi) desc(b0 + kGroups, o_nxt, l_nxt);  // under the data loads
 #pragma unroll
-      for (int i = 0; i < kEK; i++) {
+      for (int i = 0; i < EK; i++) {
         if (k0 + i < Kw) {  // wave-uniform
           const int64_t hr = urel - (int64_t)(kS * i);
           const int32_t h = hr < -4 ? -4 : (hr > 32 ? 32 : (int32_t)hr);
@@ -658,9 +665,9 @@ __device__ __forceinline__ void engine_chunk(const uint8_t* lds, const CrcParams
           swath4<0>(lds, c0, c1, c2, c3, w, lo0, lo1, lo2, lo3);
         }
       }
-      first += (uint64_t)kEK * kS;  // the next pass
-      urel -= (int64_t)(kEK * kS);
-      arel -= (int64_t)(kEK * kS);
+      first += (uint64_t)EK * kS;  // the next pass
+      urel -= (int64_t)(EK * kS);
+      arel -= (int64_t)(EK * kS);
     }
     // fold the group's stream words: in-lane M4/M8, then M16 .. M128 across the group
     uint32_t v = lapply(tree + kTreeBytes, lapply(tree, c0) ^ c1) ^ (lapply(tree, c2) ^ c3);
@@ -701,8 +708,11 @@ __device__ __forceinline__ void engine_chunk(const uint8_t* lds, const CrcParams
 }
 
 // Every other wave: tickets -> chunks (engine_chunk).
-template <int G>
+template <int G, int EK>
 __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* lds) {
+  // (test hook: no worker runs a chunk, so the dispatcher's "lost" exit leaves
+  // the requests it took unfinished whatever the timing)
+  if (e.drop_chunks) return;
   const int lane = threadIdx.x & 63;
   EngDev* d = e.dev;
   // Tickets t with t % 8 == x go to the waves of group x, each taking the
@@ -906,12 +916,12 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
     if (mode == kVerify) {
       p.ok_out = (uint8_t*)uni64(out);
       p.n_bad = (uint32_t*)uni64(bad);
-      engine_chunk<kVerify>(lds, p, c);
+      engine_chunk<kVerify, EK>(lds, p, c);
     } else if (mode == kTrailer) {
-      engine_chunk<kTrailer>(lds, p, c);
+      engine_chunk<kTrailer, EK>(lds, p, c);
     } else {
       p.out = (uint32_t*)uni64(out);
-      engine_chunk<kStore>(lds, p, c);
+      engine_chunk<kStore, EK>(lds, p, c);
     }
     // publish the chunk: its results were stored write-through (st_through);
     // once drained they are in memory, so the count needs no release fence
@@ -956,12 +966,13 @@ __device__ __forceinline__ void engine_work(const EngParams& e, const uint8_t* l
     }
     // the next ticket: claimed after this chunk is counted (the claim's add
     // is contended; issued before the chunk, every load of the chunk waited
-    // for it: in-order vmcnt)
+    // for it: in-order vmcnt; issued under the chunk's last loads instead, it
+    // measured the same: profiles/r06_engine_waves.log)
     t = claim();
   }
 }
 
-template <int G, int W>
+template <int G, int W, int EK>
 __global__ void __launch_bounds__(W * 64) crc32c_engine_kernel(EngParams e) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   lds_fill_tables(lds, e.tab.tab_main, e.tab.tab_tree, tree_levels<G>() * kTreeBytes / 16, e.tab.tab_byte, 64);
@@ -976,7 +987,15 @@ __global__ void __launch_bounds__(W * 64) crc32c_engine_kernel(EngParams e) {
     engine_dispatch(e);
     return;
   }
-  engine_work<G>(e, lds);
+  engine_work<G, EK>(e, lds);
+}
+
+// The instantiation a launch of `waves` waves per CU uses: 9-12 waves the
+// two-pass build (kEK12 swaths per pass, 157 VGPRs: 3 waves per SIMD), up to
+// 8 the one-pass build (kEK, 211 VGPRs).
+inline const void* engine_fn(uint32_t waves) {
+  return waves > (uint32_t)kEngWaves8 ? reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG, kEngMaxWaves, kEK12>)
+                                      : reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG, kEngWaves8, kEK>);
 }
 
 template <int G>
@@ -1083,6 +1102,7 @@ struct Engine {
   uint64_t gap_ticks_max = 0;                   // the dispatchers' longest gap between two polls
   uint32_t idle_us = 0, waves = 0;
   uint32_t give_up_us = 0;                    // 0: 20 s (nova_sst_engine_set_give_up_us, a test hook)
+  uint32_t drop_chunks = 0;                   // nova_sst_engine_set_drop_chunks (a test hook)
   // Take-backs waiting (with mu released) for an instance to end: no instance
   // is launched meanwhile, so the stream's last work stays the one waited for.
   int tb_active = 0;
@@ -1174,8 +1194,10 @@ struct Engine {
     if (e == hipSuccess) e = hipMalloc((void**)&ddev, sizeof(EngDev));
     if (e == hipSuccess) e = hipMemset(ddev, 0, sizeof(EngDev));  // slots: seq1 = 0 (never written)
     if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG, kEngMaxWaves>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)engine_lds<kEngG>(kEngMaxWaves));
+      for (const uint32_t wv : {(uint32_t)kEngWaves8, (uint32_t)kEngMaxWaves})
+        if (e == hipSuccess)
+          e = hipFuncSetAttribute(engine_fn(wv), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)engine_lds<kEngG>((int)wv));
 
     if (e != hipSuccess) {
       (void)hipGetLastError();
@@ -1298,6 +1320,7 @@ struct Engine {
     p.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
     // 20 s (every spin of the engine is bounded); shorter only through the test hook
     p.give_up_ticks = give_up_us ? (uint64_t)give_up_us * 100 : 20ull * 100000000ull;
+    p.drop_chunks = drop_chunks;
     p.slice_ticks = (uint64_t)slice_us * 100;
     p.htrace = trace ? htrace : nullptr;
     static const uint32_t page_poll = (uint32_t)env_u64("NOVA_SST_ENGINE_PAGE_POLL", 1);
@@ -1310,8 +1333,7 @@ struct Engine {
     p.tab.zline = reinterpret_cast<const uint8_t*>(t->zero_word);
     if (queue_mode == 1) {
       void* args[] = {&p};
-      e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&crc32c_engine_kernel<kEngG, kEngMaxWaves>),
-                                     dim3((uint32_t)cus), dim3(64 * waves), args,
+      e = hipLaunchCooperativeKernel(engine_fn(waves), dim3((uint32_t)cus), dim3(64 * waves), args,
                                      (unsigned)engine_lds<kEngG>((int)waves), stream);
       if (e != hipSuccess) {  // not available: plain launches (time-sliced like the others)
         (void)hipGetLastError();
@@ -1319,9 +1341,9 @@ struct Engine {
       }
     }
     if (queue_mode != 1) {
-      hipLaunchKernelGGL((crc32c_engine_kernel<kEngG, kEngMaxWaves>), dim3((uint32_t)cus), dim3(64 * waves),
-                         engine_lds<kEngG>((int)waves), stream, p);
-      e = hipGetLastError();
+      void* args[] = {&p};
+      e = hipLaunchKernel(engine_fn(waves), dim3((uint32_t)cus), dim3(64 * waves), args,
+                          engine_lds<kEngG>((int)waves), stream);
     }
     if (e != hipSuccess) {
       running = false;
@@ -1896,6 +1918,15 @@ int nova_sst_engine_set_give_up_us(uint32_t us) {
   if (!gp) return err;
   std::lock_guard<SpinMutex> lk(gp->mu);
   gp->give_up_us = us;  // from the next instance
+  return 0;
+}
+
+int nova_sst_engine_set_drop_chunks(uint32_t on) {
+  int err = 0;
+  Engine* gp = engine_for_device(&err);
+  if (!gp) return err;
+  std::lock_guard<SpinMutex> lk(gp->mu);
+  gp->drop_chunks = on ? 1u : 0u;  // from the next instance
   return 0;
 }
 

@@ -278,9 +278,9 @@ def test_engine_take_back_when_held_off(torch_gpu, oracle, engine_on):
 
 def test_engine_lost_request_frees_its_slot(torch_gpu, oracle, engine_on):
     """an instance that took a request and ended without
-    finishing it (here a "lost" exit: give-up and idle times cut to 1 us by
-    test hooks, so the dispatcher gives up on a 128K-block table ~1 us after
-    taking it, and its workers stop) left
+    finishing it (here a "lost" exit: test hooks make the workers run no chunk
+    and cut the give-up and idle times to 1 us, so the dispatcher gives up on
+    the table ~1 us after taking it, whatever the engine's speed) left
     that request's completion words unwritten; no later instance revisits it,
     so its ring slot never freed and the request reaching that slot a ring
     turn later waited 1 s and fell back.  Now the take-back writes them once
@@ -298,10 +298,12 @@ def test_engine_lost_request_frees_its_slot(torch_gpu, oracle, engine_on):
     try:
         C.engine_set_give_up_us(1)
         C.engine_set_idle_us(1)
+        C.engine_set_drop_chunks(True)
         C.queue_verify_blocks(big["img"], big["offs"], big["lens"], ok, nb)
     finally:
         C.engine_set_give_up_us(0)
         C.engine_set_idle_us(0)
+        C.engine_set_drop_chunks(False)
     assert np.array_equal(ok.cpu().numpy(), big["want"]) and int(nb.item()) == 2
     c1 = C.engine_counters()
     assert c1["exits_lost"] - c0["exits_lost"] >= 1 or c1["errors"] - c0["errors"] >= 1, (c0, c1)
