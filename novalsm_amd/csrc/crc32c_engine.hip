@@ -1628,10 +1628,16 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
     g.next_seq = seq + 1;
     g.inflight.fetch_add(1);
     const uint64_t blocks = g.inflight_blocks.fetch_add(n) + n;
-    // blocks per chunk: 4 (one round of the chunk body) per 16K blocks in
-    // flight -- short chunks (latency) when the engine is quiet, longer ones
-    // (fewer tickets per block) when it is busy (tools/concurrent_sst.py sweep)
-    const uint32_t cb = cb_fixed ? cb_fixed : (uint32_t)std::min<uint64_t>(16, 4 * ((blocks + 16383) / 16384));
+    // blocks per chunk, a multiple of 4 (one round of the chunk body): short
+    // chunks (latency) when the engine is quiet, longer ones (fewer tickets per
+    // block) when it is busy.  12 waves (1.5x the workers): 4 per 20K blocks in
+    // flight, rounded down -- for 4K-block tables 4 up to 9 callers, 8 at 10-14,
+    // 12 at 15-19 (each the best of 4 / 8 / 12 / 16 in the sweeps,
+    // profiles/r06_engine_cb12.log); 8 waves: 4 per 16K, rounded up
+    // (tools/concurrent_sst.py sweeps, round 4).
+    const uint64_t cb_auto = g.waves > (uint32_t)kEngWaves8 ? 4 * std::max<uint64_t>(1, blocks / 20480)
+                                                            : 4 * ((blocks + 16383) / 16384);
+    const uint32_t cb = cb_fixed ? cb_fixed : (uint32_t)std::min<uint64_t>(16, cb_auto);
     const uint32_t half[kWords] = {
         (uint32_t)(uint64_t)base, (uint32_t)((uint64_t)base >> 32), (uint32_t)(uint64_t)offs,
         (uint32_t)((uint64_t)offs >> 32), (uint32_t)(uint64_t)sizes, (uint32_t)((uint64_t)sizes >> 32),

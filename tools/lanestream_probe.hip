@@ -127,6 +127,80 @@ __global__ void __launch_bounds__(768) probe_kernel(const u4* __restrict__ a, si
   if (x == 0x9e3779b9u) out[blockIdx.x] = x;
 }
 
+// Span shape (round 6, session 2): each lane owns a CONTIGUOUS 64-B span of
+// the wave's 4 KiB unit (lane-strided 16-B loads: each instruction touches the
+// unit's 64 lines, the four together read them whole), the next unit's loads
+// in flight while a unit computes.  The compute is the span design's for short
+// log records: CHAINS sequential word chains per lane (16 / CHAINS dependent
+// 4-lookup steps each, a reset/mask select per word), and, with SCAN, a
+// 6-level cross-lane carry scan per unit (one 4-lookup operator and a
+// shuffle per level) -- the cost of giving each record crossing a span its
+// carry-in.  No CRC is checked: timing only.
+__device__ __forceinline__ unsigned wstep(unsigned c, unsigned w, unsigned lo) {
+  const unsigned x = c ^ w;
+  const unsigned a0 = __builtin_amdgcn_perm(x, lo, 0x0c020400u);
+  const unsigned a1 = __builtin_amdgcn_perm(x, lo | 128u, 0x0c020500u);
+  const unsigned a2 = __builtin_amdgcn_perm(x, lo | 0x10000u, 0x0c020600u);
+  const unsigned a3 = __builtin_amdgcn_perm(x, lo | 0x10080u, 0x0c020700u);
+  return lds32(a0) ^ lds32(a1) ^ lds32(a2) ^ lds32(a3);
+}
+template <bool NT, int CHAINS, bool SCAN>
+__global__ void __launch_bounds__(768) span_kernel(const u4* __restrict__ a, size_t n16, unsigned* out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  for (unsigned i = threadIdx.x * 16; i < 131072; i += blockDim.x * 16)
+    *reinterpret_cast<__attribute__((address_space(3))) u4*>(i) = u4{i, i * 3u, i * 5u, i * 7u};
+  __syncthreads();
+  const size_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const size_t gw = (size_t)blockIdx.x * nw + wave, tw = (size_t)gridDim.x * nw;
+  const unsigned lo = (unsigned)(lane & 31) << 2;
+  const size_t units = n16 / 256;
+  unsigned acc = 0, ev = (unsigned)lane * 0x9e3779b9u;
+  size_t u = gw;
+  if (u >= units) return;
+  const u4* p = a + u * 256 + lane * 4;
+  u4 x0 = ld<NT>(p), x1 = ld<NT>(p + 1), x2 = ld<NT>(p + 2), x3 = ld<NT>(p + 3);
+  for (; u < units; u += tw) {
+    const u4 y0 = x0, y1 = x1, y2 = x2, y3 = x3;
+    if (u + tw < units) {
+      const u4* q = a + (u + tw) * 256 + lane * 4;
+      x0 = ld<NT>(q), x1 = ld<NT>(q + 1), x2 = ld<NT>(q + 2), x3 = ld<NT>(q + 3);
+    }
+    const unsigned w[16] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w,
+                            y2.x, y2.y, y2.z, y2.w, y3.x, y3.y, y3.z, y3.w};
+    unsigned c[CHAINS];
+#pragma unroll
+    for (int k = 0; k < CHAINS; k++) c[k] = 0;
+    constexpr int L = 16 / CHAINS;
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+#pragma unroll
+      for (int k = 0; k < CHAINS; k++) {
+        // per-word events: a reset (record start) and a keep mask, as selects
+        const unsigned bit = (ev >> ((k * L + i) & 31)) & 1u;
+        const unsigned wm = bit ? (w[k * L + i] & 0xffff0000u) : w[k * L + i];
+        const unsigned cin = bit ? 0xffffffffu : c[k];
+        acc ^= bit ? c[k] : 0u;  // the ended record's state
+        c[k] = wstep(cin, wm, lo);
+      }
+    }
+    unsigned v = c[0];
+#pragma unroll
+    for (int k = 1; k < CHAINS; k++) v = wstep(v, c[k], lo);
+    if constexpr (SCAN) {
+#pragma unroll
+      for (int lvl = 0; lvl < 6; lvl++) {
+        const int d = 1 << lvl;
+        const unsigned o = __shfl_up(v, d);
+        const unsigned sh = wstep(o, 0u, lo);
+        v = ((int)lane >= d && !(ev & (1u << lvl))) ? (v ^ sh) : v;
+      }
+    }
+    acc ^= v;
+    ev = ev * 1664525u + 1013904223u;
+  }
+  if (acc == 0x9e3779b9u) out[blockIdx.x] = acc;
+}
+
 int main(int argc, char** argv) {
   const size_t bytes = 4ull << 30, n16 = bytes / 16;
   u4* a = nullptr;
@@ -156,7 +230,35 @@ int main(int argc, char** argv) {
            shape, run_b, waves, nt, comp, best, gbs, gbs / 8000.0);
     fflush(stdout);
   };
-  if (argc > 1 && std::string(argv[1]) == "depth") {
+  auto run_span = [&](auto kern, int waves, int nt, int chains, int scan) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    float best = 1e9f;
+    for (int it = 0; it < 6; it++) {
+      (void)hipEventRecord(e0, 0);
+      hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * waves), 131072, 0, a, n16, out);
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (it > 0 && ms < best) best = ms;
+    }
+    const double gbs = (double)bytes / (best * 1e-3) / 1e9;
+    printf("{\"shape\": \"span64\", \"waves\": %d, \"nt\": %d, \"chains\": %d, \"scan\": %d, "
+           "\"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n", waves, nt, chains, scan, best, gbs, gbs / 8000.0);
+    fflush(stdout);
+  };
+  if (argc > 1 && std::string(argv[1]) == "span") {
+    for (int waves : {8, 12}) {
+      run_span(span_kernel<false, 1, false>, waves, 0, 1, 0);
+      run_span(span_kernel<true, 1, false>, waves, 1, 1, 0);
+      run_span(span_kernel<false, 2, false>, waves, 0, 2, 0);
+      run_span(span_kernel<false, 4, false>, waves, 0, 4, 0);
+      run_span(span_kernel<false, 2, true>, waves, 0, 2, 1);
+      run_span(span_kernel<false, 4, true>, waves, 0, 4, 1);
+      run_span(span_kernel<true, 4, true>, waves, 1, 4, 1);
+    }
+    run(probe_kernel<true, false>, 64, 8192, 12, 1, 0);  // coalesced reference
+  } else if (argc > 1 && std::string(argv[1]) == "depth") {
     // two lanes per stream, default policy, 8 KiB per lane: issue work per
     // step (K) against steps of loads in flight (DEPTH)
     for (int waves : {8, 12}) {
