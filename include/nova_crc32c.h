@@ -222,8 +222,10 @@ int nova_sst_engine_set_idle_us(uint32_t us);
  * (written by the host through the PCIe BAR; NOVA_SST_ENGINE_RING=host keeps
  * it in pinned host memory); requests whose completion words the host wrote
  * after the instance that took them ended without finishing them (a "lost"
- * exit or a worker error; their ring slots would never free otherwise). */
-#define NOVA_ENGINE_COUNTERS 24
+ * exit or a worker error; their ring slots would never free otherwise); the
+ * waves per CU its instances launch with (NOVA_SST_ENGINE_WAVES, default 12;
+ * 0 before the engine's first use). */
+#define NOVA_ENGINE_COUNTERS 25
 int nova_sst_engine_counters(uint64_t* out, size_t n);
 /* Time slice of an engine instance in us, from the next instance (0: back to
  * NOVA_SST_ENGINE_SLICE_US, default 20000; 0xFFFFFFFF: none).  An instance

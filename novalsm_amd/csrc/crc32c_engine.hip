@@ -1828,7 +1828,7 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
       gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
       (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice], gp->launch_ns_max / 1000,
       gp->launch_slow, gp->gap_ticks_max / 100, gp->sleep_waits, (uint64_t)gp->max_spinners,
-      (uint64_t)gp->in_dev, gp->host_done};
+      (uint64_t)gp->in_dev, gp->host_done, (uint64_t)gp->waves};
   for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
   return 0;
 }

@@ -479,13 +479,13 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
                                           "taken_back", "unsafe", "yield_waits", "yield_bumps", "broken",
                                           "backing_off", "exits_slice", "launch_us_max", "launch_slow",
                                           "poll_gap_us_max", "sleep_waits", "max_spinners",
-                                          "ring_device", "host_marked_done"};
+                                          "ring_device", "host_marked_done", "waves"};
   for (int i = 0; i < NOVA_ENGINE_COUNTERS; i++) {
     if (i == 3 || i == 14 || i == 15) continue;  // states, not counts
     char b[64];
-    // launch_us_max, poll_gap_us_max, max_spinners, ring_device: not counts
+    // launch_us_max, poll_gap_us_max, max_spinners, ring_device, waves: not counts
     snprintf(b, sizeof b, "%s\"%s\": %llu", eng.size() > 1 ? ", " : "", cn[i],
-             (unsigned long long)(i == 17 || i == 19 || i == 21 || i == 22 ? c1[i] : c1[i] - c0[i]));
+             (unsigned long long)(i == 17 || i == 19 || i == 21 || i == 22 || i == 24 ? c1[i] : c1[i] - c0[i]));
     eng += b;
   }
   eng += "}";

@@ -536,3 +536,36 @@ def test_engine_empty_and_single_block_requests(torch_gpu, oracle, engine_on):
         nb.zero_()
         C.queue_verify_blocks(img, offs, ln_t, okv, nb)
         assert okv.cpu().numpy().tolist() == [1] * len(lens) and int(nb.item()) == 0, lens
+
+
+def test_engine_one_pass_build_in_child():
+    """The default engine is the 12-wave build (a block's loads in two passes,
+    DESIGN.md 3.5g "Round 6"); NOVA_SST_ENGINE_WAVES <= 8 selects the round-5
+    one-pass build.  A child process (the variable is read once per process)
+    runs both ops at 1 and 4 callers on that build through the native caller
+    harness, which checks every call's flags and the final trailers against
+    the oracle: all verified, nothing fell back, launched at 8 waves."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import json\n"
+        "from novalsm_amd import callers\n"
+        "out = []\n"
+        "for op in ('verify', 'trailers'):\n"
+        "    for t in (1, 4):\n"
+        "        r = callers.run(op, t, 1024, 0.2, 'engine', warm_s=0.05, seed=21 + t)\n"
+        "        out.append({'op': op, 't': t, 'verified': r['verified'], 'calls': r['calls'],\n"
+        "                    'fallbacks': r['engine']['fallbacks'], 'launches': r['engine']['launches'],\n"
+        "                    'waves': r['engine']['waves']})\n"
+        "print(json.dumps(out))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NOVA_SST_ENGINE_WAVES="8", PYTHONPATH=root)
+    p = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=100)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    for r in res:
+        assert r["verified"] and r["fallbacks"] == 0 and r["calls"] > 0 and r["launches"] >= 1, r
+        assert r["waves"] == 8, r
+    assert C.engine_counters()["waves"] in (0, 12)  # this process: the default build
