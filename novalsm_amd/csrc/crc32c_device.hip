@@ -175,16 +175,19 @@ __global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint
                                                        uint32_t keymode) {
   __shared__ uint32_t cnt[kLogSortBins];
   __shared__ uint16_t kk[kLogSortWin];  // keymode > 0: every record's key, for the stable ranks
+  // blockDim.x threads (64-256, log_sort_threads) take win / blockDim.x records each
+  const uint32_t nt = blockDim.x;
   const uint64_t w0 = (uint64_t)blockIdx.x * win;
-  for (uint32_t b = threadIdx.x; b < kLogSortBins; b += blockDim.x) cnt[b] = 0;
+  for (uint32_t b = threadIdx.x; b < kLogSortBins; b += nt) cnt[b] = 0;
   __syncthreads();
-  constexpr int kPer = kLogSortWin / 256;
+  constexpr int kPer = kLogSortWin / 64;
   uint32_t key[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
-    const uint64_t i = w0 + threadIdx.x + 256u * k;
+    const uint32_t j = threadIdx.x + nt * k;
+    const uint64_t i = w0 + j;
     key[k] = 0;
-    if (threadIdx.x + 256u * k < win && i < n) {
+    if (j < win && i < n) {
       const uint64_t o = offs[i];
       const uint64_t be = log_block_end(o, buf_len);
       uint64_t e = i + 1 < n ? offs[i + 1] : be;
@@ -197,23 +200,44 @@ __global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint
       key[k] = S < kLogSortBins ? (uint32_t)S : kLogSortBins - 1;
       if (keymode >= 2) key[k] >>= keymode - 1;
       atomicAdd(&cnt[key[k]], 1u);
-      if (keymode) kk[threadIdx.x + 256u * k] = (uint16_t)key[k];
+      if (keymode) kk[j] = (uint16_t)key[k];
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // exclusive prefix in descending key order
-    uint32_t run = 0;
-    for (int b = kLogSortBins - 1; b >= 0; b--) {
-      const uint32_t c = cnt[b];
-      cnt[b] = run;
-      run += c;
+  // Exclusive prefix in descending key order, by wave 0: lane l sums the
+  // reversed bins [5l, 5l + 5) (320 >= kLogSortBins), one wave scan of those
+  // sums, then it writes its five bins' starts.  (One thread walking the 288
+  // bins was half the kernel's time: tools/logsort_probe.hip,
+  // profiles/r06_logsort_probe.log.)
+  static_assert(5 * 64 >= kLogSortBins, "five bins per lane");
+  if (threadIdx.x < 64) {
+    const uint32_t l = threadIdx.x;
+    uint32_t c[5], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      const int r = (int)(5 * l) + q;
+      c[q] = r < (int)kLogSortBins ? cnt[kLogSortBins - 1 - r] : 0u;
+      sum += c[q];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(incl, d);
+      if ((int)l >= d) incl += o;
+    }
+    uint32_t run = incl - sum;
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      const int r = (int)(5 * l) + q;
+      if (r < (int)kLogSortBins) cnt[kLogSortBins - 1 - r] = run;
+      run += c[q];
     }
   }
   __syncthreads();
   if (keymode) {  // stable: rank = the bin's start + earlier records of the same key
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
-      const uint32_t j = threadIdx.x + 256u * k;
+      const uint32_t j = threadIdx.x + nt * k;
       const uint64_t i = w0 + j;
       if (j < win && i < n) {
         uint32_t r = cnt[key[k]];
@@ -225,8 +249,9 @@ __global__ void __launch_bounds__(256) log_sort_kernel(uint64_t base, const uint
   }
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
-    const uint64_t i = w0 + threadIdx.x + 256u * k;
-    if (threadIdx.x + 256u * k < win && i < n) perm[w0 + atomicAdd(&cnt[key[k]], 1u)] = (uint32_t)i;
+    const uint32_t j = threadIdx.x + nt * k;
+    const uint64_t i = w0 + j;
+    if (j < win && i < n) perm[w0 + atomicAdd(&cnt[key[k]], 1u)] = (uint32_t)i;
   }
 }
 
@@ -759,6 +784,18 @@ constexpr uint64_t kTrailerTwoPassMin = 1u << 18;  // blocks: the trailer writer
 // image; measured over payloads U[1,512] .. U[1,16384] B the best window spanned
 // 0.25-1 MiB, and a fixed 512 records lost up to 15 points on large records
 // (profiles/r03_logsort_sweep6.log).
+// Threads per log_sort_kernel workgroup: a quarter of the window, 64 to 256
+// (one wave takes four records per lane of a 256-record window).
+// tools/logsort_probe.hip on 2M records in 8K windows: 36.6-36.9 us with 256
+// threads and one thread's prefix, 28.7-29.1 with 64 threads, 16.9-17.2 with
+// the wave's prefix, 13.1-13.3 with both (profiles/r06_logsort_probe.log); in
+// the log4k verify line 30.8 -> 14.2 us.  (log_unperm_kernel at 64 threads
+// measured the same 7.2-7.4 us and keeps 256.)
+uint32_t log_sort_threads(uint32_t win) {
+  const uint32_t t = win / 4;
+  return t < 64 ? 64u : (t > 256 ? 256u : t);
+}
+
 uint32_t log_sort_window(uint64_t n, uint64_t bytes) {
   const uint64_t avg = n && bytes / n ? bytes / n : 1;
   const uint64_t w = (512u * 1024u) / avg;
@@ -977,7 +1014,7 @@ int run(int mode, CrcParams& p, bool uniform, uint64_t bytes_per_block, hipStrea
     uint8_t* st_pos = reinterpret_cast<uint8_t*>(mode == kLogWrite ? crc_pos + n : perm + n);
     const uint64_t wgs = (n + win - 1) / win;
     const int km = g_diag ? g_tune_logkey.load() : 0;
-    hipLaunchKernelGGL(log_sort_kernel, dim3(wgs), dim3(256), 0, stream, (uint64_t)p.base, p.offsets, n,
+    hipLaunchKernelGGL(log_sort_kernel, dim3(wgs), dim3(log_sort_threads(win)), 0, stream, (uint64_t)p.base, p.offsets, n,
                        (uint64_t)p.buf_len, 16u * (uint32_t)G, win, perm, (uint32_t)(km >= 0 && km <= 3 ? km : 0));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
