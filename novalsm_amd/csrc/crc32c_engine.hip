@@ -115,9 +115,10 @@ constexpr int kEngG = 16;         // lanes per block (units kernel: G = 16)
 // Launch bound: 12 waves per CU, two passes of kEK12 swaths per 4 KiB block
 // (157 VGPRs).  Round 4's 12-wave build kept the one-pass loads (kEK) and
 // spilled; the 8-wave one-pass build (211 VGPRs) stays for
-// NOVA_SST_ENGINE_WAVES <= 8.  Round 6, same boxes (profiles/r06_engine_waves.log):
-// verify at 16 callers 4.55-4.68 -> 5.12-5.28 TB/s, 8 callers 4.33-4.35 ->
-// 4.60-4.70; trailers 4.35-4.43 -> 4.72-4.82 / 4.24 -> 4.39-4.47.
+// NOVA_SST_ENGINE_WAVES <= 8.  Round 6 (profiles/r06_engine_waves.log, with
+// the chunk rule retuned for it in engine_submit: r06_engine_cb12.log): verify
+// at 16 callers 4.55-4.68 -> 5.27-5.36 TB/s, 8 callers 4.33-4.35 -> 4.91-5.04;
+// trailers 4.35-4.43 -> 4.73-4.85 / 4.24 -> 4.78-4.83.
 constexpr int kEngMaxWaves = 12;
 constexpr int kEngWaves8 = 8;
 constexpr int kEngWaves = 12;
