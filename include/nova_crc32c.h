@@ -224,8 +224,10 @@ int nova_sst_engine_set_idle_us(uint32_t us);
  * after the instance that took them ended without finishing them (a "lost"
  * exit or a worker error; their ring slots would never free otherwise); the
  * waves per CU its instances launch with (NOVA_SST_ENGINE_WAVES, default 12;
- * 0 before the engine's first use). */
-#define NOVA_ENGINE_COUNTERS 25
+ * 0 before the engine's first use); requests declined during a yield storm
+ * (instances exiting for other launches of the library over 5000 times a
+ * second: the plain call ran, not counted as fallbacks). */
+#define NOVA_ENGINE_COUNTERS 26
 int nova_sst_engine_counters(uint64_t* out, size_t n);
 /* Time slice of an engine instance in us, from the next instance (0: back to
  * NOVA_SST_ENGINE_SLICE_US, default 20000; 0xFFFFFFFF: none).  An instance

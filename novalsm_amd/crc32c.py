@@ -470,7 +470,7 @@ ENGINE_COUNTERS = ("requests", "launches", "fallbacks", "running", "exits_idle",
                    "exits_stop", "exits_lost", "timeouts", "errors", "taken_back", "unsafe",
                    "yield_waits", "yield_bumps", "broken", "backing_off", "exits_slice", "launch_us_max",
                    "launch_slow", "poll_gap_us_max", "sleep_waits", "max_spinners",
-                   "ring_device", "host_marked_done", "waves")
+                   "ring_device", "host_marked_done", "waves", "storm_declined")
 
 
 def engine_counters() -> dict:

@@ -1041,6 +1041,9 @@ int spinner_budget() {
 // engine_submit's result when the request could not be taken back: the
 // caller must NOT run the plain call (the engine may still write the outputs)
 constexpr int kEngineUnsafe = -1000;
+constexpr int kEngineDeclined = -1001;  // a yield storm: the plain call, nothing was published
+constexpr uint64_t kStormExitsPerS = 5000;  // plain calls back to back: ~7900 yield exits / s; one per 200 us: ~2600
+constexpr int64_t kStormWindowNs = 2000000, kStormHoldNs = 20000000;
 // ring-full wait before the request goes to the plain call (nothing published yet)
 constexpr uint64_t kRingWaitMs = 1000;
 
@@ -1126,6 +1129,15 @@ struct Engine {
   std::atomic<bool> live{false};
   std::mutex ymu;
   uint64_t ygen = 0;
+  // Yield storms: plain launches of the library arriving back to back make
+  // every instance exit after a few requests (1.19 TB/s for 8 engine callers
+  // against ~2.4 for the same callers' direct calls: profiles/r06_engine_mixed_gaps.log).
+  // Over windows of at least 2 ms, more than kStormExitsPerS instance exits
+  // for yields a second route the requests of the next 20 ms to the plain
+  // path (declined, not failed).  Instance exits, not plain launches, are
+  // counted: plain calls while no instance runs cost the engine nothing.
+  int64_t storm_t0_ns = 0, storm_until_ns = 0;  // under mu
+  uint64_t storm_x0 = 0, storm_declined = 0;     // under mu
   std::unordered_map<uint64_t, hipEvent_t> yev;
   // trace (nova_sst_engine_set_trace): per-request spans, summed under tmu
   uint64_t* htrace = nullptr;  // pinned, kRing x kTrWords
@@ -1612,6 +1624,21 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
     const auto t_held = Clock::now();
     lc.lock_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_held - t_lock).count();
     if (g.broken) return NOVA_E_NODEV;
+    {  // yield storm: decline (the caller runs the plain call) until it is over
+      const int64_t now = (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              Clock::now().time_since_epoch()).count();
+      if (now - g.storm_t0_ns >= kStormWindowNs) {
+        const uint64_t x = g.exits[kWhyYield];
+        if (g.storm_t0_ns && (x - g.storm_x0) * 1000000000ull > kStormExitsPerS * (uint64_t)(now - g.storm_t0_ns))
+          g.storm_until_ns = now + kStormHoldNs;
+        g.storm_t0_ns = now;
+        g.storm_x0 = x;
+      }
+      if (now < g.storm_until_ns) {
+        g.storm_declined++;
+        return kEngineDeclined;
+      }
+    }
     int dev = 0;
     (void)hipGetDevice(&dev);
     if ((err = g.init_locked(dev))) return err;
@@ -1764,6 +1791,7 @@ int engine_submit(int mode, const uint8_t* base, const uint64_t* offs, const uin
 }
 
 bool engine_unsafe(int rc) { return rc == kEngineUnsafe; }
+bool engine_declined(int rc) { return rc == kEngineDeclined; }
 
 std::atomic<int> g_engine_override{-1};  // nova_sst_engine_set_enabled (-1: NOVA_SST_ENGINE)
 
@@ -1829,7 +1857,7 @@ int nova_sst_engine_counters(uint64_t* out, size_t n) {
       gp->timeouts, gp->errors, gp->taken_back, gp->unsafe, gp->yield_waits, gp->ygen,
       (uint64_t)gp->broken, (uint64_t)gp->backing_off(), gp->exits[kWhySlice], gp->launch_ns_max / 1000,
       gp->launch_slow, gp->gap_ticks_max / 100, gp->sleep_waits, (uint64_t)gp->max_spinners,
-      (uint64_t)gp->in_dev, gp->host_done, (uint64_t)gp->waves};
+      (uint64_t)gp->in_dev, gp->host_done, (uint64_t)gp->waves, gp->storm_declined};
   for (size_t i = 0; i < n && i < NOVA_ENGINE_COUNTERS; i++) out[i] = v[i];
   return 0;
 }

@@ -42,6 +42,13 @@
 
 #include "crc32c_internal.hpp"
 
+namespace nova_dev {
+// engine_submit's code for a request declined during a yield storm
+// (crc32c_engine.hip): nothing was published, the caller runs the plain call,
+// and it is not counted as a fallback.
+bool engine_declined(int rc);
+}  // namespace nova_dev
+
 namespace {
 
 using namespace nova_dev;
@@ -303,9 +310,11 @@ int enqueue(Req& r, hipStream_t stream) {
     if (erc == 0) return 0;
     // the engine may still write this request's outputs: no plain call
     if (engine_unsafe(erc)) return NOVA_E_NODEV;
-    engine_count_fallback();
-    if (r.mode == kVerify && r.bad && (e = hipMemsetAsync(r.bad, 0, sizeof(uint32_t), stream)) != hipSuccess)
-      return (int)e;
+    if (!engine_declined(erc)) {  // (declined in a yield storm: the engine never saw the request)
+      engine_count_fallback();
+      if (r.mode == kVerify && r.bad && (e = hipMemsetAsync(r.bad, 0, sizeof(uint32_t), stream)) != hipSuccess)
+        return (int)e;
+    }
     plain = true;
   }
   if (plain) {

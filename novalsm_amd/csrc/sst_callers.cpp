@@ -479,7 +479,7 @@ int nova_callers_run(const nova_callers_cfg* cfg, char* json, size_t cap) {
                                           "taken_back", "unsafe", "yield_waits", "yield_bumps", "broken",
                                           "backing_off", "exits_slice", "launch_us_max", "launch_slow",
                                           "poll_gap_us_max", "sleep_waits", "max_spinners",
-                                          "ring_device", "host_marked_done", "waves"};
+                                          "ring_device", "host_marked_done", "waves", "storm_declined"};
   for (int i = 0; i < NOVA_ENGINE_COUNTERS; i++) {
     if (i == 3 || i == 14 || i == 15) continue;  // states, not counts
     char b[64];

@@ -108,7 +108,8 @@ def test_engine_mixed_callers(torch_gpu, oracle, engine_on, op):
     """8 native threads hammer nova_sst_queue_* on their
     own 4096-block tables for 1 s while a 9th thread issues plain
     nova_sstable_verify_blocks, nova_log_verify_records and nova_crc32c_batch
-    calls back to back on its own stream.  Every engine call's result and every
+    calls on its own stream, one every 0.5 ms (below the yield-storm rate; back
+    to back: test_engine_yield_storm_goes_plain).  Every engine call's result and every
     plain call's result is exact (sst_callers.cpp checks them natively against
     expectations taken from the oracle), nothing falls back or times out, the
     engine yields to the plain calls (its instances exit for them), and the
@@ -116,18 +117,53 @@ def test_engine_mixed_callers(torch_gpu, oracle, engine_on, op):
     (the requests the engine had taken, its exit, and the plain call itself)."""
     from novalsm_amd import callers
     plain, keep = _plain_inputs(torch_gpu, oracle)
+    plain.gap_us = 500.0
     r = callers.run(op, 8, 4096, 1.0, "engine", warm_s=0.3, seed=3, plain=plain)
     print(json.dumps(r))
     assert r["verified"] and r["wrong_results"] == 0 and r["rc"] == 0, r
     e, pl = r["engine"], r["plain"]
     assert e["fallbacks"] == 0 and e["timeouts"] == 0 and e["errors"] == 0 and e["unsafe"] == 0, e
-    assert e["exits_yield"] >= 1, e
+    assert e["exits_yield"] >= 1 and e["storm_declined"] == 0, e
     for name, s in pl.items():
         assert s["wrong"] == 0, (name, s)
         assert s["calls"] >= 10, (name, s)
         assert s["max_us"] <= 2000.0, (name, s)
     assert r["calls_in_window"] >= 1000, r  # the engine callers kept going
     del keep
+
+
+def test_engine_yield_storm_goes_plain(torch_gpu, oracle, engine_on):
+    """Plain calls back to back (~7900 instance exits for yields a second) made
+    every engine instance exit after a few requests: 8 engine callers fell to ~1.2 TB/s,
+    half of what their direct calls reach.  In such a storm the engine
+    declines requests for 20 ms at a time and the callers run the plain call
+    (storm_declined counts them; they are not fallbacks).  Every result exact,
+    nothing failed, the plain calls' latency bounded as with yields."""
+    from novalsm_amd import callers
+    plain, keep = _plain_inputs(torch_gpu, oracle)
+    plain.gap_us = 0.0
+    r = callers.run("verify", 8, 4096, 1.0, "engine", warm_s=0.3, seed=4, plain=plain)
+    print(json.dumps(r))
+    assert r["verified"] and r["wrong_results"] == 0 and r["rc"] == 0, r
+    e, pl = r["engine"], r["plain"]
+    assert e["fallbacks"] == 0 and e["timeouts"] == 0 and e["errors"] == 0 and e["unsafe"] == 0, e
+    assert e["storm_declined"] >= 1, e
+    for name, s in pl.items():
+        assert s["wrong"] == 0 and s["calls"] >= 10 and s["max_us"] <= 2000.0, (name, s)
+    assert r["calls_in_window"] >= 1000, r
+    del keep
+    # the storm is over once the plain calls stop: the next requests run on the engine
+    time.sleep(0.05)
+    c0 = C.engine_counters()
+    tb = _sst_table(torch_gpu, oracle, 256, 91, victims=(17,))
+    ok = torch_gpu.empty(tb["n"], dtype=torch_gpu.uint8, device="cuda")
+    nb = torch_gpu.zeros(1, dtype=torch_gpu.int32, device="cuda")
+    torch_gpu.cuda.synchronize()
+    for _ in range(3):
+        C.queue_verify_blocks(tb["img"], tb["offs"], tb["lens"], ok, nb)
+    c1 = C.engine_counters()
+    assert np.array_equal(ok.cpu().numpy(), tb["want"])
+    assert c1["requests"] - c0["requests"] >= 1 and c1["fallbacks"] == c0["fallbacks"], (c0, c1)
 
 
 def test_engine_yields_to_a_plain_call(torch_gpu, oracle, engine_on):
